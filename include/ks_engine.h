@@ -1,0 +1,146 @@
+/*
+ * ks_engine.h — C-ABI of the MI355X-native kubesim scheduling engine.
+ *
+ * This is the boundary a kubesim host binds (cgo / ctypes / JNI).
+ * Plain C types only: caller-owned host buffers are copied in, outputs go to
+ * caller-allocated buffers with explicit lengths, device state is owned by the opaque
+ * handle.  A handle is single-threaded (not re-entrant), like the reference's
+ * single-goroutine Run loop (kubesim/kubesim.go:101-122).
+ *
+ * What each entry point replaces in the reference (wangchen615/kubernetes-simulator):
+ *   ks_create / ks_load_nodes ... NewKubeSim node construction (kubesim/kubesim.go:32-61,
+ *                                 kubesim/config/config.go:44-90, kubesim/node/node.go:22-27)
+ *   ks_submit_pods .............. submit + podQueue.append (kubesim/kubesim.go:126-139,
+ *                                 kubesim/podqueue.go:18-23); api.Submitter output
+ *                                 (api/submitter.go:15) with its arrival tick
+ *   ks_step ..................... Run's tick loop + scheduleOne (kubesim/kubesim.go:90-166):
+ *                                 Filter (:168-188), Score + argmax (:190-225),
+ *                                 Node.CreatePod (kubesim/node/node.go:36-60)
+ *   ks_filter ................... api.Filter.Filter for every node (api/scheduler.go:19)
+ *   ks_score .................... api.Scorer.Score aggregated over the registered scorers
+ *                                 (api/scheduler.go:36, kubesim/kubesim.go:193-206)
+ *   ks_usage .................... Σ Pod.ResourceUsage(clock) per node (kubesim/pod/pod.go:47-63)
+ *   ks_last_error ............... the error text Run would return
+ *
+ * Status codes map 1:1 onto the reference's error kinds (strongerrors):
+ *   KS_EINVAL    InvalidArgument (bad names, bad simSpec, bad quantities, bad config)
+ *   KS_ENOTFOUND NotFound — no node selected; the run stops exactly as kubesim.go:217-220
+ *   KS_EDEVICE   HIP / RCCL failure (no reference counterpart)
+ * After KS_ENOTFOUND or a bind-time KS_EINVAL the run is aborted: later ks_step calls return
+ * the same code, as Run would have returned.
+ *
+ * Units: cpu, memory and nvidia.com/gpu quantities are int64 milli-units (exact for every
+ * resource.Quantity that is a whole number of milli-units); the pods capacity is
+ * Capacity.Pods().Value() (a count; absent ⇒ 0).  An absent cpu / memory / gpu capacity key
+ * is -1.  All inputs must be non-negative and below 2^59.
+ */
+#ifndef KS_ENGINE_H
+#define KS_ENGINE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KS_ABI_VERSION 1
+
+typedef enum {
+    KS_OK = 0,
+    KS_EINVAL = 1,
+    KS_ENOTFOUND = 2,
+    KS_EDEVICE = 3,
+    KS_ENOMEM = 4,
+} ks_status;
+
+/* filter_mode: the reference discards the Filter result (kubesim/kubesim.go:182) —
+ * REFERENCE_LITERAL reproduces that; FEEDS_SCORE lets the filters gate the candidates. */
+enum { KS_FILTER_REFERENCE_LITERAL = 0, KS_FILTER_FEEDS_SCORE = 1 };
+/* filters (bitmask) */
+enum { KS_FILTER_FIT = 1, KS_FILTER_TAINT = 2, KS_FILTER_SELECTOR = 4 };
+/* scorers: CONST returns `value` for every node (examples/main.go:147-155 with value 1);
+ * LEAST_REQUESTED / BALANCED are the integer forms of SURVEY.md §8(a14). */
+enum { KS_SCORER_CONST = 0, KS_SCORER_LEAST_REQUESTED = 1, KS_SCORER_BALANCED = 2 };
+/* bind status (kubesim/pod/pod.go:20-27) */
+enum { KS_POD_OK = 0, KS_POD_OVER_CAPACITY = 1 };
+/* per-pod flags: the pod will fail at bind with InvalidArgument
+ * (empty namespace/name: kubesim/node/node.go:133-143; bad simSpec: kubesim/pod/pod.go:31-39) */
+enum { KS_PODFLAG_BAD_KEY = 1, KS_PODFLAG_BAD_SPEC = 2 };
+
+typedef struct {
+    int32_t kind;   /* KS_SCORER_* */
+    int32_t weight; /* >= 0 */
+    int32_t value;  /* CONST only */
+} ks_scorer;
+
+typedef struct {
+    int32_t abi_version;  /* KS_ABI_VERSION */
+    int32_t tick_seconds; /* config `tick` (kubesim/kubesim.go:239), >= 1 */
+    int32_t filter_mode;  /* KS_FILTER_REFERENCE_LITERAL / KS_FILTER_FEEDS_SCORE */
+    uint32_t filters;     /* KS_FILTER_* bits */
+    int32_t n_scorers;    /* 0..8; registration order */
+    ks_scorer scorers[8];
+    int32_t device;       /* HIP device ordinal */
+    int32_t batch_pods;   /* pods resolved per scan (0 = default) */
+    int32_t reserved[8];
+} ks_config;
+
+typedef struct {
+    int64_t pod;    /* FIFO index (submission order) */
+    int32_t node;   /* node index (ks_load_nodes order) */
+    int32_t status; /* KS_POD_* */
+    int64_t tick;   /* bind tick (clock = start + tick * tick_seconds) */
+} ks_bind;
+
+typedef struct ks_engine ks_engine;
+
+ks_status ks_create(const ks_config* cfg, ks_engine** out);
+void ks_destroy(ks_engine* eng);
+
+/* Load the cluster (once).  alloc[n][4] = {cpu, memory, nvidia.com/gpu, pods};
+ * taint[n] = OR of dictionary bits of the node's NoSchedule/NoExecute taints;
+ * label[n] = OR of dictionary bits of its (key,value) labels (W = 1). */
+ks_status ks_load_nodes(ks_engine* eng, int64_t n, const int64_t* alloc, const uint64_t* taint,
+                        const uint64_t* label);
+
+/* Append m pods to the FIFO.  arrival_tick = the tick whose Submit call returned the pod
+ * (non-decreasing; <= the current tick means "next tick").  req[m][3] container-summed
+ * requests with keymask (1 cpu, 2 memory, 4 gpu); tol = dictionary taints tolerated; sel =
+ * dictionary labels required (bit 63 = impossible); simSpec as CSR: phase_off[m+1],
+ * phase_sec[Φ] (int32), phase_use[Φ][3]; flags = KS_PODFLAG_* (may be NULL). */
+ks_status ks_submit_pods(ks_engine* eng, int64_t m, const int64_t* arrival_tick,
+                         const int64_t* req, const uint8_t* keymask, const uint64_t* tol,
+                         const uint64_t* sel, const int32_t* phase_off, const int32_t* phase_sec,
+                         const int64_t* phase_use, const uint8_t* flags);
+
+/* Advance `ticks` ticks.  Writes up to `cap` binds to out (one per tick that had a queued
+ * pod) and the number of binds made to *n_out. */
+ks_status ks_step(ks_engine* eng, int64_t ticks, ks_bind* out, int64_t cap, int64_t* n_out);
+
+/* Filter mask (all enabled filters) / aggregated score (-1 = no entry) of queued pod `pod`
+ * against the cluster state at the current tick.  mask_out[n], score_out[n]. */
+ks_status ks_filter(ks_engine* eng, int64_t pod, uint8_t* mask_out);
+ks_status ks_score(ks_engine* eng, int64_t pod, int64_t* score_out);
+
+/* usage_out[n][3]: Σ over pods on each node of ResourceUsage at the current tick. */
+ks_status ks_usage(ks_engine* eng, int64_t* usage_out);
+
+int64_t ks_current_tick(const ks_engine* eng);
+int64_t ks_queued_pods(const ks_engine* eng);
+const char* ks_last_error(const ks_engine* eng);
+
+/* Timing of the last ks_step on the engine's stream (HIP events): total device ms and the
+ * summed scan / resolve kernel ms, number of scan+resolve launches. */
+typedef struct {
+    double step_ms;
+    double scan_ms;
+    double resolve_ms;
+    int64_t launches;
+    int64_t pods;
+} ks_step_stats;
+ks_status ks_last_step_stats(const ks_engine* eng, ks_step_stats* out);
+void ks_set_profiling(ks_engine* eng, int enable);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

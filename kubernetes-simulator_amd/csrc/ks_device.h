@@ -1,0 +1,192 @@
+// ks_device.h — device-side records and the fused Filter + Score evaluator (gfx950).
+//
+// One (pod, node) evaluation = the reference's Filter loop (kubesim/kubesim.go:168-188) and
+// score aggregation (:190-206) collapsed into one integer expression:
+//   * resource fit   == Node.CreatePod's admission test (kubesim/node/node.go:44-47)
+//   * taint          == every NoSchedule/NoExecute taint tolerated (toleration.go:37-56),
+//                       pre-reduced on the host to (node_taint & ~pod_tol) == 0
+//   * node selector  == (node_label & pod_sel) == pod_sel
+//   * scores         == const / LeastRequested / BalancedAllocation, integer-exact
+// and returns total+1 (0 = not a candidate), so the argmax key
+//   key = (total+1) << 32 | (0xFFFFFFFF - node)
+// is maximal for the highest total and, among ties, the lowest node index.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ks {
+
+constexpr int kWave = 64;
+
+enum : uint32_t { kFilterFit = 1, kFilterTaint = 2, kFilterSelector = 4 };
+
+// Launch-uniform configuration (kernel argument, lives in SGPRs).
+struct Cfg {
+    int32_t n_nodes;       // real nodes; indices >= n_nodes are padding
+    int32_t nwb;           // wave-blocks of 64 nodes (padded node count / 64)
+    int32_t filter_feeds;  // 1: filters gate the candidate set
+    uint32_t filters;      // kFilter* bits (only used when filter_feeds)
+    int32_t has_scorers;   // 0: nodeScore stays empty ⇒ NotFound
+    int32_t w_lr;          // summed weight of LeastRequested scorers
+    int32_t w_ba;          // summed weight of BalancedAllocation scorers
+    int32_t const_total;   // Σ weight*value over constant scorers
+    int32_t tick_seconds;
+    int32_t pad_;
+};
+
+// Pod record, 48 B, read with scalar loads (uniform per pod).
+struct alignas(16) PodRec {
+    int64_t req[3];    // milli cpu, milli memory, milli gpu (absent ⇒ 0)
+    uint64_t tol;      // dictionary taints this pod tolerates
+    uint64_t sel;      // dictionary labels this pod requires
+    uint32_t keymask;  // request keys present: 1 cpu, 2 memory, 4 gpu
+    uint32_t flags;    // KS_PODFLAG_*
+};
+static_assert(sizeof(PodRec) == 48, "PodRec layout");
+
+// Node state: 80 B per node, stored struct-of-arrays in HBM.
+struct NodeSoA {
+    int64_t* ac;   // alloc cpu (milli; -1 absent)
+    int64_t* am;   // alloc memory
+    int64_t* ag;   // alloc gpu
+    int64_t* ap;   // Capacity.Pods().Value()
+    int64_t* rc;   // requested cpu of running pods
+    int64_t* rm;
+    int64_t* rg;
+    int64_t* nr;   // running pods
+    uint64_t* taint;
+    uint64_t* label;
+};
+
+struct NodeV {
+    int64_t ac, am, ag, ap, rc, rm, rg, nr;
+    uint64_t taint, label;
+};
+
+__device__ __forceinline__ NodeV load_node(const NodeSoA& s, int64_t i) {
+    NodeV v;
+    v.ac = s.ac[i]; v.am = s.am[i]; v.ag = s.ag[i]; v.ap = s.ap[i];
+    v.rc = s.rc[i]; v.rm = s.rm[i]; v.rg = s.rg[i]; v.nr = s.nr[i];
+    v.taint = s.taint[i]; v.label = s.label[i];
+    return v;
+}
+
+// Admission / resource-fit (kubesim/node/node.go:44-47).  Keys requested only by running
+// pods cannot fail: they passed admission against the same static capacity and requests are
+// non-negative.  An absent capacity key is -1, so any request of that
+// key — including 0 — fails, as resourceListGE does (kubesim/node/resource.go:54-55).
+__device__ __forceinline__ bool fits(const PodRec& p, const NodeV& n) {
+    bool ok = n.nr < n.ap;
+    if (p.keymask & 1) ok &= n.rc + p.req[0] <= n.ac;
+    if (p.keymask & 2) ok &= n.rm + p.req[1] <= n.am;
+    if (p.keymask & 4) ok &= n.rg + p.req[2] <= n.ag;
+    return ok;
+}
+
+// floor(y / a) for 0 <= y <= 10*a (restoring division, 4 steps, no hardware divide).
+template <typename T>
+__device__ __forceinline__ int32_t div_upto10(T y, T a) {
+    int32_t q = 0;
+    if (y >= (a << 3)) { q = 8; y -= (a << 3); }
+    if (y >= (a << 2)) { q += 4; y -= (a << 2); }
+    if (y >= (a << 1)) { q += 2; y -= (a << 1); }
+    if (y >= a) q += 1;
+    return q;
+}
+
+// LeastRequested per resource: (A - u) * 10 / A, 0 if A <= 0 or u > A.
+__device__ __forceinline__ int32_t lr_one(int64_t A, int64_t u) {
+    if (A <= 0 || u > A) return 0;
+    return div_upto10<int64_t>((A - u) * 10, A);
+}
+
+// BalancedAllocation, exact: floor(10 * (1 - |uc/Ac - um/Am|)), 0 if a fraction >= 1.
+__device__ __forceinline__ int32_t ba_score(int64_t Ac, int64_t Am, int64_t uc, int64_t um) {
+    if (Ac <= 0 || Am <= 0 || uc >= Ac || um >= Am) return 0;
+    typedef unsigned __int128 u128;
+    u128 D = (u128)(uint64_t)Ac * (uint64_t)Am;
+    u128 a = (u128)(uint64_t)uc * (uint64_t)Am;
+    u128 b = (u128)(uint64_t)um * (uint64_t)Ac;
+    u128 X = a > b ? a - b : b - a;
+    return div_upto10<u128>((D - X) * 10, D);
+}
+
+// Fused Filter + Score.  Returns weighted total + 1, or 0 when the node is not a candidate.
+__device__ __forceinline__ uint32_t eval_total1(const Cfg& c, const PodRec& p, const NodeV& n) {
+    if (!c.has_scorers) return 0;
+    if (c.filter_feeds) {
+        bool ok = true;
+        if (c.filters & kFilterFit) ok &= fits(p, n);
+        if (c.filters & kFilterTaint) ok &= (n.taint & ~p.tol) == 0;
+        if (c.filters & kFilterSelector) ok &= (n.label & p.sel) == p.sel;
+        if (!ok) return 0;
+    }
+    int64_t uc = n.rc + p.req[0];
+    int64_t um = n.rm + p.req[1];
+    int32_t total = c.const_total;
+    if (c.w_lr) total += c.w_lr * ((lr_one(n.ac, uc) + lr_one(n.am, um)) >> 1);
+    if (c.w_ba) total += c.w_ba * ba_score(n.ac, n.am, uc, um);
+    return (uint32_t)total + 1u;
+}
+
+__device__ __forceinline__ uint64_t make_key(uint32_t total1, uint32_t node) {
+    return total1 ? (((uint64_t)total1 << 32) | (uint64_t)(0xFFFFFFFFu - node)) : 0ull;
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        uint32_t w = __shfl_xor(v, o, kWave);
+        v = v > w ? v : w;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        uint64_t w = __shfl_xor(v, o, kWave);
+        v = v > w ? v : w;
+    }
+    return v;
+}
+
+// Best key of a wave's 64 nodes (lane l holds node base + l): the max total and, among
+// ties, the lowest lane — a 32-bit max plus one ballot instead of a 64-bit reduction.
+__device__ __forceinline__ uint64_t wave_best_key(uint32_t total1, uint32_t base) {
+    uint32_t m = wave_max_u32(total1);
+    if (m == 0) return 0ull;
+    uint64_t hit = __ballot(total1 == m);
+    uint32_t lane = (uint32_t)__ffsll((unsigned long long)hit) - 1u;
+    return make_key(m, base + lane);
+}
+
+// Arguments of the batch kernels (expire_head / scan / resolve).
+struct EngineArgs {
+    Cfg c;
+    NodeSoA s;
+    const PodRec* pods;
+    const int32_t* dur;      // ticks a bound-Ok pod runs (0: never counted)
+    const int64_t* exp_off;  // [P+1]: expiries due before pod j binds
+    const int32_t* exp_pod;
+    int32_t* b_node;
+    int32_t* b_status;
+    uint8_t* expired;
+    uint64_t* wbkey;         // [B][nwb]
+    int64_t* ctr;            // start, end, error code, error pod, early stops
+    int32_t B;
+    int32_t PG;              // pods per scan workgroup
+};
+
+// Launchers (defined in ks_kernels.hip).
+hipError_t launch_batch(const EngineArgs& a, hipStream_t st, hipEvent_t e_scan0, hipEvent_t e_scan1,
+                        hipEvent_t e_res1);
+hipError_t launch_eval_pod(const Cfg& c, const NodeSoA& s, const PodRec* pod, uint32_t filters, uint8_t* mask,
+                           int64_t* score, hipStream_t st);
+hipError_t launch_flush(const NodeSoA& s, const PodRec* pods, const int64_t* fin, int64_t t, int64_t n_done,
+                        const int32_t* b_node, const int32_t* b_status, uint8_t* expired, hipStream_t st);
+hipError_t launch_usage(int64_t q_lo, int64_t q_hi, int64_t t, int32_t tick_s, const int32_t* b_node,
+                        const int32_t* b_status, const int64_t* t0, const int32_t* dur, const int32_t* phase_off,
+                        const int32_t* cum_sec, const int64_t* use, unsigned long long* usage, hipStream_t st);
+
+}  // namespace ks

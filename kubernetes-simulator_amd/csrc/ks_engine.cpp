@@ -1,0 +1,543 @@
+// ks_engine.cpp — host side of the C-ABI declared in include/ks_engine.h.
+//
+// Host responsibilities (everything that is independent of placements):
+//  * FIFO + one-pod-per-tick: the bind tick of pod j is max(bind_tick[j-1] + 1, arrival_j)
+//    (kubesim/kubesim.go:105-121 pops at most one pod per tick and always binds it), so bind
+//    ticks are fixed at submit time.
+//  * expiry schedule: a bound-Ok pod q runs while (t - t0) * tick < Σ phase seconds
+//    (kubesim/pod/pod.go:67-69), i.e. for dur = ceil(S / tick) ticks.  Its expiry is attached
+//    to the first later pod whose bind tick reaches t0 + dur; the device applies it (if q was
+//    bound Ok) right before that pod is scheduled.
+//  * batching: launches (expire_head, scan, resolve) triples until the device counter says
+//    every pod due in [tick+1, tick+ticks] is bound, then copies the binds back.
+// Placements themselves are decided on the device only.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <queue>
+#include <string>
+#include <vector>
+
+#include "../../include/ks_engine.h"
+#include "ks_device.h"
+
+
+namespace {
+
+constexpr int64_t kMaxNodes = 16384LL * 64;  // one resolver launch covers <= 16384 wave-blocks
+constexpr int64_t kMaxValue = 1LL << 59;
+constexpr int kMaxBatch = 512;
+constexpr int kDefaultBatch = 256;
+constexpr int64_t kNever = std::numeric_limits<int64_t>::max();
+
+// Growable device array (stream-ordered copies on growth).
+template <typename T>
+struct DVec {
+    T* p = nullptr;
+    int64_t n = 0, cap = 0;
+    hipError_t reserve(int64_t want, hipStream_t st) {
+        if (want <= cap) return hipSuccess;
+        int64_t nc = std::max<int64_t>(want, std::max<int64_t>(cap * 2, 1024));
+        T* q = nullptr;
+        hipError_t e = hipMalloc(&q, sizeof(T) * nc);
+        if (e != hipSuccess) return e;
+        if (n) {
+            e = hipMemcpyAsync(q, p, sizeof(T) * n, hipMemcpyDeviceToDevice, st);
+            if (e != hipSuccess) return e;
+            e = hipStreamSynchronize(st);
+            if (e != hipSuccess) return e;
+        }
+        if (p) (void)hipFree(p);
+        p = q;
+        cap = nc;
+        return hipSuccess;
+    }
+    hipError_t append(const T* h, int64_t k, hipStream_t st) {
+        hipError_t e = reserve(n + k, st);
+        if (e != hipSuccess) return e;
+        if (k) e = hipMemcpyAsync(p + n, h, sizeof(T) * k, hipMemcpyHostToDevice, st);
+        n += k;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = cap = 0;
+    }
+};
+
+}  // namespace
+
+struct ks_engine {
+    ks_config cfg{};
+    ks::Cfg dc{};
+    hipStream_t st = nullptr;
+    int device = 0;
+    bool profiling = false;
+
+    // nodes
+    int64_t n = 0, n_pad = 0;
+    int nwb = 0;
+    bool nodes_loaded = false;
+    void* node_mem = nullptr;
+    ks::NodeSoA s{};
+
+    // pods (device)
+    DVec<ks::PodRec> pods;
+    DVec<int32_t> dur, b_node, b_status, phase_off, cum_sec, exp_pod;
+    DVec<int64_t> exp_off, t0, fin, use;
+    DVec<uint8_t> expired;
+    // pods (host mirror of placement-independent facts)
+    std::vector<int64_t> h_bind_tick, h_fin;
+    std::vector<int64_t> h_exp_off{0};
+    std::vector<int32_t> h_dur;
+    std::priority_queue<std::pair<int64_t, int64_t>, std::vector<std::pair<int64_t, int64_t>>,
+                        std::greater<std::pair<int64_t, int64_t>>>
+        pending;  // (finish tick, pod) not yet attached to a later pod
+    int64_t P = 0, F = 0;
+    int64_t last_arrival = 0;
+
+    // progress
+    int64_t tick = 0, done = 0, usage_lo = 0;
+    int err = KS_OK;
+    std::string errmsg;
+
+    // batch machinery
+    int B = kDefaultBatch, PG = 32;
+    uint64_t* wbkey = nullptr;
+    int64_t* d_ctr = nullptr;
+    int64_t* h_ctr = nullptr;  // pinned
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    std::vector<hipEvent_t> prof_ev;
+    ks_step_stats stats{};
+
+    // scratch for queries
+    uint8_t* d_mask = nullptr;
+    int64_t* d_score = nullptr;
+    unsigned long long* d_usage = nullptr;
+};
+
+namespace {
+
+ks_status fail(ks_engine* e, ks_status code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (e) e->errmsg = buf;
+    return code;
+}
+
+#define HIPCHK(e, expr)                                                                     \
+    do {                                                                                    \
+        hipError_t _r = (expr);                                                             \
+        if (_r != hipSuccess)                                                               \
+            return fail((e), KS_EDEVICE, "%s failed: %s", #expr, hipGetErrorString(_r));    \
+    } while (0)
+
+ks::EngineArgs make_args(ks_engine* e) {
+    ks::EngineArgs a{};
+    a.c = e->dc;
+    a.s = e->s;
+    a.pods = e->pods.p;
+    a.dur = e->dur.p;
+    a.exp_off = e->exp_off.p;
+    a.exp_pod = e->exp_pod.p;
+    a.b_node = e->b_node.p;
+    a.b_status = e->b_status.p;
+    a.expired = e->expired.p;
+    a.wbkey = e->wbkey;
+    a.ctr = e->d_ctr;
+    a.B = e->B;
+    a.PG = e->PG;
+    return a;
+}
+
+}  // namespace
+
+extern "C" {
+
+ks_status ks_create(const ks_config* cfg, ks_engine** out) {
+    if (!cfg || !out) return KS_EINVAL;
+    *out = nullptr;
+    if (cfg->abi_version != KS_ABI_VERSION) return KS_EINVAL;
+    if (cfg->tick_seconds < 1) return KS_EINVAL;
+    if (cfg->filter_mode != KS_FILTER_REFERENCE_LITERAL && cfg->filter_mode != KS_FILTER_FEEDS_SCORE)
+        return KS_EINVAL;
+    if (cfg->filters & ~7u) return KS_EINVAL;
+    if (cfg->n_scorers < 0 || cfg->n_scorers > 8) return KS_EINVAL;
+    if (cfg->batch_pods < 0 || cfg->batch_pods > kMaxBatch) return KS_EINVAL;
+    int64_t const_total = 0, w_lr = 0, w_ba = 0;
+    for (int i = 0; i < cfg->n_scorers; i++) {
+        const ks_scorer& sc = cfg->scorers[i];
+        if (sc.weight < 0) return KS_EINVAL;
+        switch (sc.kind) {
+            case KS_SCORER_CONST:
+                if (sc.value < 0) return KS_EINVAL;
+                const_total += (int64_t)sc.weight * sc.value;
+                break;
+            case KS_SCORER_LEAST_REQUESTED: w_lr += sc.weight; break;
+            case KS_SCORER_BALANCED: w_ba += sc.weight; break;
+            default: return KS_EINVAL;
+        }
+    }
+    if (const_total + 10 * (w_lr + w_ba) >= (1LL << 31) - 2) return KS_EINVAL;  // total + 1 fits u32 keys
+
+    ks_engine* e = new ks_engine();
+    e->cfg = *cfg;
+    e->device = cfg->device;
+    e->B = cfg->batch_pods ? cfg->batch_pods : kDefaultBatch;
+    e->dc.filter_feeds = cfg->filter_mode == KS_FILTER_FEEDS_SCORE;
+    e->dc.filters = cfg->filters;
+    e->dc.has_scorers = cfg->n_scorers > 0;
+    e->dc.w_lr = (int32_t)w_lr;
+    e->dc.w_ba = (int32_t)w_ba;
+    e->dc.const_total = (int32_t)const_total;
+    e->dc.tick_seconds = cfg->tick_seconds;
+    hipError_t r = hipSetDevice(e->device);
+    if (r == hipSuccess) r = hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking);
+    if (r == hipSuccess) r = hipMalloc(&e->d_ctr, 8 * sizeof(int64_t));
+    if (r == hipSuccess) r = hipHostMalloc(&e->h_ctr, 8 * sizeof(int64_t), hipHostMallocDefault);
+    for (int i = 0; i < 4 && r == hipSuccess; i++) r = hipEventCreate(&e->ev[i]);
+    if (r == hipSuccess) r = hipMemsetAsync(e->d_ctr, 0, 8 * sizeof(int64_t), e->st);
+    if (r == hipSuccess) r = hipStreamSynchronize(e->st);
+    if (r != hipSuccess) {
+        delete e;
+        return KS_EDEVICE;
+    }
+    *out = e;
+    return KS_OK;
+}
+
+void ks_destroy(ks_engine* e) {
+    if (!e) return;
+    (void)hipSetDevice(e->device);
+    if (e->st) (void)hipStreamSynchronize(e->st);
+    e->pods.release(); e->dur.release(); e->b_node.release(); e->b_status.release();
+    e->phase_off.release(); e->cum_sec.release(); e->exp_pod.release(); e->exp_off.release();
+    e->t0.release(); e->fin.release(); e->use.release(); e->expired.release();
+    if (e->node_mem) (void)hipFree(e->node_mem);
+    if (e->wbkey) (void)hipFree(e->wbkey);
+    if (e->d_ctr) (void)hipFree(e->d_ctr);
+    if (e->h_ctr) (void)hipHostFree(e->h_ctr);
+    if (e->d_mask) (void)hipFree(e->d_mask);
+    if (e->d_score) (void)hipFree(e->d_score);
+    if (e->d_usage) (void)hipFree(e->d_usage);
+    for (auto ev : e->ev) if (ev) (void)hipEventDestroy(ev);
+    for (auto ev : e->prof_ev) (void)hipEventDestroy(ev);
+    if (e->st) (void)hipStreamDestroy(e->st);
+    delete e;
+}
+
+ks_status ks_load_nodes(ks_engine* e, int64_t n, const int64_t* alloc, const uint64_t* taint, const uint64_t* label) {
+    if (!e) return KS_EINVAL;
+    if (e->nodes_loaded) return fail(e, KS_EINVAL, "nodes already loaded");
+    if (n < 0 || n > kMaxNodes) return fail(e, KS_EINVAL, "node count %lld outside [0, %lld]", (long long)n, (long long)kMaxNodes);
+    if (n && (!alloc || !taint || !label)) return fail(e, KS_EINVAL, "null node buffer");
+    for (int64_t i = 0; i < n; i++) {
+        for (int k = 0; k < 3; k++)
+            if (alloc[i * 4 + k] < -1 || alloc[i * 4 + k] >= kMaxValue)
+                return fail(e, KS_EINVAL, "node %lld: capacity %d out of range", (long long)i, k);
+        if (alloc[i * 4 + 3] < 0 || alloc[i * 4 + 3] >= kMaxValue)
+            return fail(e, KS_EINVAL, "node %lld: pods capacity out of range", (long long)i);
+    }
+    HIPCHK(e, hipSetDevice(e->device));
+    e->n = n;
+    e->n_pad = std::max<int64_t>(64, (n + 63) / 64 * 64);
+    e->nwb = (int)(e->n_pad / 64);
+    const int64_t np = e->n_pad;
+    // host staging in SoA order: ac am ag ap rc rm rg nr taint label
+    std::vector<int64_t> h(10 * np, 0);
+    for (int64_t i = 0; i < np; i++) {
+        const bool real = i < n;
+        for (int k = 0; k < 4; k++) h[k * np + i] = real ? alloc[i * 4 + k] : (k == 3 ? 0 : -1);
+        h[8 * np + i] = real ? (int64_t)taint[i] : 0;
+        h[9 * np + i] = real ? (int64_t)label[i] : 0;
+    }
+    HIPCHK(e, hipMalloc(&e->node_mem, sizeof(int64_t) * 10 * np));
+    HIPCHK(e, hipMemcpyAsync(e->node_mem, h.data(), sizeof(int64_t) * 10 * np, hipMemcpyHostToDevice, e->st));
+    int64_t* b = (int64_t*)e->node_mem;
+    e->s.ac = b; e->s.am = b + np; e->s.ag = b + 2 * np; e->s.ap = b + 3 * np;
+    e->s.rc = b + 4 * np; e->s.rm = b + 5 * np; e->s.rg = b + 6 * np; e->s.nr = b + 7 * np;
+    e->s.taint = (uint64_t*)(b + 8 * np); e->s.label = (uint64_t*)(b + 9 * np);
+    e->dc.n_nodes = (int32_t)n;
+    e->dc.nwb = e->nwb;
+    // pods per scan workgroup: aim for >= ~2048 workgroups (8 per CU) per scan
+    const int64_t wgx = (e->nwb + 3) / 4;
+    int pg = 1;
+    while (pg < e->B && wgx * ((e->B + pg * 2 - 1) / (pg * 2)) >= 2048) pg *= 2;
+    e->PG = pg;
+    HIPCHK(e, hipMalloc(&e->wbkey, sizeof(uint64_t) * (size_t)e->B * e->nwb));
+    HIPCHK(e, hipMalloc(&e->d_mask, std::max<int64_t>(n, 1)));
+    HIPCHK(e, hipMalloc(&e->d_score, sizeof(int64_t) * std::max<int64_t>(n, 1)));
+    HIPCHK(e, hipMalloc(&e->d_usage, sizeof(unsigned long long) * 3 * std::max<int64_t>(n, 1)));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    e->nodes_loaded = true;
+    return KS_OK;
+}
+
+ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const int64_t* req, const uint8_t* keymask,
+                         const uint64_t* tol, const uint64_t* sel, const int32_t* phase_off, const int32_t* phase_sec,
+                         const int64_t* phase_use, const uint8_t* flags) {
+    if (!e) return KS_EINVAL;
+    if (!e->nodes_loaded) return fail(e, KS_EINVAL, "ks_load_nodes must precede ks_submit_pods");
+    if (m < 0) return fail(e, KS_EINVAL, "negative pod count");
+    if (m == 0) return KS_OK;
+    if (!arrival || !req || !keymask || !tol || !sel || !phase_off) return fail(e, KS_EINVAL, "null pod buffer");
+    if (e->P + m >= (1LL << 31)) return fail(e, KS_EINVAL, "too many pods");
+    if (phase_off[0] != 0) return fail(e, KS_EINVAL, "phase_off[0] must be 0");
+    const int64_t nf = phase_off[m];
+    if (nf && (!phase_sec || !phase_use)) return fail(e, KS_EINVAL, "null phase buffer");
+    // validate first, mutate after
+    int64_t last = e->last_arrival;
+    for (int64_t i = 0; i < m; i++) {
+        if (arrival[i] < last) return fail(e, KS_EINVAL, "arrival ticks must be non-decreasing (pod %lld)", (long long)(e->P + i));
+        last = arrival[i];
+        if (phase_off[i + 1] < phase_off[i]) return fail(e, KS_EINVAL, "phase_off must be non-decreasing");
+        for (int k = 0; k < 3; k++)
+            if (req[i * 3 + k] < 0 || req[i * 3 + k] >= kMaxValue)
+                return fail(e, KS_EINVAL, "pod %lld: request out of range", (long long)(e->P + i));
+    }
+    for (int64_t f = 0; f < nf * 3; f++)
+        if (phase_use[f] < 0 || phase_use[f] >= kMaxValue) return fail(e, KS_EINVAL, "usage out of range");
+
+    std::vector<ks::PodRec> recs(m);
+    std::vector<int32_t> dur(m), poff(m), cum(nf);
+    std::vector<int64_t> t0(m), fin(m), eoff(m);
+    std::vector<int32_t> epod;
+    epod.reserve(m);
+    int64_t prev_bind = e->P ? e->h_bind_tick[e->P - 1] : e->tick;
+    for (int64_t i = 0; i < m; i++) {
+        const int64_t j = e->P + i;
+        ks::PodRec& r = recs[i];
+        const uint8_t km = keymask[i] & 7;
+        for (int k = 0; k < 3; k++) r.req[k] = (km >> k & 1) ? req[i * 3 + k] : 0;
+        r.tol = tol[i];
+        r.sel = sel[i];
+        r.keymask = km;
+        r.flags = flags ? flags[i] : 0;
+        const int64_t arr = std::max<int64_t>(arrival[i], e->tick + 1);
+        const int64_t bt = std::max<int64_t>(prev_bind + 1, arr);
+        prev_bind = bt;
+        uint32_t acc = 0;  // int32 wrapping, kubesim/pod/pod.go:155-162
+        for (int32_t f = phase_off[i]; f < phase_off[i + 1]; f++) {
+            acc += (uint32_t)phase_sec[f];
+            cum[f] = (int32_t)acc;
+        }
+        const int32_t S = (int32_t)acc;
+        const int64_t d = S > 0 ? ((int64_t)S + e->cfg.tick_seconds - 1) / e->cfg.tick_seconds : 0;
+        dur[i] = (int32_t)d;
+        t0[i] = bt;
+        fin[i] = d > 0 ? bt + d : kNever;
+        poff[i] = (int32_t)(e->F + phase_off[i]);
+        // expiries due before pod j binds: finish tick in (bind_tick[j-1], bind_tick[j]]
+        while (!e->pending.empty() && e->pending.top().first <= bt) {
+            epod.push_back((int32_t)e->pending.top().second);
+            e->pending.pop();
+        }
+        eoff[i] = e->h_exp_off.back() + (int64_t)epod.size();
+        if (d > 0) e->pending.push({fin[i], j});
+    }
+    // device uploads
+    hipStream_t st = e->st;
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, e->pods.append(recs.data(), m, st));
+    HIPCHK(e, e->dur.append(dur.data(), m, st));
+    HIPCHK(e, e->t0.append(t0.data(), m, st));
+    HIPCHK(e, e->fin.append(fin.data(), m, st));
+    std::vector<int32_t> neg(m, -1);
+    HIPCHK(e, e->b_node.append(neg.data(), m, st));
+    HIPCHK(e, e->b_status.append(neg.data(), m, st));
+    std::vector<uint8_t> zero(m, 0);
+    HIPCHK(e, e->expired.append(zero.data(), m, st));
+    // phase_off holds P+1 entries: overwrite the trailing sentinel
+    if (e->phase_off.n) e->phase_off.n -= 1;
+    HIPCHK(e, e->phase_off.append(poff.data(), m, st));
+    const int32_t tail = (int32_t)(e->F + nf);
+    HIPCHK(e, e->phase_off.append(&tail, 1, st));
+    HIPCHK(e, e->cum_sec.append(cum.data(), nf, st));
+    HIPCHK(e, e->use.append(phase_use, nf * 3, st));
+    if (e->exp_off.n == 0) {
+        const int64_t z = 0;
+        HIPCHK(e, e->exp_off.append(&z, 1, st));
+    }
+    HIPCHK(e, e->exp_off.append(eoff.data(), m, st));
+    HIPCHK(e, e->exp_pod.append(epod.data(), (int64_t)epod.size(), st));
+    HIPCHK(e, hipStreamSynchronize(st));  // host staging vectors die here
+    e->h_bind_tick.insert(e->h_bind_tick.end(), t0.begin(), t0.end());
+    e->h_fin.insert(e->h_fin.end(), fin.begin(), fin.end());
+    e->h_dur.insert(e->h_dur.end(), dur.begin(), dur.end());
+    e->h_exp_off.insert(e->h_exp_off.end(), eoff.begin(), eoff.end());
+    e->P += m;
+    e->F += nf;
+    e->last_arrival = last;
+    return KS_OK;
+}
+
+ks_status ks_step(ks_engine* e, int64_t ticks, ks_bind* out, int64_t cap, int64_t* n_out) {
+    if (!e || !n_out || ticks < 0) return KS_EINVAL;
+    *n_out = 0;
+    if (e->err) return (ks_status)e->err;
+    if (!e->nodes_loaded) return fail(e, KS_EINVAL, "no nodes loaded");
+    HIPCHK(e, hipSetDevice(e->device));
+    const int64_t t_end = e->tick + ticks;
+    // pods whose bind tick falls in (tick, t_end]
+    const int64_t p_hi = std::upper_bound(e->h_bind_tick.begin() + e->done, e->h_bind_tick.end(), t_end) -
+                         e->h_bind_tick.begin();
+    e->stats = ks_step_stats{};
+    if (p_hi <= e->done) {
+        e->tick = t_end;
+        return KS_OK;
+    }
+    hipStream_t st = e->st;
+    e->h_ctr[0] = e->done;
+    e->h_ctr[1] = p_hi;
+    e->h_ctr[2] = 0;
+    e->h_ctr[3] = -1;
+    e->h_ctr[4] = 0;
+    HIPCHK(e, hipMemcpyAsync(e->d_ctr, e->h_ctr, 5 * sizeof(int64_t), hipMemcpyHostToDevice, st));
+    HIPCHK(e, hipEventRecord(e->ev[0], st));
+    const ks::EngineArgs a = make_args(e);
+    int64_t start = e->done;
+    int64_t launches = 0;
+    double scan_ms = 0, res_ms = 0;
+    while (true) {
+        const int64_t nbat = (p_hi - start + e->B - 1) / e->B;
+        for (int64_t b = 0; b < nbat; b++) {
+            hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
+            if (e->profiling) {
+                while ((int64_t)e->prof_ev.size() < 3 * (launches + 1)) {
+                    hipEvent_t ev;
+                    HIPCHK(e, hipEventCreate(&ev));
+                    e->prof_ev.push_back(ev);
+                }
+                e0 = e->prof_ev[3 * launches];
+                e1 = e->prof_ev[3 * launches + 1];
+                e2 = e->prof_ev[3 * launches + 2];
+            }
+            HIPCHK(e, ks::launch_batch(a, st, e0, e1, e2));
+            launches++;
+        }
+        HIPCHK(e, hipMemcpyAsync(e->h_ctr, e->d_ctr, 5 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(e, hipStreamSynchronize(st));
+        start = e->h_ctr[0];
+        if (e->h_ctr[2] != 0 || start >= p_hi) break;
+    }
+    HIPCHK(e, hipEventRecord(e->ev[1], st));
+    const int64_t new_done = start;
+    const int64_t nb = new_done - e->done;
+    std::vector<int32_t> node(nb), status(nb);
+    if (nb) {
+        HIPCHK(e, hipMemcpyAsync(node.data(), e->b_node.p + e->done, sizeof(int32_t) * nb, hipMemcpyDeviceToHost, st));
+        HIPCHK(e, hipMemcpyAsync(status.data(), e->b_status.p + e->done, sizeof(int32_t) * nb, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(e, hipStreamSynchronize(st));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e->ev[0], e->ev[1]);
+    if (e->profiling) {
+        for (int64_t l = 0; l < launches; l++) {
+            float a1 = 0, a2 = 0;
+            (void)hipEventElapsedTime(&a1, e->prof_ev[3 * l], e->prof_ev[3 * l + 1]);
+            (void)hipEventElapsedTime(&a2, e->prof_ev[3 * l + 1], e->prof_ev[3 * l + 2]);
+            scan_ms += a1;
+            res_ms += a2;
+        }
+    }
+    e->stats.step_ms = ms;
+    e->stats.scan_ms = scan_ms;
+    e->stats.resolve_ms = res_ms;
+    e->stats.launches = launches;
+    e->stats.pods = nb;
+    for (int64_t i = 0; i < nb && i < cap; i++) {
+        out[i].pod = e->done + i;
+        out[i].node = node[i];
+        out[i].status = status[i];
+        out[i].tick = e->h_bind_tick[e->done + i];
+    }
+    *n_out = nb;
+    e->done = new_done;
+    if (e->h_ctr[2] != 0) {
+        const int64_t pod = e->h_ctr[3];
+        e->err = (int)e->h_ctr[2];
+        e->tick = e->h_bind_tick[pod];
+        e->done = pod + 1;  // popped from the queue, not bound
+        if (e->err == KS_ENOTFOUND)
+            fail(e, KS_ENOTFOUND, "node \"\" not found (pod %lld, tick %lld)", (long long)pod, (long long)e->tick);
+        else
+            fail(e, KS_EINVAL, "pod %lld: invalid pod key or simSpec (tick %lld)", (long long)pod, (long long)e->tick);
+        return (ks_status)e->err;
+    }
+    e->tick = t_end;
+    return KS_OK;
+}
+
+static ks_status flush_expiries(ks_engine* e) {
+    HIPCHK(e, ks::launch_flush(e->s, e->pods.p, e->fin.p, e->tick, e->done, e->b_node.p, e->b_status.p,
+                               e->expired.p, e->st));
+    return KS_OK;
+}
+
+static ks_status eval_pod(ks_engine* e, int64_t pod) {
+    if (!e->nodes_loaded) return fail(e, KS_EINVAL, "no nodes loaded");
+    if (pod < 0 || pod >= e->P) return fail(e, KS_EINVAL, "pod %lld out of range", (long long)pod);
+    HIPCHK(e, hipSetDevice(e->device));
+    ks_status r = flush_expiries(e);
+    if (r != KS_OK) return r;
+    if (e->n == 0) return KS_OK;
+    HIPCHK(e, ks::launch_eval_pod(e->dc, e->s, e->pods.p + pod, e->cfg.filters, e->d_mask, e->d_score, e->st));
+    return KS_OK;
+}
+
+ks_status ks_filter(ks_engine* e, int64_t pod, uint8_t* mask_out) {
+    if (!e || !mask_out) return KS_EINVAL;
+    ks_status r = eval_pod(e, pod);
+    if (r != KS_OK) return r;
+    if (e->n) HIPCHK(e, hipMemcpyAsync(mask_out, e->d_mask, e->n, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    return KS_OK;
+}
+
+ks_status ks_score(ks_engine* e, int64_t pod, int64_t* score_out) {
+    if (!e || !score_out) return KS_EINVAL;
+    ks_status r = eval_pod(e, pod);
+    if (r != KS_OK) return r;
+    if (e->n)
+        HIPCHK(e, hipMemcpyAsync(score_out, e->d_score, sizeof(int64_t) * e->n, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    return KS_OK;
+}
+
+ks_status ks_usage(ks_engine* e, int64_t* usage_out) {
+    if (!e || !usage_out) return KS_EINVAL;
+    if (!e->nodes_loaded) return fail(e, KS_EINVAL, "no nodes loaded");
+    if (e->n == 0) return KS_OK;
+    HIPCHK(e, hipSetDevice(e->device));
+    while (e->usage_lo < e->done && e->h_fin[e->usage_lo] <= e->tick) e->usage_lo++;
+    HIPCHK(e, hipMemsetAsync(e->d_usage, 0, sizeof(unsigned long long) * 3 * e->n, e->st));
+    HIPCHK(e, ks::launch_usage(e->usage_lo, e->done, e->tick, e->cfg.tick_seconds, e->b_node.p, e->b_status.p,
+                               e->t0.p, e->dur.p, e->phase_off.p, e->cum_sec.p, e->use.p, e->d_usage, e->st));
+    HIPCHK(e, hipMemcpyAsync(usage_out, e->d_usage, sizeof(int64_t) * 3 * e->n, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    return KS_OK;
+}
+
+int64_t ks_current_tick(const ks_engine* e) { return e ? e->tick : -1; }
+int64_t ks_queued_pods(const ks_engine* e) { return e ? e->P - e->done : -1; }
+const char* ks_last_error(const ks_engine* e) { return e ? e->errmsg.c_str() : "null engine"; }
+
+ks_status ks_last_step_stats(const ks_engine* e, ks_step_stats* out) {
+    if (!e || !out) return KS_EINVAL;
+    *out = e->stats;
+    return KS_OK;
+}
+
+void ks_set_profiling(ks_engine* e, int enable) {
+    if (e) e->profiling = enable != 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,85 @@
+"""ctypes binding of the C-ABI in include/ks_engine.h (libks_engine.so, built in-tree).
+
+There is no fallback: if the HIP library is missing or fails to load, importing the engine
+raises.  The CPU oracle under oracle/ is test infrastructure and is never used here.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libks_engine.so")
+
+KS_OK, KS_EINVAL, KS_ENOTFOUND, KS_EDEVICE, KS_ENOMEM = 0, 1, 2, 3, 4
+KS_FILTER_REFERENCE_LITERAL, KS_FILTER_FEEDS_SCORE = 0, 1
+KS_FILTER_FIT, KS_FILTER_TAINT, KS_FILTER_SELECTOR = 1, 2, 4
+KS_SCORER_CONST, KS_SCORER_LEAST_REQUESTED, KS_SCORER_BALANCED = 0, 1, 2
+KS_POD_OK, KS_POD_OVER_CAPACITY = 0, 1
+KS_PODFLAG_BAD_KEY, KS_PODFLAG_BAD_SPEC = 1, 2
+KS_ABI_VERSION = 1
+
+STATUS_NAMES = {KS_OK: "OK", KS_EINVAL: "InvalidArgument", KS_ENOTFOUND: "NotFound",
+                KS_EDEVICE: "DeviceError", KS_ENOMEM: "OutOfMemory"}
+
+# every symbol include/ks_engine.h declares
+EXPORTED_SYMBOLS = ("ks_create", "ks_destroy", "ks_load_nodes", "ks_submit_pods", "ks_step",
+                    "ks_filter", "ks_score", "ks_usage", "ks_current_tick", "ks_queued_pods",
+                    "ks_last_error", "ks_last_step_stats", "ks_set_profiling")
+
+
+class KsScorer(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("weight", C.c_int32), ("value", C.c_int32)]
+
+
+class KsConfig(C.Structure):
+    _fields_ = [("abi_version", C.c_int32), ("tick_seconds", C.c_int32), ("filter_mode", C.c_int32),
+                ("filters", C.c_uint32), ("n_scorers", C.c_int32), ("scorers", KsScorer * 8),
+                ("device", C.c_int32), ("batch_pods", C.c_int32), ("reserved", C.c_int32 * 8)]
+
+
+class KsBind(C.Structure):
+    _fields_ = [("pod", C.c_int64), ("node", C.c_int32), ("status", C.c_int32), ("tick", C.c_int64)]
+
+
+class KsStepStats(C.Structure):
+    _fields_ = [("step_ms", C.c_double), ("scan_ms", C.c_double), ("resolve_ms", C.c_double),
+                ("launches", C.c_int64), ("pods", C.c_int64)]
+
+
+_lib = None
+
+
+def load():
+    """Load libks_engine.so (fails loudly if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc, gfx950)")
+    L = C.CDLL(LIB_PATH)
+    p = C.c_void_p
+    L.ks_create.argtypes = [C.POINTER(KsConfig), C.POINTER(C.c_void_p)]
+    L.ks_create.restype = C.c_int
+    L.ks_destroy.argtypes = [p]
+    L.ks_destroy.restype = None
+    L.ks_load_nodes.argtypes = [p, C.c_int64, p, p, p]
+    L.ks_submit_pods.argtypes = [p, C.c_int64] + [p] * 9
+    L.ks_step.argtypes = [p, C.c_int64, p, C.c_int64, C.POINTER(C.c_int64)]
+    L.ks_filter.argtypes = [p, C.c_int64, p]
+    L.ks_score.argtypes = [p, C.c_int64, p]
+    L.ks_usage.argtypes = [p, p]
+    for f in ("ks_load_nodes", "ks_submit_pods", "ks_step", "ks_filter", "ks_score", "ks_usage"):
+        getattr(L, f).restype = C.c_int
+    L.ks_current_tick.argtypes = [p]
+    L.ks_current_tick.restype = C.c_int64
+    L.ks_queued_pods.argtypes = [p]
+    L.ks_queued_pods.restype = C.c_int64
+    L.ks_last_error.argtypes = [p]
+    L.ks_last_error.restype = C.c_char_p
+    L.ks_last_step_stats.argtypes = [p, C.POINTER(KsStepStats)]
+    L.ks_last_step_stats.restype = C.c_int
+    L.ks_set_profiling.argtypes = [p, C.c_int]
+    L.ks_set_profiling.restype = None
+    _lib = L
+    return L

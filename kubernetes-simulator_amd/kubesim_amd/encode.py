@@ -1,0 +1,137 @@
+"""Host ingest: structured trace → the int64 SoA + bitmask records the C-ABI takes.
+
+This is the host half of the Filter predicates of SURVEY.md §8(a13):
+
+* taints: the distinct ``(key, value, effect)`` triples with effect NoSchedule or
+  NoExecute are dictionary-encoded; a node carries the OR of its taints' bits.
+  PreferNoSchedule never filters, so it gets no bit.  For every pod the host evaluates
+  ``Toleration.ToleratesTaint`` (``vendor/k8s.io/api/core/v1/toleration.go:37-56``) of each
+  of its tolerations against every dictionary taint, once, and ships the OR as ``tol``.
+  The device test is then ``(node_taint & ~tol) == 0``.
+* labels: the distinct ``(key, value)`` node-label pairs are dictionary-encoded; a pod's
+  nodeSelector becomes ``sel``; a selector pair no node carries sets bit 63, which no node
+  ever has, so the pod is infeasible everywhere.  Device test: ``(label & sel) == sel``.
+* capacity: ``alloc[n][4]`` in milli-units for cpu / memory / gpu with ``-1`` for an absent
+  key (absent fails every requested key, ``kubesim/node/resource.go:54-55``), and
+  ``Capacity.Pods().Value()`` (absent ⇒ 0, ``vendor/k8s.io/api/core/v1/resource.go:44-49``).
+* requests: ``req[m][3]`` plus a key-presence mask (``getResourceReq``,
+  ``kubesim/node/resource.go:43-49``).
+
+Inputs must be non-negative; the device's incremental admission relies on it.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .tracegen import (CPU, GPU, MEM, NO_EXECUTE, NO_SCHEDULE, OP_EQUAL, OP_EXISTS, PODS,
+                       EFFECT_NONE)
+
+SEL_IMPOSSIBLE = np.uint64(1) << np.uint64(63)
+MAX_TAINT_BITS = 64
+MAX_LABEL_BITS = 63
+
+
+class EncodeError(ValueError):
+    """Raised for inputs outside the device path's exact domain (maps to KS_EINVAL)."""
+
+
+def _or_reduce_csr(bits: np.ndarray, off: np.ndarray) -> np.ndarray:
+    n = len(off) - 1
+    out = np.zeros(n, dtype=np.uint64)
+    if len(bits) == 0:
+        return out
+    counts = np.diff(off)
+    nz = counts > 0
+    red = np.bitwise_or.reduceat(bits, off[:-1][nz].astype(np.int64))
+    out[nz] = red
+    return out
+
+
+def encode_nodes(nodes: dict):
+    """Return ``(alloc[n][4] i64, taint[n] u64, label[n] u64, taint_dict, label_dict)``."""
+    n = nodes["n"]
+    alloc = nodes["alloc"].astype(np.int64).copy()
+    has = nodes["alloc_has"]
+    if (alloc < 0).any():
+        raise EncodeError("negative capacity is outside the device path's domain")
+    for k, bit in ((CPU, 1), (MEM, 2), (GPU, 4)):
+        alloc[(has & bit) == 0, k] = -1
+    alloc[(has & 8) == 0, PODS] = 0
+
+    t = nodes["taint"]
+    filt = (t[:, 2] == NO_SCHEDULE) | (t[:, 2] == NO_EXECUTE) if len(t) else np.zeros(0, bool)
+    trip = [tuple(r) for r in t[filt]] if len(t) else []
+    taint_dict = sorted(set(trip))
+    if len(taint_dict) > MAX_TAINT_BITS:
+        raise EncodeError(f"{len(taint_dict)} distinct NoSchedule/NoExecute taints > {MAX_TAINT_BITS} (W=1)")
+    tindex = {d: i for i, d in enumerate(taint_dict)}
+    tbits = np.zeros(len(t), dtype=np.uint64)
+    for i in np.nonzero(filt)[0]:
+        tbits[i] = np.uint64(1) << np.uint64(tindex[tuple(t[i])])
+    node_taint = _or_reduce_csr(tbits, nodes["taint_off"])
+
+    lab = nodes["label"]
+    pairs = sorted(set(map(tuple, lab))) if len(lab) else []
+    if len(pairs) > MAX_LABEL_BITS:
+        raise EncodeError(f"{len(pairs)} distinct label pairs > {MAX_LABEL_BITS} (W=1)")
+    lindex = {d: i for i, d in enumerate(pairs)}
+    lbits = np.array([np.uint64(1) << np.uint64(lindex[tuple(r)]) for r in lab], dtype=np.uint64) \
+        if len(lab) else np.zeros(0, dtype=np.uint64)
+    node_label = _or_reduce_csr(lbits, nodes["label_off"])
+    assert n == len(alloc)
+    return alloc, node_taint, node_label, taint_dict, pairs
+
+
+def tolerates(tkey, top, tval, teff, key, val, eff):
+    """Vectorised ``Toleration.ToleratesTaint`` (toleration.go:37-56); id 0 = empty string."""
+    ok = (teff == EFFECT_NONE) | (teff == eff)
+    ok &= (tkey == 0) | (tkey == key)
+    ok &= ((top == OP_EQUAL) & (tval == val)) | (top == OP_EXISTS)
+    return ok
+
+
+def encode_pods(pods: dict, taint_dict, label_dict):
+    """Return the per-pod device records (dict of arrays) for ``ks_submit_pods``."""
+    m = pods["m"]
+    req = pods["req"].astype(np.int64)
+    if (req < 0).any():
+        raise EncodeError("negative request is outside the device path's domain")
+    if (pods["phase_use"] < 0).any():
+        raise EncodeError("negative usage is outside the device path's domain")
+    keymask = pods["req_has"].astype(np.uint8) & 7
+    req = np.where(((keymask[:, None] >> np.arange(3)) & 1) == 1, req, 0)
+
+    tol = pods["tol"]
+    rowbits = np.zeros(len(tol), dtype=np.uint64)
+    if len(tol):
+        for i, (k, v, e) in enumerate(taint_dict):
+            hit = tolerates(tol[:, 0], tol[:, 1], tol[:, 2], tol[:, 3], k, v, e)
+            rowbits |= np.where(hit, np.uint64(1) << np.uint64(i), np.uint64(0))
+    tolmask = _or_reduce_csr(rowbits, pods["tol_off"])
+
+    sel = pods["sel"]
+    sbits = np.zeros(len(sel), dtype=np.uint64)
+    if len(sel):
+        lindex = {d: i for i, d in enumerate(label_dict)}
+        keys = sel[:, 0].astype(np.int64) << 32 | sel[:, 1].astype(np.int64)
+        lut = {(k << 32) | v: i for (k, v), i in lindex.items()}
+        uniq, inv = np.unique(keys, return_inverse=True)
+        ubits = np.array([np.uint64(1) << np.uint64(lut[int(u)]) if int(u) in lut else SEL_IMPOSSIBLE
+                          for u in uniq], dtype=np.uint64)
+        sbits = ubits[inv]
+    selmask = _or_reduce_csr(sbits, pods["sel_off"])
+
+    use = pods["phase_use"].astype(np.int64)
+    phas = pods["phase_has"].astype(np.uint8)
+    use = np.where(((phas[:, None] >> np.arange(3)) & 1) == 1, use, 0)
+    return dict(m=m, arrival=pods["arrival"].astype(np.int64), req=np.ascontiguousarray(req),
+                keymask=keymask, tol=tolmask, sel=selmask,
+                phase_off=pods["phase_off"].astype(np.int32),
+                phase_sec=pods["phase_sec"].astype(np.int32),
+                phase_use=np.ascontiguousarray(use), flags=pods["flags"].astype(np.uint8))
+
+
+def encode_trace(trace: dict):
+    alloc, taint, label, tdict, ldict = encode_nodes(trace["nodes"])
+    pods = encode_pods(trace["pods"], tdict, ldict)
+    return dict(alloc=alloc, taint=taint, label=label, taint_dict=tdict, label_dict=ldict, pods=pods)

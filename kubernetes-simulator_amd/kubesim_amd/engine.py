@@ -1,0 +1,153 @@
+"""Python handle over the C-ABI (include/ks_engine.h): the device scheduling engine.
+
+``Engine`` mirrors the reference's engine surface (kubesim/kubesim.go):
+
+=====================  ==============================================================
+reference              here
+=====================  ==============================================================
+NewKubeSim             ``Engine(tick_seconds, filter_mode, filters, scorers)`` +
+                       ``load_nodes`` (kubesim/kubesim.go:32-61)
+RegisterFilter /       ``filters`` bits / ``scorers`` list, fixed at creation
+RegisterScorer         (kubesim/kubesim.go:78-86); built-in device plugins only
+submit (Submitter)     ``submit`` (kubesim/kubesim.go:126-139)
+Run                    ``step(ticks)`` — advances the tick loop (kubesim/kubesim.go:90-123)
+api.Filter / Scorer    ``filter(pod)`` / ``score(pod)``
+=====================  ==============================================================
+
+Errors come back as :class:`KsError` with the reference's kind (``InvalidArgument`` /
+``NotFound``); binds made before an aborting error are still returned by ``step``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import KsBind, KsConfig, KsStepStats
+
+
+class KsError(RuntimeError):
+    def __init__(self, code: int, msg: str, binds=None):
+        super().__init__(f"{_lib.STATUS_NAMES.get(code, code)}: {msg}")
+        self.code = code
+        self.kind = _lib.STATUS_NAMES.get(code, str(code))
+        self.binds = binds
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _c(a, dt):
+    return np.ascontiguousarray(a, dtype=dt)
+
+
+class Engine:
+    def __init__(self, *, tick_seconds=10, filter_mode=_lib.KS_FILTER_REFERENCE_LITERAL, filters=0,
+                 scorers=((_lib.KS_SCORER_CONST, 1, 1),), device=0, batch_pods=0):
+        L = _lib.load()
+        cfg = KsConfig()
+        cfg.abi_version = _lib.KS_ABI_VERSION
+        cfg.tick_seconds = tick_seconds
+        cfg.filter_mode = filter_mode
+        cfg.filters = filters
+        cfg.n_scorers = len(scorers)
+        for i, (k, w, v) in enumerate(scorers):
+            cfg.scorers[i].kind, cfg.scorers[i].weight, cfg.scorers[i].value = k, w, v
+        cfg.device = device
+        cfg.batch_pods = batch_pods
+        h = C.c_void_p()
+        rc = L.ks_create(C.byref(cfg), C.byref(h))
+        if rc != _lib.KS_OK:
+            raise KsError(rc, "ks_create rejected the configuration")
+        self._L = L
+        self.h = h
+        self.n = 0
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.ks_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, rc, binds=None):
+        if rc != _lib.KS_OK:
+            raise KsError(rc, self._L.ks_last_error(self.h).decode(), binds)
+
+    # -- cluster / queue ---------------------------------------------------------------------
+    def load_nodes(self, alloc, taint, label):
+        alloc = _c(alloc, np.int64).reshape(-1, 4)
+        self.n = len(alloc)
+        self._check(self._L.ks_load_nodes(self.h, self.n, _p(alloc), _p(_c(taint, np.uint64)),
+                                          _p(_c(label, np.uint64))))
+
+    def submit(self, pods: dict):
+        """Append encoded pods (see kubesim_amd.encode.encode_pods)."""
+        m = pods["m"]
+        arrs = [_c(pods["arrival"], np.int64), _c(pods["req"], np.int64).reshape(-1, 3),
+                _c(pods["keymask"], np.uint8), _c(pods["tol"], np.uint64), _c(pods["sel"], np.uint64),
+                _c(pods["phase_off"], np.int32), _c(pods["phase_sec"], np.int32),
+                _c(pods["phase_use"], np.int64).reshape(-1, 3), _c(pods["flags"], np.uint8)]
+        self._check(self._L.ks_submit_pods(self.h, m, *[_p(a) for a in arrs]))
+
+    # -- tick loop ---------------------------------------------------------------------------
+    def step(self, ticks: int, cap: int | None = None):
+        """Advance ``ticks`` ticks; returns binds as a structured numpy array
+        (pod, node, status, tick)."""
+        cap = ticks if cap is None else cap
+        out = (KsBind * max(cap, 1))()
+        n = C.c_int64(0)
+        rc = self._L.ks_step(self.h, ticks, out, cap, C.byref(n))
+        k = min(n.value, cap)
+        arr = np.frombuffer(out, dtype=np.dtype([("pod", "<i8"), ("node", "<i4"), ("status", "<i4"),
+                                                 ("tick", "<i8")]), count=k).copy()
+        self._check(rc, arr)
+        return arr
+
+    def filter(self, pod: int):
+        mask = np.zeros(self.n, np.uint8)
+        self._check(self._L.ks_filter(self.h, pod, _p(mask)))
+        return mask
+
+    def score(self, pod: int):
+        score = np.zeros(self.n, np.int64)
+        self._check(self._L.ks_score(self.h, pod, _p(score)))
+        return score
+
+    def usage(self):
+        out = np.zeros((self.n, 3), np.int64)
+        self._check(self._L.ks_usage(self.h, _p(out)))
+        return out
+
+    @property
+    def tick(self):
+        return self._L.ks_current_tick(self.h)
+
+    @property
+    def queued(self):
+        return self._L.ks_queued_pods(self.h)
+
+    def last_step_stats(self):
+        s = KsStepStats()
+        self._L.ks_last_step_stats(self.h, C.byref(s))
+        return dict(step_ms=s.step_ms, scan_ms=s.scan_ms, resolve_ms=s.resolve_ms, launches=s.launches,
+                    pods=s.pods)
+
+    def set_profiling(self, on: bool):
+        self._L.ks_set_profiling(self.h, 1 if on else 0)
+
+
+def engine_for_trace(trace, enc, **cfg):
+    """Create an Engine loaded with an encoded trace's nodes."""
+    eng = Engine(tick_seconds=trace["tick_seconds"], **cfg)
+    eng.load_nodes(enc["alloc"], enc["taint"], enc["label"])
+    return eng

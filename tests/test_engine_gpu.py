@@ -1,0 +1,104 @@
+"""GPU parity: the HIP engine (through the C-ABI) vs the CPU oracle, bit for bit.
+
+Placements, bind order, bind ticks, bind status and per-tick node usage must be identical
+(integer work: no tolerance).  Sizes are small enough for the oracle to finish in seconds;
+full-size configs are covered by size-independent invariants in test_engine_gpu_large.py.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from harness import (MODES, assert_same_binds, encoded, engine_run, make_engine, make_oracle,
+                     oracle_run, small_trace)
+from kubesim_amd import tracegen
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _lockstep(trace, mode, ticks, batch_pods=0, usage_every=1, chunk=1):
+    enc = encoded(trace)
+    eng = make_engine(trace, enc, mode, batch_pods)
+    eng.submit(enc["pods"])
+    ora = make_oracle(trace, mode)
+    ora.submit(trace)
+    t = 0
+    while t < ticks:
+        k = min(chunk, ticks - t)
+        eb, erc = engine_run(eng, k, k)
+        ob, orc = oracle_run(ora, k)
+        assert_same_binds(eb, ob)
+        assert erc == orc, (t, erc, orc, eng.tick, ora.tick)
+        t += k
+        if erc:
+            break
+        if usage_every and (t // chunk) % usage_every == 0:
+            np.testing.assert_array_equal(eng.usage(), ora.usage(), err_msg=f"usage at tick {t}")
+    return eng, ora
+
+
+def test_c1_kat():
+    """config/sample.yml + examples/main.go: even pods Ok on node-0, odd OverCapacity."""
+    with open(os.path.join(GOLDEN, "c1_kat.json")) as f:
+        kat = json.load(f)
+    tr = tracegen.c1_trace(kat["ticks"])
+    enc = encoded(tr)
+    eng = make_engine(tr, enc, "literal_const")
+    eng.submit(enc["pods"])
+    for t, exp in enumerate(kat["binds"], start=1):
+        b = eng.step(1)
+        assert [(int(x["pod"]), int(x["node"]), int(x["tick"]), int(x["status"])) for x in b] == [tuple(exp)]
+        np.testing.assert_array_equal(eng.usage(), np.array(kat["usage"][t - 1], dtype=np.int64))
+
+
+@pytest.mark.parametrize("mode", sorted(MODES))
+@pytest.mark.parametrize("seed", [1, 2])
+def test_lockstep_small(mode, seed):
+    tr = small_trace(seed, n_nodes=40, n_pods=160, arrival="stream")
+    _lockstep(tr, mode, 400)
+
+
+@pytest.mark.parametrize("batch", [1, 3, 64, 256, 512])
+@pytest.mark.parametrize("mode", ["literal_lrba_filters_ignored", "feeds_all_lrba"])
+def test_batched_vs_oracle(mode, batch):
+    tr = small_trace(7, n_nodes=300, n_pods=2500, taints=False, selectors=False)
+    enc = encoded(tr)
+    eng = make_engine(tr, enc, mode, batch)
+    eng.submit(enc["pods"])
+    ora = make_oracle(tr, mode)
+    ora.submit(tr)
+    for chunk in (1, 17, 500, 2000):
+        eb, erc = engine_run(eng, chunk, chunk)
+        ob, orc = oracle_run(ora, chunk)
+        assert_same_binds(eb, ob)
+        assert erc == orc
+        np.testing.assert_array_equal(eng.usage(), ora.usage())
+
+
+def test_short_pods_many_expiries():
+    """Durations of 1-3 ticks: every pod expires inside its own batch; exercises the
+    in-batch expiry path and the cache budget (early commits)."""
+    tr = small_trace(11, n_nodes=2000, n_pods=6000, taints=False, selectors=False, tolerations=False)
+    p = tr["pods"]
+    p["phase_sec"][:] = 1 + (np.arange(len(p["phase_sec"])) % 12)
+    _lockstep(tr, "feeds_all_lrba", 6000, batch_pods=512, chunk=1500)
+
+
+def test_filter_score_match_oracle():
+    tr = small_trace(5, n_nodes=64, n_pods=300)
+    mode = "feeds_all_lrba"
+    enc = encoded(tr)
+    eng = make_engine(tr, enc, mode)
+    eng.submit(enc["pods"])
+    ora = make_oracle(tr, mode)
+    ora.submit(tr)
+    for ticks in (0, 13, 40):
+        engine_run(eng, ticks, ticks) if ticks else None
+        oracle_run(ora, ticks) if ticks else None
+        done = tr["pods"]["m"] - eng.queued
+        for pod in (done, done + 1, done + 7):
+            feas, score = ora.eval(pod)
+            np.testing.assert_array_equal(eng.filter(pod), feas)
+            np.testing.assert_array_equal(eng.score(pod), score)
