@@ -75,7 +75,7 @@ __device__ __forceinline__ NodeV load_node(const NodeSoA& s, int64_t i) {
 // pods cannot fail: they passed admission against the same static capacity and requests are
 // non-negative.  An absent capacity key is -1, so any request of that
 // key — including 0 — fails, as resourceListGE does (kubesim/node/resource.go:54-55).
-__device__ __forceinline__ bool fits(const PodRec& p, const NodeV& n) {
+__host__ __device__ __forceinline__ bool fits(const PodRec& p, const NodeV& n) {
     bool ok = n.nr < n.ap;
     if (p.keymask & 1) ok &= n.rc + p.req[0] <= n.ac;
     if (p.keymask & 2) ok &= n.rm + p.req[1] <= n.am;
@@ -85,7 +85,7 @@ __device__ __forceinline__ bool fits(const PodRec& p, const NodeV& n) {
 
 // floor(y / a) for 0 <= y <= 10*a (restoring division, 4 steps, no hardware divide).
 template <typename T>
-__device__ __forceinline__ int32_t div_upto10(T y, T a) {
+__host__ __device__ __forceinline__ int32_t div_upto10(T y, T a) {
     int32_t q = 0;
     if (y >= (a << 3)) { q = 8; y -= (a << 3); }
     if (y >= (a << 2)) { q += 4; y -= (a << 2); }
@@ -95,13 +95,13 @@ __device__ __forceinline__ int32_t div_upto10(T y, T a) {
 }
 
 // LeastRequested per resource: (A - u) * 10 / A, 0 if A <= 0 or u > A.
-__device__ __forceinline__ int32_t lr_one(int64_t A, int64_t u) {
+__host__ __device__ __forceinline__ int32_t lr_one(int64_t A, int64_t u) {
     if (A <= 0 || u > A) return 0;
     return div_upto10<int64_t>((A - u) * 10, A);
 }
 
 // BalancedAllocation, exact: floor(10 * (1 - |uc/Ac - um/Am|)), 0 if a fraction >= 1.
-__device__ __forceinline__ int32_t ba_score(int64_t Ac, int64_t Am, int64_t uc, int64_t um) {
+__host__ __device__ __forceinline__ int32_t ba_score(int64_t Ac, int64_t Am, int64_t uc, int64_t um) {
     if (Ac <= 0 || Am <= 0 || uc >= Ac || um >= Am) return 0;
     typedef unsigned __int128 u128;
     u128 D = (u128)(uint64_t)Ac * (uint64_t)Am;
@@ -112,7 +112,7 @@ __device__ __forceinline__ int32_t ba_score(int64_t Ac, int64_t Am, int64_t uc, 
 }
 
 // Fused Filter + Score.  Returns weighted total + 1, or 0 when the node is not a candidate.
-__device__ __forceinline__ uint32_t eval_total1(const Cfg& c, const PodRec& p, const NodeV& n) {
+__host__ __device__ __forceinline__ uint32_t eval_total1(const Cfg& c, const PodRec& p, const NodeV& n) {
     if (!c.has_scorers) return 0;
     if (c.filter_feeds) {
         bool ok = true;

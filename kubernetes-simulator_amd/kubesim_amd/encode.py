@@ -60,22 +60,22 @@ def encode_nodes(nodes: dict):
 
     t = nodes["taint"]
     filt = (t[:, 2] == NO_SCHEDULE) | (t[:, 2] == NO_EXECUTE) if len(t) else np.zeros(0, bool)
-    trip = [tuple(r) for r in t[filt]] if len(t) else []
+    trip = [tuple(int(x) for x in r) for r in t[filt]] if len(t) else []
     taint_dict = sorted(set(trip))
     if len(taint_dict) > MAX_TAINT_BITS:
         raise EncodeError(f"{len(taint_dict)} distinct NoSchedule/NoExecute taints > {MAX_TAINT_BITS} (W=1)")
     tindex = {d: i for i, d in enumerate(taint_dict)}
     tbits = np.zeros(len(t), dtype=np.uint64)
     for i in np.nonzero(filt)[0]:
-        tbits[i] = np.uint64(1) << np.uint64(tindex[tuple(t[i])])
+        tbits[i] = np.uint64(1) << np.uint64(tindex[tuple(int(x) for x in t[i])])
     node_taint = _or_reduce_csr(tbits, nodes["taint_off"])
 
     lab = nodes["label"]
-    pairs = sorted(set(map(tuple, lab))) if len(lab) else []
+    pairs = sorted(set((int(k), int(v)) for k, v in lab)) if len(lab) else []
     if len(pairs) > MAX_LABEL_BITS:
         raise EncodeError(f"{len(pairs)} distinct label pairs > {MAX_LABEL_BITS} (W=1)")
     lindex = {d: i for i, d in enumerate(pairs)}
-    lbits = np.array([np.uint64(1) << np.uint64(lindex[tuple(r)]) for r in lab], dtype=np.uint64) \
+    lbits = np.array([np.uint64(1) << np.uint64(lindex[(int(r[0]), int(r[1]))]) for r in lab], dtype=np.uint64) \
         if len(lab) else np.zeros(0, dtype=np.uint64)
     node_label = _or_reduce_csr(lbits, nodes["label_off"])
     assert n == len(alloc)
@@ -105,16 +105,15 @@ def encode_pods(pods: dict, taint_dict, label_dict):
     rowbits = np.zeros(len(tol), dtype=np.uint64)
     if len(tol):
         for i, (k, v, e) in enumerate(taint_dict):
-            hit = tolerates(tol[:, 0], tol[:, 1], tol[:, 2], tol[:, 3], k, v, e)
+            hit = tolerates(tol[:, 0], tol[:, 1], tol[:, 2], tol[:, 3], int(k), int(v), int(e))
             rowbits |= np.where(hit, np.uint64(1) << np.uint64(i), np.uint64(0))
     tolmask = _or_reduce_csr(rowbits, pods["tol_off"])
 
     sel = pods["sel"]
     sbits = np.zeros(len(sel), dtype=np.uint64)
     if len(sel):
-        lindex = {d: i for i, d in enumerate(label_dict)}
-        keys = sel[:, 0].astype(np.int64) << 32 | sel[:, 1].astype(np.int64)
-        lut = {(k << 32) | v: i for (k, v), i in lindex.items()}
+        keys = (sel[:, 0].astype(np.int64) << 32) | sel[:, 1].astype(np.int64)
+        lut = {(int(k) << 32) | int(v): i for i, (k, v) in enumerate(label_dict)}
         uniq, inv = np.unique(keys, return_inverse=True)
         ubits = np.array([np.uint64(1) << np.uint64(lut[int(u)]) if int(u) in lut else SEL_IMPOSSIBLE
                           for u in uniq], dtype=np.uint64)

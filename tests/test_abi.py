@@ -1,0 +1,55 @@
+"""The C-ABI library loads on a GPU-less host and exports exactly what include/ks_engine.h
+declares; configuration validation needs no device."""
+import ctypes as C
+import os
+import re
+
+from kubesim_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "ks_engine.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ks_[a-z_]+)\s*\(", src)))
+
+
+def test_header_and_binding_agree():
+    assert _declared() == sorted(_lib.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.load()
+    for sym in _declared():
+        assert hasattr(L, sym), sym
+
+
+def test_bad_configs_rejected_without_device():
+    L = _lib.load()
+    def create(**kw):
+        cfg = _lib.KsConfig()
+        cfg.abi_version = _lib.KS_ABI_VERSION
+        cfg.tick_seconds = 10
+        cfg.n_scorers = 1
+        cfg.scorers[0].kind, cfg.scorers[0].weight, cfg.scorers[0].value = 0, 1, 1
+        for k, v in kw.items():
+            setattr(cfg, k, v)
+        h = C.c_void_p()
+        return L.ks_create(C.byref(cfg), C.byref(h))
+    assert create(abi_version=99) == _lib.KS_EINVAL
+    assert create(tick_seconds=0) == _lib.KS_EINVAL
+    assert create(filter_mode=7) == _lib.KS_EINVAL
+    assert create(filters=8) == _lib.KS_EINVAL
+    assert create(n_scorers=9) == _lib.KS_EINVAL
+    assert create(batch_pods=100000) == _lib.KS_EINVAL
+
+
+def test_engine_refuses_without_library(monkeypatch, tmp_path):
+    import importlib
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "missing.so"))
+    monkeypatch.setattr(_lib, "_lib", None)
+    import pytest
+    with pytest.raises(ImportError):
+        _lib.load()
+    importlib.reload(_lib)

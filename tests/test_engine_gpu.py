@@ -56,8 +56,17 @@ def test_c1_kat():
 @pytest.mark.parametrize("mode", sorted(MODES))
 @pytest.mark.parametrize("seed", [1, 2])
 def test_lockstep_small(mode, seed):
-    tr = small_trace(seed, n_nodes=40, n_pods=160, arrival="stream")
+    tr = small_trace(seed, n_nodes=400, n_pods=300, arrival="stream")
     _lockstep(tr, mode, 400)
+
+
+def test_golden_small_traces_engine():
+    """Committed fixtures (tests/golden/small_traces.json) — no oracle at run time."""
+    from golden_traces import check_case
+    with open(os.path.join(GOLDEN, "small_traces.json")) as f:
+        gold = json.load(f)
+    for case in gold["cases"]:
+        check_case(case, "engine")
 
 
 @pytest.mark.parametrize("batch", [1, 3, 64, 256, 512])

@@ -1,0 +1,82 @@
+"""The C oracle against the independent Python restatement, the hand-derived C1 KAT and the
+committed golden fixtures (CPU only)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from harness import MODES, make_oracle, small_trace
+from kubesim_amd import tracegen
+from pysim import PySim
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _lockstep_oracle_vs_pysim(tr, mode, ticks):
+    fm, fl, sc = MODES[mode]
+    co = make_oracle(tr, mode)
+    co.submit(tr)
+    ps = PySim(tr, filter_mode=fm, filters=fl, scorers=sc)
+    ps.submit(tr)
+    for t in range(ticks):
+        b1, rc1 = co.step(1)
+        b2, e2 = ps.step(1)
+        assert list(zip(b1["pod"].tolist(), b1["node"].tolist(), b1["tick"].tolist(), b1["status"].tolist())) == b2, t
+        assert (rc1 != 0) == (e2 is not None)
+        np.testing.assert_array_equal(co.usage(), np.array(ps.usage(), dtype=np.int64).reshape(-1, 3))
+        if rc1:
+            return t
+    return ticks
+
+
+@pytest.mark.parametrize("mode", sorted(MODES))
+@pytest.mark.parametrize("seed", [3, 4])
+def test_oracle_matches_python_restatement(mode, seed):
+    tr = small_trace(seed, n_nodes=30, n_pods=90, arrival="stream")
+    _lockstep_oracle_vs_pysim(tr, mode, 200)
+
+
+def test_oracle_matches_python_restatement_long_run():
+    """No taints: the feeds-score mode runs long enough for expiries and refills."""
+    tr = small_trace(9, n_nodes=40, n_pods=400, taints=False, selectors=False)
+    p = tr["pods"]
+    p["phase_sec"][:] = 5 + (np.arange(len(p["phase_sec"])) * 37) % 150
+    assert _lockstep_oracle_vs_pysim(tr, "feeds_all_lrba", 400) == 400
+
+
+def test_c1_kat_oracle():
+    with open(os.path.join(GOLDEN, "c1_kat.json")) as f:
+        kat = json.load(f)
+    tr = tracegen.c1_trace(kat["ticks"])
+    co = make_oracle(tr, "literal_const")
+    co.submit(tr)
+    for t, exp in enumerate(kat["binds"], start=1):
+        b, rc = co.step(1)
+        assert rc == 0
+        assert [(int(b["pod"][0]), int(b["node"][0]), int(b["tick"][0]), int(b["status"][0]))] == [tuple(exp)]
+        np.testing.assert_array_equal(co.usage(), np.array(kat["usage"][t - 1]))
+
+
+def test_golden_small_traces_oracle():
+    with open(os.path.join(GOLDEN, "small_traces.json")) as f:
+        gold = json.load(f)
+    from golden_traces import check_case
+    for case in gold["cases"]:
+        check_case(case, "oracle")
+
+
+def test_error_semantics():
+    """NotFound beats a bad pod key; a bad key beats a bad simSpec; both abort the run."""
+    tr = tracegen.c1_trace(6)
+    tr["pods"]["flags"][2] = 1  # empty namespace/name
+    co = make_oracle(tr, "literal_const")
+    co.submit(tr)
+    b, rc = co.step(10)
+    assert rc == 1 and len(b["pod"]) == 2 and co.tick == 3
+    b, rc = co.step(5)
+    assert rc == 1 and len(b["pod"]) == 0
+    co2 = make_oracle(tr, "no_scorers")
+    co2.submit(tr)
+    b, rc = co2.step(10)
+    assert rc == 2 and len(b["pod"]) == 0 and co2.tick == 1
