@@ -1,0 +1,205 @@
+"""Benchmark: pod-node Filter+Score evals/s (and pods bound/s) of the HIP scheduling engine.
+
+Workload (BASELINE.json configs[2], "C3"): 50,000 nodes with taints and labels, a 1M-pod
+trace with tolerations / nodeSelectors / multi-phase simSpec, Filter (fit + taint +
+selector) feeding Score (LeastRequested + BalancedAllocation), argmax, bind — one pod per
+tick, in FIFO order, exactly the reference's loop (kubesim/kubesim.go:90-225).  Synthetic
+data (tracegen, seed 0x5EED0003).
+
+A "step" is one ks_step over --pods-per-step ticks (one bind per tick).  Every pod is
+evaluated against every node (the reference's O(N) per pod), so evals = pods × nodes.
+Inputs are resident on the device before the timed region (ks_submit_pods), the timed
+region is K ks_step calls bracketed by a barrier + device synchronisation.
+
+N > 1 (torchrun): every rank runs an independent what-if replica of the workload
+(BASELINE.json configs[3] style: cluster replica × pod trace, seed ^ rank) on its own GPU;
+no data-path collective — weak scaling; value = all ranks' evals ÷ the slowest rank's time.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "kubernetes-simulator_amd"))
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+BYTES_PER_EVAL = 80     # alloc[4] + reqTotal[3] + nRunning + taint + label
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(trace, scorers, sample_pods, budget_s):
+    """The C oracle (faithful CPU restatement) on the first `sample_pods` pods of the same
+    trace, single-threaded, on this host."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    from kubesim_amd import tracegen
+    pyoracle.build()
+    tr = tracegen.slice_pods(trace, 0, sample_pods)
+    co = pyoracle.COracle(tr, filter_mode=1, filters=7, scorers=scorers)
+    co.submit(tr)
+    n = trace["nodes"]["n"]
+    done, t0 = 0, time.perf_counter()
+    while done < sample_pods and time.perf_counter() - t0 < budget_s:
+        k = min(64, sample_pods - done)
+        b, rc = co.step(k)
+        done += k
+        if rc:
+            break
+    dt = time.perf_counter() - t0
+    return dict(value=done * n / dt, unit="evals/s", cores=1, kind="port",
+                sample=f"C3 nodes ({n}), first {done} pods of the trace, oracle/ks_oracle.c single-threaded",
+                pods_per_s=done / dt, seconds=round(dt, 2))
+
+
+def load_traffic(n_launch_pods):
+    """HBM bytes per scan launch from the committed PMC profile (FETCH_SIZE ×2 gfx950
+    correction + WRITE_SIZE, per MI355X_MICROARCH.md §HBM), if present."""
+    p = os.path.join(ROOT, "profiles", "pmc_scan.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_scan_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pods-per-step", type=int, default=32768)
+    ap.add_argument("--nodes", type=int, default=50_000)
+    ap.add_argument("--pods", type=int, default=1_000_000)
+    ap.add_argument("--batch", type=int, default=0, help="pods per scan/resolve batch (0 = engine default)")
+    ap.add_argument("--cpu-sample-pods", type=int, default=4000)
+    ap.add_argument("--cpu-budget-s", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    from kubesim_amd import encode, tracegen
+    from kubesim_amd.engine import Engine
+
+    need = (args.steps + args.warmup) * args.pods_per_step
+    n_pods = max(args.pods, need)
+    seed = 0x5EED0003 ^ rank
+    t0 = time.perf_counter()
+    trace = tracegen.c3_trace(n_nodes=args.nodes, n_pods=n_pods, seed=seed)
+    enc = encode.encode_trace(trace)
+    scorers = ((1, 1, 0), (2, 1, 0))  # LeastRequested w1 + BalancedAllocation w1
+    eng = Engine(tick_seconds=trace["tick_seconds"], filter_mode=1, filters=7, scorers=scorers,
+                 device=local, batch_pods=args.batch)
+    eng.load_nodes(enc["alloc"], enc["taint"], enc["label"])
+    eng.submit(enc["pods"])
+    log(f"[rank {rank}] trace {args.nodes} nodes x {n_pods} pods ready in {time.perf_counter() - t0:.1f}s")
+
+    S = args.pods_per_step
+    for _ in range(args.warmup):
+        eng.step(S)
+
+    def barrier():
+        # ks_step synchronises the engine's stream before returning; the extra device-wide
+        # synchronize keeps the bracket honest if anything else were queued.
+        if dist is not None:
+            dist.barrier()
+        try:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.synchronize(local)
+        except ImportError:
+            pass
+
+    barrier()
+    t_start = time.perf_counter()
+    binds = 0
+    for _ in range(args.steps):
+        binds += len(eng.step(S))   # ks_step returns after its last kernel has completed
+    t_el = time.perf_counter() - t_start
+    barrier()
+    if dist is not None:
+        import torch
+        t = torch.tensor([t_el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_el = float(t.item())
+        c = torch.tensor([binds], dtype=torch.float64)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        total_binds = int(c.item())
+    else:
+        total_binds = binds
+
+    # per-kernel breakdown on one more (profiled) step: HIP events on the engine's stream
+    eng.set_profiling(True)
+    eng.step(S)
+    st = eng.last_step_stats()
+    eng.set_profiling(False)
+
+    if rank == 0:
+        nodes = args.nodes
+        evals = total_binds * nodes
+        value = evals / t_el
+        pods_per_s = total_binds / t_el
+        launches = max(st["launches"], 1)
+        pods_per_launch = st["pods"] / launches
+        scan_avg_ms = st["scan_ms"] / launches
+        res_avg_ms = st["resolve_ms"] / launches
+        # algorithmic bytes of one scan launch: 80 B per (pod, node) eval
+        scan_alg_bytes = BYTES_PER_EVAL * pods_per_launch * nodes
+        achieved = scan_alg_bytes / (scan_avg_ms * 1e-3) / 1e9 if scan_avg_ms > 0 else None
+        traffic = load_traffic(pods_per_launch)
+        cpu = None
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(trace, scorers, args.cpu_sample_pods, args.cpu_budget_s)
+        line = {
+            "metric": "pod-node Filter+Score evals/sec and pods bound/sec at 50k nodes, 1-8 GPUs",
+            "value": value,
+            "unit": "evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": t_el * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic (tracegen C3, seed 0x5EED0003 ^ rank)",
+            "config": {"workload": "C3: 50k nodes w/ taints+labels, 1M-pod trace, Filter(fit+taint+selector)"
+                                   " -> Score(LR+BA) -> argmax -> bind, 1 pod/tick",
+                       "nodes": nodes, "pods_per_step": S, "trace_pods": n_pods,
+                       "parallelism": "replicas" if world > 1 else "single-gpu",
+                       "batch_pods": args.batch or 256},
+            "pods_per_s": pods_per_s,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+                         "kernel": "scan_kernel",
+                         "note": "algorithmic bytes = 80 B x (pods x nodes) per scan launch; the scan reuses "
+                                 "each node record across the batch's pods, so frac can exceed 1 — traffic is "
+                                 "the measured HBM bytes per launch"},
+            "kernels": {"launches_per_step": launches, "pods_per_launch": pods_per_launch,
+                        "scan_avg_ms": scan_avg_ms, "resolve_avg_ms": res_avg_ms,
+                        "profiled_step_ms": st["step_ms"]},
+            "cpu_baseline": cpu,
+            "host": {"cpu": platform.processor() or platform.machine(), "nproc": os.cpu_count()},
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -17,6 +17,7 @@
 namespace ks {
 
 constexpr int kWave = 64;
+constexpr int kTopL = 8;  // exact top-L snapshot candidates kept per pod
 
 enum : uint32_t { kFilterFit = 1, kFilterTaint = 2, kFilterSelector = 4 };
 
@@ -172,13 +173,18 @@ struct EngineArgs {
     int32_t* b_node;
     int32_t* b_status;
     uint8_t* expired;
-    uint64_t* wbkey;         // [B][nwb]
+    uint64_t* lists;         // [B][nblk][kTopL] per-block top-L keys (scan -> merge)
+    uint64_t* cand;          // [B][kTopL] per-pod global top-L keys (merge -> resolve)
     int64_t* ctr;            // start, end, error code, error pod, early stops
     int32_t B;
     int32_t PG;              // pods per scan workgroup
+    int32_t nblk;            // 256-node scan blocks
 };
 
-// Launchers (defined in ks_kernels.hip).
+// Launchers and limits (defined in ks_kernels.hip).
+int max_batch_pods();
+int max_pods_per_scan_wg();
+int block_nodes();
 hipError_t launch_batch(const EngineArgs& a, hipStream_t st, hipEvent_t e_scan0, hipEvent_t e_scan1,
                         hipEvent_t e_res1);
 hipError_t launch_eval_pod(const Cfg& c, const NodeSoA& s, const PodRec* pod, uint32_t filters, uint8_t* mask,

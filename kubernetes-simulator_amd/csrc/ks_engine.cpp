@@ -28,9 +28,9 @@
 
 namespace {
 
-constexpr int64_t kMaxNodes = 16384LL * 64;  // one resolver launch covers <= 16384 wave-blocks
+constexpr int64_t kMaxNodes = 1LL << 24;  // node ids fit the packed key; lists stay < 2^31 entries
 constexpr int64_t kMaxValue = 1LL << 59;
-constexpr int kMaxBatch = 512;
+constexpr int kMaxBatch = 256;
 constexpr int kDefaultBatch = 256;
 constexpr int64_t kNever = std::numeric_limits<int64_t>::max();
 
@@ -108,7 +108,9 @@ struct ks_engine {
 
     // batch machinery
     int B = kDefaultBatch, PG = 32;
-    uint64_t* wbkey = nullptr;
+    uint64_t* lists = nullptr;
+    uint64_t* cand = nullptr;
+    int nblk = 0;
     int64_t* d_ctr = nullptr;
     int64_t* h_ctr = nullptr;  // pinned
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -151,7 +153,9 @@ ks::EngineArgs make_args(ks_engine* e) {
     a.b_node = e->b_node.p;
     a.b_status = e->b_status.p;
     a.expired = e->expired.p;
-    a.wbkey = e->wbkey;
+    a.lists = e->lists;
+    a.cand = e->cand;
+    a.nblk = e->nblk;
     a.ctr = e->d_ctr;
     a.B = e->B;
     a.PG = e->PG;
@@ -222,7 +226,8 @@ void ks_destroy(ks_engine* e) {
     e->phase_off.release(); e->cum_sec.release(); e->exp_pod.release(); e->exp_off.release();
     e->t0.release(); e->fin.release(); e->use.release(); e->expired.release();
     if (e->node_mem) (void)hipFree(e->node_mem);
-    if (e->wbkey) (void)hipFree(e->wbkey);
+    if (e->lists) (void)hipFree(e->lists);
+    if (e->cand) (void)hipFree(e->cand);
     if (e->d_ctr) (void)hipFree(e->d_ctr);
     if (e->h_ctr) (void)hipHostFree(e->h_ctr);
     if (e->d_mask) (void)hipFree(e->d_mask);
@@ -267,12 +272,16 @@ ks_status ks_load_nodes(ks_engine* e, int64_t n, const int64_t* alloc, const uin
     e->s.taint = (uint64_t*)(b + 8 * np); e->s.label = (uint64_t*)(b + 9 * np);
     e->dc.n_nodes = (int32_t)n;
     e->dc.nwb = e->nwb;
-    // pods per scan workgroup: aim for >= ~2048 workgroups (8 per CU) per scan
-    const int64_t wgx = (e->nwb + 3) / 4;
+    // pods per scan workgroup: the most pod reuse per node load that still leaves >= ~2048
+    // workgroups (8 per CU) per scan
+    e->nblk = (int)((e->n_pad + ks::block_nodes() - 1) / ks::block_nodes());
     int pg = 1;
-    while (pg < e->B && wgx * ((e->B + pg * 2 - 1) / (pg * 2)) >= 2048) pg *= 2;
+    while (pg < ks::max_pods_per_scan_wg() && pg < e->B &&
+           (int64_t)e->nblk * ((e->B + pg * 2 - 1) / (pg * 2)) >= 2048)
+        pg *= 2;
     e->PG = pg;
-    HIPCHK(e, hipMalloc(&e->wbkey, sizeof(uint64_t) * (size_t)e->B * e->nwb));
+    HIPCHK(e, hipMalloc(&e->lists, sizeof(uint64_t) * (size_t)e->B * e->nblk * ks::kTopL));
+    HIPCHK(e, hipMalloc(&e->cand, sizeof(uint64_t) * (size_t)e->B * ks::kTopL));
     HIPCHK(e, hipMalloc(&e->d_mask, std::max<int64_t>(n, 1)));
     HIPCHK(e, hipMalloc(&e->d_score, sizeof(int64_t) * std::max<int64_t>(n, 1)));
     HIPCHK(e, hipMalloc(&e->d_usage, sizeof(unsigned long long) * 3 * std::max<int64_t>(n, 1)));

@@ -1,42 +1,50 @@
 // ks_kernels.hip — CDNA4 (gfx950) kernels of the kubesim scheduling engine.
 //
-// The reference schedules one pod per tick (kubesim/kubesim.go:105-121): every pod's
-// placement depends on the binds before it.  The engine keeps that order exactly but does
-// not pay one full-cluster pass per pod on the critical path.  Per batch of B pods:
+// The reference schedules one pod per tick (kubesim/kubesim.go:105-121) and every placement
+// depends on the binds before it.  The engine keeps that order exactly, but only a tiny part
+// of each pod's decision is sequential.  Per batch of B pods:
 //
-//   expire_head  applies the expiries due at the batch's first pod (tiny)
-//   scan         every (pod, node) pair of the batch against the node state as of the batch
-//                start ("snapshot"); per pod and per wave-block of 64 nodes it keeps the best
-//                packed key.  Node records are read once per pod group, not once per pod.
-//   resolve      one 1024-thread workgroup walks the batch in FIFO order.  Only wave-blocks
-//                touched since the snapshot (a bind or an expiry landed in them) can differ
-//                from the scan; they are cached in LDS and re-evaluated exactly, every other
-//                wave-block's scan key is still exact.  The max over both is the reference's
-//                argmax; the admission test and the bind update the LDS cache; the cache is
-//                written back at the end.  This is exact, not approximate.
+//   expire_head  applies the expiries due before the batch's first pod.
+//   scan         evaluates every (pod, node) pair of the batch against the node state as of
+//                the batch start (the "snapshot"): fused Filter + Score + packed key.  Node
+//                records are read once per pod group; per pod and per 256-node block it keeps
+//                the exact top-L keys.
+//   merge        per pod: exact global top-L keys of the snapshot (sorted).
+//   resolve      one 1024-thread workgroup walks the batch in FIFO order.  A node's key can
+//                differ from the snapshot only if the node was touched in this batch (a bind
+//                or an expiry landed on it).  Touched nodes live in an LDS table and are
+//                re-evaluated exactly for every pod; the best untouched node is the first
+//                untouched entry of the pod's top-L list — exact because any node outside the
+//                list scores below every list entry.  winner = max(those).  If all L entries
+//                are touched the batch commits early and the next batch rescans.
 //
-// Packed key: (total + 1) << 32 | (0xFFFFFFFF - node); 0 = no candidate (NotFound).
+// Packed key: (total + 1) << 32 | (0xFFFFFFFF - node); 0 = no candidate (NotFound).  Max key =
+// highest total, ties to the lowest node index.
 #include "ks_device.h"
 
 namespace ks {
 
-constexpr int kScanWaves = 4;          // 256-thread scan workgroups
-constexpr int kResolveThreads = 1024;  // 16 waves
+constexpr int kScanWaves = 4;            // 256-thread scan workgroups, one 256-node block each
+constexpr int kBlockNodes = kScanWaves * kWave;
+constexpr int kL = kTopL;                // candidate list length per pod
+constexpr int kMaxPG = 32;               // pods per scan workgroup (LDS list staging)
+constexpr int kResolveThreads = 1024;    // 16 waves
 constexpr int kResolveWaves = kResolveThreads / kWave;
-constexpr int kMaxTW = 16;             // wave-blocks cached by the resolver
-constexpr int kMaxWbPerThread = 16;    // nwb <= 16384 wave-blocks (1,048,576 nodes) per launch
-constexpr int kMaxNwb = kMaxWbPerThread * kResolveThreads;
-constexpr int kMaxBatch = 512;
-constexpr int kMaxExp = 1024;          // expiries prefetched into LDS per batch
+constexpr int kTMax = 768;               // touched-node table (LDS)
+constexpr int kHash = 2048;              // open-addressing node -> entry map (LDS)
+constexpr int kMaxBatchR = 256;          // pods per resolve launch
+constexpr int kMaxExp = kTMax - kMaxBatchR;  // expiries pre-inserted per batch
 
 enum : int64_t { kCtrStart = 0, kCtrEnd = 1, kCtrErr = 2, kCtrErrPod = 3, kCtrEarly = 4 };
 enum : uint32_t { kFlagBadKey = 1, kFlagBadSpec = 2 };
 enum : int64_t { kErrEinval = 1, kErrNotFound = 2 };
 
+__device__ __forceinline__ int popc_below(uint64_t mask, int lane) {
+    return __popcll(mask & ((1ull << lane) - 1ull));
+}
 
 // ------------------------------------------------------------------------------------------
-// expire_head: expiries due at the batch's first pod, applied straight to the node SoA so the
-// resolver's first pod never needs cache space for them.
+// expire_head: expiries due before the batch's first pod, applied straight to the node SoA.
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void expire_head_kernel(EngineArgs a) {
     const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
@@ -56,28 +64,122 @@ __global__ __launch_bounds__(256) void expire_head_kernel(EngineArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
-// scan: grid (ceil(nwb / 4), ceil(B / PG)); each wave owns one wave-block (lane = node) and
-// evaluates PG pods against it; lane 0 stores the wave-block's best key per pod.
+// scan: grid (nblk, ceil(B / PG)).  Each wave owns 64 nodes (lane = node); for each of the
+// workgroup's PG pods it extracts its exact top-L keys.  Scores are small integers, so the
+// top-L of a wave is usually one or two "tie classes": take the max score, every lane at it
+// (lowest lanes first), repeat below it — a 32-bit wave max + ballot per class.  The four
+// wave lists are then merged by rank (each list is sorted) into the block's top-L.
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void scan_kernel(EngineArgs a) {
+    __shared__ uint64_t wl[kMaxPG][kScanWaves][kL];  // per-pod, per-wave top-L lists
     const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
     if (a.ctr[kCtrErr] != 0) return;
     const int64_t nb = min<int64_t>(a.B, end - start);
     const int pg0 = blockIdx.y * a.PG;
     if (pg0 >= nb) return;
-    const int lane = threadIdx.x & (kWave - 1);
-    const int wb = blockIdx.x * kScanWaves + (threadIdx.x >> 6);
-    if (wb >= a.c.nwb) return;
-    const uint32_t base = (uint32_t)wb * kWave;
+    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
+    const int blk = blockIdx.x;
+    const uint32_t base = (uint32_t)blk * kBlockNodes + wave * kWave;
     const int64_t node = (int64_t)base + lane;
-    const NodeV n = load_node(a.s, node);
     const bool valid = node < a.c.n_nodes;
-    const int pg1 = (int)min<int64_t>(pg0 + a.PG, nb);
-    for (int b = pg0; b < pg1; ++b) {
-        const PodRec p = a.pods[start + b];
-        const uint32_t t1 = valid ? eval_total1(a.c, p, n) : 0u;
-        const uint64_t key = wave_best_key(t1, base);
-        if (lane == 0) a.wbkey[(int64_t)b * a.c.nwb + wb] = key;
+    NodeV n{};
+    if (node < (int64_t)a.c.nwb * kWave) n = load_node(a.s, node);
+    const int np = (int)min<int64_t>(a.PG, nb - pg0);
+    for (int b = 0; b < np; ++b) {
+        const PodRec p = a.pods[start + pg0 + b];
+        uint32_t rem = valid ? eval_total1(a.c, p, n) : 0u;
+        int cnt = 0;
+        for (int r = 0; r < kL && cnt < kL; ++r) {
+            const uint32_t m = wave_max_u32(rem);
+            if (m == 0) break;
+            const uint64_t mask = __ballot(rem == m);
+            if (rem == m) {
+                const int rank = cnt + popc_below(mask, lane);
+                if (rank < kL) wl[b][wave][rank] = make_key(m, base + lane);
+                rem = 0;
+            }
+            cnt += __popcll(mask);
+        }
+        if (lane >= cnt && lane < kL) wl[b][wave][lane] = 0ull;
+    }
+    __syncthreads();
+    // merge: 32 candidates per pod (4 lists x L), two pods per wave pass; the rank of a
+    // candidate = its position in its own list + the entries of the other lists above it.
+    const int half = lane >> 5, l32 = lane & 31;
+    const int li = l32 / kL, le = l32 % kL;
+    for (int b0 = wave * 2; b0 < np; b0 += kScanWaves * 2) {
+        const int b = b0 + half;
+        const uint64_t c = b < np ? wl[b][li][le] : 0ull;
+        const uint64_t nz = __ballot(c != 0);
+        if (b < np) {
+            uint64_t* out = a.lists + ((int64_t)(pg0 + b) * a.nblk + blk) * kL;
+            if (c != 0) {
+                int rank = le;
+#pragma unroll
+                for (int o = 0; o < kScanWaves; ++o) {
+                    if (o == li) continue;
+#pragma unroll
+                    for (int k = 0; k < kL; ++k) rank += wl[b][o][k] > c ? 1 : 0;
+                }
+                if (rank < kL) out[rank] = c;
+            }
+            const int total = __popcll((nz >> (half * 32)) & 0xFFFFFFFFull);
+            if (l32 < kL && l32 >= total) out[l32] = 0ull;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// merge: one 256-thread workgroup per pod; exact global top-L over the block lists.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void merge_kernel(EngineArgs a) {
+    __shared__ uint64_t red[4];
+    __shared__ int32_t owner[4];
+    const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
+    if (a.ctr[kCtrErr] != 0) return;
+    const int64_t nb = min<int64_t>(a.B, end - start);
+    const int b = blockIdx.x;
+    if (b >= nb) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint64_t top[kL];  // per-thread sorted (descending) top-L over its blocks
+#pragma unroll
+    for (int k = 0; k < kL; ++k) top[k] = 0;
+    const uint64_t* lists = a.lists + (int64_t)b * a.nblk * kL;
+    for (int blk = tid; blk < a.nblk; blk += 256) {
+#pragma unroll
+        for (int k = 0; k < kL; ++k) {
+            uint64_t v = lists[(int64_t)blk * kL + k];
+            if (v <= top[kL - 1]) break;  // block lists are sorted: nothing further can enter
+#pragma unroll
+            for (int s = 0; s < kL; ++s) {
+                const uint64_t t = top[s];
+                const bool gt = v > t;
+                top[s] = gt ? v : t;
+                v = gt ? t : v;
+            }
+        }
+    }
+    // L rounds: the workgroup max of the thread heads; its owner advances
+    int head = 0;
+    for (int r = 0; r < kL; ++r) {
+        uint64_t h = 0;
+#pragma unroll
+        for (int k = 0; k < kL; ++k) h = (k == head) ? top[k] : h;
+        const uint64_t m = wave_max_u64(h);
+        const uint64_t hit = __ballot(h == m && m != 0);
+        if (lane == 0) {
+            red[wave] = m;
+            owner[wave] = hit ? wave * 64 + __ffsll((unsigned long long)hit) - 1 : -1;
+        }
+        __syncthreads();
+        uint64_t best = 0;
+        int who = -1;
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+            if (red[w] > best) { best = red[w]; who = owner[w]; }
+        if (tid == 0) a.cand[(int64_t)b * kL + r] = best;
+        if (tid == who) head++;
+        __syncthreads();
     }
 }
 
@@ -85,52 +187,78 @@ __global__ __launch_bounds__(256) void scan_kernel(EngineArgs a) {
 // resolve: one workgroup, sequential over the batch in FIFO order (one bind per tick).
 // ------------------------------------------------------------------------------------------
 struct ResolveShared {
-    int64_t ci[kMaxTW][8][kWave];   // ac am ag ap rc rm rg nr of cached wave-blocks
-    uint64_t cu[kMaxTW][2][kWave];  // taint label
-    int32_t tw_wb[kMaxTW];
-    uint32_t touched[kMaxNwb / 32];
-    int32_t lb_node[kMaxBatch];
-    int32_t lb_stat[kMaxBatch];
-    int32_t ex_off[kMaxBatch + 1];
+    int64_t ts[8][kTMax];       // touched-node state: ac am ag ap rc rm rg nr
+    uint64_t tu[2][kTMax];      // taint label
+    int32_t tnode[kTMax];
+    int32_t hkey[kHash];        // node id or -1
+    int32_t hval[kHash];        // entry index
+    PodRec pod[kMaxBatchR];
+    int32_t dur[kMaxBatchR];
+    uint64_t cand[kMaxBatchR][kL];
+    int32_t lb_node[kMaxBatchR];
+    int32_t lb_stat[kMaxBatchR];
+    int32_t ex_off[kMaxBatchR + 1];
     int32_t ex_q[kMaxExp];
     int32_t ex_node[kMaxExp];
     int32_t ex_ok[kMaxExp];
-    int64_t ex_req[kMaxExp][3];
     uint64_t red[kResolveWaves];
-    int32_t tw_count, stop, committed, err_code, err_pod;
+    int32_t n_t, stop, committed, err_code, err_pod, nb;
 };
 
 __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// Wave 0 only: slot of wave-block wb in the LDS cache, loading it from HBM if needed.
-__device__ __forceinline__ int cache_slot(ResolveShared& sh, const EngineArgs& a, int wb, int lane) {
-    const int twc = sh.tw_count;
-    const bool hit = lane < twc && sh.tw_wb[lane] == wb;
-    const uint64_t m = __ballot(hit);
-    if (m) return __ffsll((unsigned long long)m) - 1;
-    const int slot = twc;
-    const int64_t node = (int64_t)wb * kWave + lane;
-    const NodeV v = load_node(a.s, node);
-    sh.ci[slot][0][lane] = v.ac; sh.ci[slot][1][lane] = v.am;
-    sh.ci[slot][2][lane] = v.ag; sh.ci[slot][3][lane] = v.ap;
-    sh.ci[slot][4][lane] = v.rc; sh.ci[slot][5][lane] = v.rm;
-    sh.ci[slot][6][lane] = v.rg; sh.ci[slot][7][lane] = v.nr;
-    sh.cu[slot][0][lane] = v.taint; sh.cu[slot][1][lane] = v.label;
-    if (lane == 0) {
-        sh.tw_wb[slot] = wb;
-        sh.tw_count = twc + 1;
-        sh.touched[wb >> 5] |= 1u << (wb & 31);
+__device__ __forceinline__ uint32_t hslot(int32_t node) { return ((uint32_t)node * 2654435761u) >> (32 - 11); }
+
+// entry index of `node` in the touched table, or -1
+__device__ __forceinline__ int h_find(const ResolveShared& sh, int32_t node) {
+    uint32_t s = hslot(node);
+    for (int i = 0; i < kHash; ++i) {
+        const int32_t k = sh.hkey[s];
+        if (k == node) return sh.hval[s];
+        if (k == -1) return -1;
+        s = (s + 1) & (kHash - 1);
     }
-    lds_fence();
-    return slot;
+    return -1;
 }
 
-__device__ __forceinline__ NodeV cached_node(const ResolveShared& sh, int slot, int l) {
+// single-lane insert of a node known to be absent
+__device__ __forceinline__ void h_insert(ResolveShared& sh, int32_t node, int32_t idx) {
+    uint32_t s = hslot(node);
+    while (sh.hkey[s] != -1) s = (s + 1) & (kHash - 1);
+    sh.hkey[s] = node;
+    sh.hval[s] = idx;
+}
+
+__device__ __forceinline__ NodeV t_node(const ResolveShared& sh, int e) {
     NodeV v;
-    v.ac = sh.ci[slot][0][l]; v.am = sh.ci[slot][1][l]; v.ag = sh.ci[slot][2][l]; v.ap = sh.ci[slot][3][l];
-    v.rc = sh.ci[slot][4][l]; v.rm = sh.ci[slot][5][l]; v.rg = sh.ci[slot][6][l]; v.nr = sh.ci[slot][7][l];
-    v.taint = sh.cu[slot][0][l]; v.label = sh.cu[slot][1][l];
+    v.ac = sh.ts[0][e]; v.am = sh.ts[1][e]; v.ag = sh.ts[2][e]; v.ap = sh.ts[3][e];
+    v.rc = sh.ts[4][e]; v.rm = sh.ts[5][e]; v.rg = sh.ts[6][e]; v.nr = sh.ts[7][e];
+    v.taint = sh.tu[0][e]; v.label = sh.tu[1][e];
     return v;
+}
+
+__device__ __forceinline__ int64_t node_field(const NodeSoA& s, int f, int64_t i) {
+    switch (f) {
+        case 0: return s.ac[i]; case 1: return s.am[i]; case 2: return s.ag[i]; case 3: return s.ap[i];
+        case 4: return s.rc[i]; case 5: return s.rm[i]; case 6: return s.rg[i]; case 7: return s.nr[i];
+        case 8: return (int64_t)s.taint[i]; default: return (int64_t)s.label[i];
+    }
+}
+
+__device__ __forceinline__ void t_store_field(ResolveShared& sh, int e, int f, int64_t v) {
+    if (f < 8) sh.ts[f][e] = v; else sh.tu[f - 8][e] = (uint64_t)v;
+}
+
+__device__ __forceinline__ int32_t key_node(uint64_t key) { return (int32_t)(0xFFFFFFFFu - (uint32_t)key); }
+
+// Wave 0: first entry of pod i's list whose node is not in the touched table (-1 if none);
+// `full` = the list holds L candidates (so "none" means exhausted, not "no candidates").
+__device__ __forceinline__ int first_untouched(const ResolveShared& sh, int i, int lane, bool& full) {
+    const uint64_t c = lane < kL ? sh.cand[i][lane] : 0ull;
+    const bool ok = c != 0 && h_find(sh, key_node(c)) < 0;
+    const uint64_t m = __ballot(ok);
+    full = __popcll(__ballot(c != 0)) == kL;
+    return m ? __ffsll((unsigned long long)m) - 1 : -1;
 }
 
 __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) {
@@ -138,20 +266,36 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid >> 6;
     const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
     if (a.ctr[kCtrErr] != 0) return;
-    const int nb = (int)min<int64_t>(a.B, end - start);
+    int nb = (int)min<int64_t>(min<int64_t>(a.B, kMaxBatchR), end - start);
     if (nb <= 0) return;
-    const int nwb = a.c.nwb;
-    const int nper = (nwb + kResolveThreads - 1) / kResolveThreads;
-    const int64_t e_base = a.exp_off[start];
-    const int64_t e_cnt = a.exp_off[start + nb] - e_base;
 
-    for (int w = tid; w < (nwb + 31) / 32; w += kResolveThreads) sh.touched[w] = 0;
-    for (int i = tid; i <= nb; i += kResolveThreads) sh.ex_off[i] = (int32_t)(a.exp_off[start + i] - e_base);
-    for (int64_t e = tid; e < e_cnt && e < kMaxExp; e += kResolveThreads) {
+    // window: expiries of pods start+1 .. start+nb-1 (pod start's were applied by expire_head);
+    // shrink the batch so that they fit the pre-insert budget
+    const int64_t e_base = a.exp_off[start + 1];
+    if (tid == 0) {
+        int lo = 1, hi = nb;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) / 2;
+            if (a.exp_off[start + mid] - e_base <= kMaxExp) lo = mid; else hi = mid - 1;
+        }
+        sh.nb = lo;
+        sh.n_t = 0; sh.stop = 0; sh.committed = lo; sh.err_code = 0; sh.err_pod = -1;
+    }
+    for (int h = tid; h < kHash; h += kResolveThreads) sh.hkey[h] = -1;
+    __syncthreads();
+    nb = sh.nb;
+    const int64_t e_cnt = nb > 1 ? a.exp_off[start + nb] - e_base : 0;
+
+    for (int i = tid; i < nb; i += kResolveThreads) {
+        sh.pod[i] = a.pods[start + i];
+        sh.dur[i] = a.dur[start + i];
+    }
+    for (int i = tid; i < nb * kL; i += kResolveThreads) sh.cand[i / kL][i % kL] = a.cand[i];
+    for (int i = tid; i <= nb; i += kResolveThreads)
+        sh.ex_off[i] = i <= 1 ? 0 : (int32_t)(a.exp_off[start + i] - e_base);
+    for (int e = tid; e < e_cnt; e += kResolveThreads) {
         const int32_t q = a.exp_pod[e_base + e];
         sh.ex_q[e] = q;
-        const PodRec& pq = a.pods[q];
-        sh.ex_req[e][0] = pq.req[0]; sh.ex_req[e][1] = pq.req[1]; sh.ex_req[e][2] = pq.req[2];
         if (q < start) {
             sh.ex_node[e] = a.b_node[q];
             sh.ex_ok[e] = (a.b_status[q] == 0) && !a.expired[q];
@@ -160,104 +304,121 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
             sh.ex_ok[e] = 0;
         }
     }
-    if (tid == 0) { sh.tw_count = 0; sh.stop = 0; sh.committed = nb; sh.err_code = 0; sh.err_pod = -1; }
-
-    uint64_t pre[kMaxWbPerThread];
-#pragma unroll
-    for (int k = 0; k < kMaxWbPerThread; ++k) {
-        const int w = tid + k * kResolveThreads;
-        pre[k] = (k < nper && w < nwb) ? a.wbkey[w] : 0ull;
+    __syncthreads();
+    // pre-insert every node an expiry of this batch lands on (q bound before the batch): the
+    // per-pod expiry step then never waits on HBM
+    if (wave == 0) {
+        for (int e0 = 0; e0 < e_cnt; e0 += kWave) {
+            const int e = e0 + lane;
+            const bool want = e < e_cnt && sh.ex_ok[e];
+            const int32_t mine = want ? sh.ex_node[e] : 0;
+            uint64_t m = __ballot(want);
+            while (m) {
+                const int l = __ffsll((unsigned long long)m) - 1;
+                m &= m - 1;
+                const int32_t nd = __shfl(mine, l, kWave);
+                if (lane == 0 && h_find(sh, nd) < 0) {
+                    const int idx = sh.n_t;
+                    sh.tnode[idx] = nd;
+                    h_insert(sh, nd, idx);
+                    sh.n_t = idx + 1;
+                }
+                lds_fence();
+            }
+        }
+    }
+    __syncthreads();
+    for (int e = tid; e < sh.n_t; e += kResolveThreads) {
+        const NodeV v = load_node(a.s, sh.tnode[e]);
+        sh.ts[0][e] = v.ac; sh.ts[1][e] = v.am; sh.ts[2][e] = v.ag; sh.ts[3][e] = v.ap;
+        sh.ts[4][e] = v.rc; sh.ts[5][e] = v.rm; sh.ts[6][e] = v.rg; sh.ts[7][e] = v.nr;
+        sh.tu[0][e] = v.taint; sh.tu[1][e] = v.label;
     }
     __syncthreads();
 
+    // Wave 0 keeps the next pod's best untouched list entry and, in lanes 0-9, its snapshot
+    // fields — fetched one pod ahead, so the bind of an untouched node never waits on HBM.
+    // The touched table only grows at a bind, and the prefetch runs after the bind, so the
+    // entry is exact when the pod is resolved.
+    int pa = -1;
+    bool pfull = false;
+    int64_t fa = 0;
+    if (wave == 0) {
+        pa = first_untouched(sh, 0, lane, pfull);
+        if (pa >= 0 && lane < 10) fa = node_field(a.s, lane, key_node(sh.cand[0][pa]));
+    }
+
     for (int i = 0; i < nb; ++i) {
         const int64_t j = start + i;
-        // ---- phase A (wave 0): cache budget, then the expiries due before pod j binds
+        // ---- phase A (wave 0): the expiries due before pod j binds (nodes already in the table)
         if (wave == 0 && i > 0 && !sh.stop) {
-            const int e0 = sh.ex_off[i], e1 = sh.ex_off[i + 1];
-            if (sh.tw_count + (e1 - e0) + 1 > kMaxTW) {
-                if (lane == 0) { sh.stop = 1; sh.committed = i; }
-            } else {
-                for (int e = e0; e < e1; ++e) {
-                    int32_t q, nd, ok;
+            for (int e = sh.ex_off[i]; e < sh.ex_off[i + 1]; ++e) {
+                const int32_t q = sh.ex_q[e];
+                int32_t nd;
+                bool ok;
+                if (q >= start) { nd = sh.lb_node[q - start]; ok = sh.lb_stat[q - start] == 0; }
+                else { nd = sh.ex_node[e]; ok = sh.ex_ok[e] != 0; }
+                if (!ok) continue;
+                if (lane == 0) {
+                    const int t = h_find(sh, nd);
                     int64_t r0, r1, r2;
-                    if (e < kMaxExp) {
-                        q = sh.ex_q[e]; r0 = sh.ex_req[e][0]; r1 = sh.ex_req[e][1]; r2 = sh.ex_req[e][2];
-                        nd = sh.ex_node[e]; ok = sh.ex_ok[e];
-                    } else {  // beyond the prefetch window: read HBM directly
-                        q = a.exp_pod[e_base + e];
-                        const PodRec& pq = a.pods[q];
-                        r0 = pq.req[0]; r1 = pq.req[1]; r2 = pq.req[2];
-                        nd = q < start ? a.b_node[q] : -1;
-                        ok = q < start ? (a.b_status[q] == 0 && !a.expired[q]) : 0;
-                    }
-                    if (q >= start) {
-                        nd = sh.lb_node[q - start];
-                        ok = sh.lb_stat[q - start] == 0;
-                    }
-                    if (!ok) continue;
-                    const int slot = cache_slot(sh, a, nd >> 6, lane);
-                    if (lane == 0) {
-                        const int l = nd & 63;
-                        sh.ci[slot][4][l] -= r0; sh.ci[slot][5][l] -= r1;
-                        sh.ci[slot][6][l] -= r2; sh.ci[slot][7][l] -= 1;
-                        a.expired[q] = 1;
-                    }
-                    lds_fence();
+                    if (q >= start) { r0 = sh.pod[q - start].req[0]; r1 = sh.pod[q - start].req[1]; r2 = sh.pod[q - start].req[2]; }
+                    else { r0 = a.pods[q].req[0]; r1 = a.pods[q].req[1]; r2 = a.pods[q].req[2]; }
+                    sh.ts[4][t] -= r0; sh.ts[5][t] -= r1; sh.ts[6][t] -= r2; sh.ts[7][t] -= 1;
+                    a.expired[q] = 1;
                 }
+                lds_fence();
             }
         }
         __syncthreads();
         if (sh.stop) break;
 
-        // ---- phase B (all waves): best untouched scan key + exact keys of cached wave-blocks
-        const PodRec p = a.pods[j];
-        uint64_t best = 0;
-#pragma unroll
-        for (int k = 0; k < kMaxWbPerThread; ++k) {
-            const int w = tid + k * kResolveThreads;
-            if (k < nper && w < nwb && !((sh.touched[w >> 5] >> (w & 31)) & 1u)) best = best > pre[k] ? best : pre[k];
-        }
-        if (i + 1 < nb) {
-            const uint64_t* row = a.wbkey + (int64_t)(i + 1) * nwb;
-#pragma unroll
-            for (int k = 0; k < kMaxWbPerThread; ++k) {
-                const int w = tid + k * kResolveThreads;
-                if (k < nper && w < nwb) pre[k] = row[w];
-            }
-        }
-        const int twc = sh.tw_count;
-        for (int s = wave; s < twc; s += kResolveWaves) {
-            const uint32_t base = (uint32_t)sh.tw_wb[s] * kWave;
-            const NodeV n = cached_node(sh, s, lane);
-            const uint32_t t1 = (base + lane < (uint32_t)a.c.n_nodes) ? eval_total1(a.c, p, n) : 0u;
-            const uint64_t key = wave_best_key(t1, base);
-            best = best > key ? best : key;
+        // ---- phase B (all waves): exact keys of the touched nodes; wave 0 adds the list's
+        // best untouched key
+        const PodRec p = sh.pod[i];
+        const uint64_t kkey = (wave == 0 && pa >= 0) ? sh.cand[i][pa] : 0ull;
+        uint64_t best = (wave == 0 && lane == 0) ? kkey : 0ull;
+        const int nt = sh.n_t;
+        for (int e = tid; e < nt; e += kResolveThreads) {
+            const uint32_t t1 = eval_total1(a.c, p, t_node(sh, e));
+            const uint64_t k = make_key(t1, (uint32_t)sh.tnode[e]);
+            best = best > k ? best : k;
         }
         best = wave_max_u64(best);
         if (lane == 0) sh.red[wave] = best;
         __syncthreads();
 
-        // ---- phase C (wave 0): global argmax, CreatePod admission, bind
+        // ---- phase C (wave 0): argmax, CreatePod admission, bind; prefetch for pod i+1
         if (wave == 0) {
             uint64_t v = lane < kResolveWaves ? sh.red[lane] : 0ull;
             v = wave_max_u64(v);
-            if (v == 0) {
+            if (pa < 0 && pfull) {
+                // every list entry is touched: the untouched maximum is unknown -> rescan
+                if (lane == 0) { sh.stop = 1; sh.committed = i; }
+            } else if (v == 0) {
                 if (lane == 0) { sh.stop = 1; sh.committed = i; sh.err_code = kErrNotFound; sh.err_pod = (int32_t)j; }
             } else if (p.flags & kFlagBadKey) {
                 if (lane == 0) { sh.stop = 1; sh.committed = i; sh.err_code = kErrEinval; sh.err_pod = (int32_t)j; }
             } else {
-                const int32_t nd = (int32_t)(0xFFFFFFFFu - (uint32_t)v);
-                const int slot = cache_slot(sh, a, nd >> 6, lane);
-                const int l = nd & 63;
-                const NodeV n = cached_node(sh, slot, l);
+                const int32_t nd = key_node(v);
+                int t;
+                if (v == kkey) {
+                    // the untouched list candidate: becomes a touched entry with its snapshot state
+                    t = sh.n_t;
+                    if (lane < 10) t_store_field(sh, t, lane, fa);
+                    if (lane == 0) { sh.tnode[t] = nd; h_insert(sh, nd, t); sh.n_t = t + 1; }
+                    lds_fence();
+                } else {
+                    t = h_find(sh, nd);
+                }
+                const NodeV n = t_node(sh, t);
                 const bool ok = fits(p, n);
                 if (p.flags & kFlagBadSpec) {
                     if (lane == 0) { sh.stop = 1; sh.committed = i; sh.err_code = kErrEinval; sh.err_pod = (int32_t)j; }
                 } else if (lane == 0) {
-                    if (ok && a.dur[j] > 0) {
-                        sh.ci[slot][4][l] += p.req[0]; sh.ci[slot][5][l] += p.req[1];
-                        sh.ci[slot][6][l] += p.req[2]; sh.ci[slot][7][l] += 1;
+                    if (ok && sh.dur[i] > 0) {
+                        sh.ts[4][t] += p.req[0]; sh.ts[5][t] += p.req[1];
+                        sh.ts[6][t] += p.req[2]; sh.ts[7][t] += 1;
                     }
                     sh.lb_node[i] = nd;
                     sh.lb_stat[i] = ok ? 0 : 1;
@@ -266,22 +427,25 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
                 }
                 lds_fence();
             }
+            if (i + 1 < nb) {
+                pa = first_untouched(sh, i + 1, lane, pfull);
+                if (pa >= 0 && lane < 10) fa = node_field(a.s, lane, key_node(sh.cand[i + 1][pa]));
+            }
         }
-        // phase A of the next pod runs on wave 0 too; its barrier publishes this bind.
     }
     __syncthreads();
 
-    // ---- write back the mutable fields of every cached wave-block
-    for (int s = wave; s < sh.tw_count; s += kResolveWaves) {
-        const int64_t node = (int64_t)sh.tw_wb[s] * kWave + lane;
-        a.s.rc[node] = sh.ci[s][4][lane];
-        a.s.rm[node] = sh.ci[s][5][lane];
-        a.s.rg[node] = sh.ci[s][6][lane];
-        a.s.nr[node] = sh.ci[s][7][lane];
+    // ---- write back the mutable fields of every touched node
+    for (int e = tid; e < sh.n_t; e += kResolveThreads) {
+        const int64_t nd = sh.tnode[e];
+        a.s.rc[nd] = sh.ts[4][e];
+        a.s.rm[nd] = sh.ts[5][e];
+        a.s.rg[nd] = sh.ts[6][e];
+        a.s.nr[nd] = sh.ts[7][e];
     }
     if (tid == 0) {
         a.ctr[kCtrStart] = start + sh.committed;
-        if (sh.committed < nb && sh.err_code == 0) a.ctr[kCtrEarly] += 1;
+        if (sh.committed < a.B && sh.err_code == 0 && start + sh.committed < end) a.ctr[kCtrEarly] += 1;
         if (sh.err_code) { a.ctr[kCtrErr] = sh.err_code; a.ctr[kCtrErrPod] = sh.err_pod; }
     }
 }
@@ -345,18 +509,20 @@ __global__ __launch_bounds__(256) void usage_kernel(int64_t q_lo, int64_t q_hi, 
     }
 }
 
-}  // namespace ks
+// ---------------------------------------------------------------------------------------------
+// Launchers, called by ks_engine.cpp.
+// ---------------------------------------------------------------------------------------------
+int max_batch_pods() { return kMaxBatchR; }
+int max_pods_per_scan_wg() { return kMaxPG; }
+int block_nodes() { return kBlockNodes; }
 
-// ---------------------------------------------------------------------------------------------
-// Launchers (host side of this translation unit), called by ks_engine.cpp.
-// ---------------------------------------------------------------------------------------------
-namespace ks {
 hipError_t launch_batch(const EngineArgs& a, hipStream_t st, hipEvent_t e_scan0, hipEvent_t e_scan1,
                         hipEvent_t e_res1) {
     hipLaunchKernelGGL(expire_head_kernel, dim3(1), dim3(256), 0, st, a);
     if (e_scan0) (void)hipEventRecord(e_scan0, st);
-    dim3 g((a.c.nwb + kScanWaves - 1) / kScanWaves, (a.B + a.PG - 1) / a.PG);
-    hipLaunchKernelGGL(scan_kernel, g, dim3(kScanWaves * kWave), 0, st, a);
+    dim3 g(a.nblk, (a.B + a.PG - 1) / a.PG);
+    hipLaunchKernelGGL(scan_kernel, g, dim3(kBlockNodes), 0, st, a);
+    hipLaunchKernelGGL(merge_kernel, dim3(a.B), dim3(256), 0, st, a);
     if (e_scan1) (void)hipEventRecord(e_scan1, st);
     hipLaunchKernelGGL(resolve_kernel, dim3(1), dim3(kResolveThreads), 0, st, a);
     if (e_res1) (void)hipEventRecord(e_res1, st);

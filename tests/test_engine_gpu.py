@@ -111,3 +111,25 @@ def test_filter_score_match_oracle():
             feas, score = ora.eval(pod)
             np.testing.assert_array_equal(eng.filter(pod), feas)
             np.testing.assert_array_equal(eng.score(pod), score)
+
+
+def test_list_exhaustion_forces_rescan():
+    """Identical nodes and pods under LeastRequested: pod k takes node k, so after L binds a
+    pod's whole snapshot top-L list is touched and the batch must commit early and rescan."""
+    tr = small_trace(21, n_nodes=300, n_pods=900, taints=False, labels=False, tolerations=False,
+                     selectors=False)
+    nd, p = tr["nodes"], tr["pods"]
+    nd["alloc"][:] = nd["alloc"][0]
+    nd["alloc_has"][:] = 15
+    p["req"][:] = p["req"][0]
+    mode = "feeds_fit_lr"
+    enc = encoded(tr)
+    eng = make_engine(tr, enc, mode, 256)
+    eng.submit(enc["pods"])
+    ora = make_oracle(tr, mode)
+    ora.submit(tr)
+    eb, erc = engine_run(eng, 900, 900)
+    ob, orc = oracle_run(ora, 900)
+    assert_same_binds(eb, ob)
+    assert erc == orc
+    assert eng.last_step_stats()["launches"] > 900 // 256 + 2  # early commits happened
