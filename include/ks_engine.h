@@ -138,6 +138,10 @@ typedef struct {
     int64_t pods;
 } ks_step_stats;
 ks_status ks_last_step_stats(const ks_engine* eng, ks_step_stats* out);
+/* Device counters (diagnostics): [0] next pod, [1] step end, [2] error, [3] error pod,
+ * [4] batches that committed early (top-L list exhausted), [8..12] resolver phase cycle
+ * sums in a -DKS_STAMPS diagnostic build. */
+ks_status ks_debug_counters(ks_engine* eng, int64_t* out16);
 void ks_set_profiling(ks_engine* eng, int enable);
 
 #ifdef __cplusplus

@@ -101,14 +101,31 @@ __host__ __device__ __forceinline__ int32_t lr_one(int64_t A, int64_t u) {
     return div_upto10<int64_t>((A - u) * 10, A);
 }
 
+__host__ __device__ __forceinline__ int bitlen(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return x ? 64 - __clzll((long long)x) : 0;
+#else
+    return x ? 64 - __builtin_clzll(x) : 0;
+#endif
+}
+
 // BalancedAllocation, exact: floor(10 * (1 - |uc/Ac - um/Am|)), 0 if a fraction >= 1.
+// With D = Ac*Am and X = |uc*Am - um*Ac| the score is floor(10 (D - X) / D).  When Ac*Am
+// < 2^59 every intermediate fits 64 bits (the common case once memory is held in bytes, see
+// ks_engine.cpp's memory scale); otherwise the same formula runs in 128 bits.
 __host__ __device__ __forceinline__ int32_t ba_score(int64_t Ac, int64_t Am, int64_t uc, int64_t um) {
     if (Ac <= 0 || Am <= 0 || uc >= Ac || um >= Am) return 0;
+    if (bitlen((uint64_t)Ac) + bitlen((uint64_t)Am) <= 59) {
+        const uint64_t D = (uint64_t)Ac * (uint64_t)Am;
+        const uint64_t a = (uint64_t)uc * (uint64_t)Am, b = (uint64_t)um * (uint64_t)Ac;
+        const uint64_t X = a > b ? a - b : b - a;
+        return div_upto10<uint64_t>((D - X) * 10, D);
+    }
     typedef unsigned __int128 u128;
-    u128 D = (u128)(uint64_t)Ac * (uint64_t)Am;
-    u128 a = (u128)(uint64_t)uc * (uint64_t)Am;
-    u128 b = (u128)(uint64_t)um * (uint64_t)Ac;
-    u128 X = a > b ? a - b : b - a;
+    const u128 D = (u128)(uint64_t)Ac * (uint64_t)Am;
+    const u128 a = (u128)(uint64_t)uc * (uint64_t)Am;
+    const u128 b = (u128)(uint64_t)um * (uint64_t)Ac;
+    const u128 X = a > b ? a - b : b - a;
     return div_upto10<u128>((D - X) * 10, D);
 }
 
@@ -134,22 +151,25 @@ __device__ __forceinline__ uint64_t make_key(uint32_t total1, uint32_t node) {
     return total1 ? (((uint64_t)total1 << 32) | (uint64_t)(0xFFFFFFFFu - node)) : 0ull;
 }
 
+// Wave-wide unsigned max in VALU DPP moves (no LDS crossbar): Hillis-Steele row_shr 1/2/4/8
+// leaves each 16-lane row's max in its lane 15, row_bcast 15/31 folds the rows into lane 63.
+__device__ __forceinline__ uint32_t dpp_max_step(uint32_t v, uint32_t w) { return v > w ? v : w; }
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        uint32_t w = __shfl_xor(v, o, kWave);
-        v = v > w ? v : w;
-    }
-    return v;
+    v = dpp_max_step(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    v = dpp_max_step(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    v = dpp_max_step(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    v = dpp_max_step(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    v = dpp_max_step(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v = dpp_max_step(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
+// 64-bit max as two 32-bit maxes: the high words, then the low words of the lanes at it.
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        uint64_t w = __shfl_xor(v, o, kWave);
-        v = v > w ? v : w;
-    }
-    return v;
+    const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
+    const uint32_t mh = wave_max_u32(hi);
+    const uint32_t ml = wave_max_u32(hi == mh ? lo : 0u);
+    return ((uint64_t)mh << 32) | ml;
 }
 
 // Best key of a wave's 64 nodes (lane l holds node base + l): the max total and, among
@@ -187,6 +207,7 @@ int max_pods_per_scan_wg();
 int block_nodes();
 hipError_t launch_batch(const EngineArgs& a, hipStream_t st, hipEvent_t e_scan0, hipEvent_t e_scan1,
                         hipEvent_t e_res1);
+hipError_t launch_rescale_memory(const NodeSoA& s, int64_t n_pad, PodRec* pods, int64_t P, hipStream_t st);
 hipError_t launch_eval_pod(const Cfg& c, const NodeSoA& s, const PodRec* pod, uint32_t filters, uint8_t* mask,
                            int64_t* score, hipStream_t st);
 hipError_t launch_flush(const NodeSoA& s, const PodRec* pods, const int64_t* fin, int64_t t, int64_t n_done,

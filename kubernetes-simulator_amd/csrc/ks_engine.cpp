@@ -8,6 +8,11 @@
 //    (kubesim/pod/pod.go:67-69), i.e. for dur = ceil(S / tick) ticks.  Its expiry is attached
 //    to the first later pod whose bind tick reaches t0 + dur; the device applies it (if q was
 //    bound Ok) right before that pod is scheduled.
+//  * memory scale: memory quantities arrive in milli-bytes; while every node capacity and pod
+//    request is a whole number of bytes the device holds bytes instead (x1/1000 — exact, and
+//    every fit / LeastRequested / BalancedAllocation result is unit-free), which keeps the
+//    BalancedAllocation products inside 64 bits.  A later fractional-byte request switches the
+//    device back to milli-bytes once (rescale_memory_kernel).
 //  * batching: launches (expire_head, scan, resolve) triples until the device counter says
 //    every pod due in [tick+1, tick+ticks] is bound, then copies the binds back.
 // Placements themselves are decided on the device only.
@@ -100,6 +105,7 @@ struct ks_engine {
         pending;  // (finish tick, pod) not yet attached to a later pod
     int64_t P = 0, F = 0;
     int64_t last_arrival = 0;
+    int64_t mem_div = 1000;  // device memory unit = milli-bytes / mem_div
 
     // progress
     int64_t tick = 0, done = 0, usage_lo = 0;
@@ -205,10 +211,10 @@ ks_status ks_create(const ks_config* cfg, ks_engine** out) {
     e->dc.tick_seconds = cfg->tick_seconds;
     hipError_t r = hipSetDevice(e->device);
     if (r == hipSuccess) r = hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking);
-    if (r == hipSuccess) r = hipMalloc(&e->d_ctr, 8 * sizeof(int64_t));
-    if (r == hipSuccess) r = hipHostMalloc(&e->h_ctr, 8 * sizeof(int64_t), hipHostMallocDefault);
+    if (r == hipSuccess) r = hipMalloc(&e->d_ctr, 16 * sizeof(int64_t));
+    if (r == hipSuccess) r = hipHostMalloc(&e->h_ctr, 16 * sizeof(int64_t), hipHostMallocDefault);
     for (int i = 0; i < 4 && r == hipSuccess; i++) r = hipEventCreate(&e->ev[i]);
-    if (r == hipSuccess) r = hipMemsetAsync(e->d_ctr, 0, 8 * sizeof(int64_t), e->st);
+    if (r == hipSuccess) r = hipMemsetAsync(e->d_ctr, 0, 16 * sizeof(int64_t), e->st);
     if (r == hipSuccess) r = hipStreamSynchronize(e->st);
     if (r != hipSuccess) {
         delete e;
@@ -257,10 +263,14 @@ ks_status ks_load_nodes(ks_engine* e, int64_t n, const int64_t* alloc, const uin
     e->nwb = (int)(e->n_pad / 64);
     const int64_t np = e->n_pad;
     // host staging in SoA order: ac am ag ap rc rm rg nr taint label
+    e->mem_div = 1000;
+    for (int64_t i = 0; i < n; i++)
+        if (alloc[i * 4 + 1] > 0 && alloc[i * 4 + 1] % 1000 != 0) e->mem_div = 1;
     std::vector<int64_t> h(10 * np, 0);
     for (int64_t i = 0; i < np; i++) {
         const bool real = i < n;
         for (int k = 0; k < 4; k++) h[k * np + i] = real ? alloc[i * 4 + k] : (k == 3 ? 0 : -1);
+        if (real && h[np + i] > 0) h[np + i] /= e->mem_div;
         h[8 * np + i] = real ? (int64_t)taint[i] : 0;
         h[9 * np + i] = real ? (int64_t)label[i] : 0;
     }
@@ -315,6 +325,16 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
     for (int64_t f = 0; f < nf * 3; f++)
         if (phase_use[f] < 0 || phase_use[f] >= kMaxValue) return fail(e, KS_EINVAL, "usage out of range");
 
+    if (e->mem_div != 1) {
+        bool frac = false;
+        for (int64_t i = 0; i < m && !frac; i++) frac = (keymask[i] & 2) && req[i * 3 + 1] % e->mem_div != 0;
+        if (frac) {
+            HIPCHK(e, hipSetDevice(e->device));
+            HIPCHK(e, ks::launch_rescale_memory(e->s, e->n_pad, e->pods.p, e->P, e->st));
+            HIPCHK(e, hipStreamSynchronize(e->st));
+            e->mem_div = 1;
+        }
+    }
     std::vector<ks::PodRec> recs(m);
     std::vector<int32_t> dur(m), poff(m), cum(nf);
     std::vector<int64_t> t0(m), fin(m), eoff(m);
@@ -326,6 +346,7 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
         ks::PodRec& r = recs[i];
         const uint8_t km = keymask[i] & 7;
         for (int k = 0; k < 3; k++) r.req[k] = (km >> k & 1) ? req[i * 3 + k] : 0;
+        r.req[1] /= e->mem_div;
         r.tol = tol[i];
         r.sel = sel[i];
         r.keymask = km;
@@ -542,6 +563,14 @@ const char* ks_last_error(const ks_engine* e) { return e ? e->errmsg.c_str() : "
 ks_status ks_last_step_stats(const ks_engine* e, ks_step_stats* out) {
     if (!e || !out) return KS_EINVAL;
     *out = e->stats;
+    return KS_OK;
+}
+
+ks_status ks_debug_counters(ks_engine* e, int64_t* out16) {
+    if (!e || !out16) return KS_EINVAL;
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipMemcpyAsync(out16, e->d_ctr, 16 * sizeof(int64_t), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
     return KS_OK;
 }
 

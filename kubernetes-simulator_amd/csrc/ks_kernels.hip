@@ -34,6 +34,8 @@ constexpr int kTMax = 768;               // touched-node table (LDS)
 constexpr int kHash = 2048;              // open-addressing node -> entry map (LDS)
 constexpr int kMaxBatchR = 256;          // pods per resolve launch
 constexpr int kMaxExp = kTMax - kMaxBatchR;  // expiries pre-inserted per batch
+constexpr int kFilterBits = 1 << 16;     // touched filter indexed by node & 0xFFFF (no false
+                                         // negatives; exact below 65,536 nodes)
 
 enum : int64_t { kCtrStart = 0, kCtrEnd = 1, kCtrErr = 2, kCtrErrPod = 3, kCtrEarly = 4 };
 enum : uint32_t { kFlagBadKey = 1, kFlagBadSpec = 2 };
@@ -201,11 +203,33 @@ struct ResolveShared {
     int32_t ex_q[kMaxExp];
     int32_t ex_node[kMaxExp];
     int32_t ex_ok[kMaxExp];
+    int32_t ex_entry[kMaxExp];  // table entry of the expiry's node (q bound before the batch)
+    int64_t ex_req[kMaxExp][3];
+    int32_t lb_entry[kMaxBatchR];
+    uint32_t tfilt[kFilterBits / 32];
     uint64_t red[kResolveWaves];
+    int32_t red_e[kResolveWaves];
     int32_t n_t, stop, committed, err_code, err_pod, nb;
 };
 
 __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Diagnostic build only (-DKS_STAMPS): per-phase cycle sums of the resolver's wave 0, written
+// to ctr[8..15]; the real kernel executes no stamp.
+#ifdef KS_STAMPS
+__device__ __forceinline__ uint64_t stamp() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define KS_STAMP(var) uint64_t var = stamp()
+#define KS_ACC(slot, a, b) acc[slot] += (b) - (a)
+#else
+#define KS_STAMP(var)
+#define KS_ACC(slot, a, b)
+#endif
 
 __device__ __forceinline__ uint32_t hslot(int32_t node) { return ((uint32_t)node * 2654435761u) >> (32 - 11); }
 
@@ -227,6 +251,15 @@ __device__ __forceinline__ void h_insert(ResolveShared& sh, int32_t node, int32_
     while (sh.hkey[s] != -1) s = (s + 1) & (kHash - 1);
     sh.hkey[s] = node;
     sh.hval[s] = idx;
+    const uint32_t f = (uint32_t)node & (kFilterBits - 1);
+    sh.tfilt[f >> 5] |= 1u << (f & 31);
+}
+
+// touched? — one LDS read unless the filter bit is shared with another node
+__device__ __forceinline__ bool is_touched(const ResolveShared& sh, int32_t node) {
+    const uint32_t f = (uint32_t)node & (kFilterBits - 1);
+    if (!((sh.tfilt[f >> 5] >> (f & 31)) & 1u)) return false;
+    return h_find(sh, node) >= 0;
 }
 
 __device__ __forceinline__ NodeV t_node(const ResolveShared& sh, int e) {
@@ -255,7 +288,7 @@ __device__ __forceinline__ int32_t key_node(uint64_t key) { return (int32_t)(0xF
 // `full` = the list holds L candidates (so "none" means exhausted, not "no candidates").
 __device__ __forceinline__ int first_untouched(const ResolveShared& sh, int i, int lane, bool& full) {
     const uint64_t c = lane < kL ? sh.cand[i][lane] : 0ull;
-    const bool ok = c != 0 && h_find(sh, key_node(c)) < 0;
+    const bool ok = c != 0 && !is_touched(sh, key_node(c));
     const uint64_t m = __ballot(ok);
     full = __popcll(__ballot(c != 0)) == kL;
     return m ? __ffsll((unsigned long long)m) - 1 : -1;
@@ -282,6 +315,7 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
         sh.n_t = 0; sh.stop = 0; sh.committed = lo; sh.err_code = 0; sh.err_pod = -1;
     }
     for (int h = tid; h < kHash; h += kResolveThreads) sh.hkey[h] = -1;
+    for (int w = tid; w < kFilterBits / 32; w += kResolveThreads) sh.tfilt[w] = 0;
     __syncthreads();
     nb = sh.nb;
     const int64_t e_cnt = nb > 1 ? a.exp_off[start + nb] - e_base : 0;
@@ -299,6 +333,9 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
         if (q < start) {
             sh.ex_node[e] = a.b_node[q];
             sh.ex_ok[e] = (a.b_status[q] == 0) && !a.expired[q];
+            sh.ex_req[e][0] = a.pods[q].req[0];
+            sh.ex_req[e][1] = a.pods[q].req[1];
+            sh.ex_req[e][2] = a.pods[q].req[2];
         } else {
             sh.ex_node[e] = -1;
             sh.ex_ok[e] = 0;
@@ -317,13 +354,16 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
                 const int l = __ffsll((unsigned long long)m) - 1;
                 m &= m - 1;
                 const int32_t nd = __shfl(mine, l, kWave);
-                if (lane == 0 && h_find(sh, nd) < 0) {
-                    const int idx = sh.n_t;
-                    sh.tnode[idx] = nd;
-                    h_insert(sh, nd, idx);
-                    sh.n_t = idx + 1;
+                if (lane == 0) {
+                    int idx = h_find(sh, nd);
+                    if (idx < 0) {
+                        idx = sh.n_t;
+                        sh.tnode[idx] = nd;
+                        h_insert(sh, nd, idx);
+                        sh.n_t = idx + 1;
+                    }
+                    sh.ex_entry[e0 + l] = idx;
                 }
-                lds_fence();
             }
         }
     }
@@ -348,50 +388,64 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
         if (pa >= 0 && lane < 10) fa = node_field(a.s, lane, key_node(sh.cand[0][pa]));
     }
 
+#ifdef KS_STAMPS
+    uint64_t acc[4] = {0, 0, 0, 0};
+#endif
     for (int i = 0; i < nb; ++i) {
         const int64_t j = start + i;
+        KS_STAMP(s0);
         // ---- phase A (wave 0): the expiries due before pod j binds (nodes already in the table)
         if (wave == 0 && i > 0 && !sh.stop) {
             for (int e = sh.ex_off[i]; e < sh.ex_off[i + 1]; ++e) {
                 const int32_t q = sh.ex_q[e];
-                int32_t nd;
+                int t;
                 bool ok;
-                if (q >= start) { nd = sh.lb_node[q - start]; ok = sh.lb_stat[q - start] == 0; }
-                else { nd = sh.ex_node[e]; ok = sh.ex_ok[e] != 0; }
+                if (q >= start) { t = sh.lb_entry[q - start]; ok = sh.lb_stat[q - start] == 0; }
+                else { t = sh.ex_entry[e]; ok = sh.ex_ok[e] != 0; }
                 if (!ok) continue;
                 if (lane == 0) {
-                    const int t = h_find(sh, nd);
                     int64_t r0, r1, r2;
                     if (q >= start) { r0 = sh.pod[q - start].req[0]; r1 = sh.pod[q - start].req[1]; r2 = sh.pod[q - start].req[2]; }
-                    else { r0 = a.pods[q].req[0]; r1 = a.pods[q].req[1]; r2 = a.pods[q].req[2]; }
+                    else { r0 = sh.ex_req[e][0]; r1 = sh.ex_req[e][1]; r2 = sh.ex_req[e][2]; }
                     sh.ts[4][t] -= r0; sh.ts[5][t] -= r1; sh.ts[6][t] -= r2; sh.ts[7][t] -= 1;
                     a.expired[q] = 1;
                 }
-                lds_fence();
             }
         }
+        KS_STAMP(s1);
         __syncthreads();
         if (sh.stop) break;
+        KS_STAMP(s2);
 
         // ---- phase B (all waves): exact keys of the touched nodes; wave 0 adds the list's
         // best untouched key
         const PodRec p = sh.pod[i];
         const uint64_t kkey = (wave == 0 && pa >= 0) ? sh.cand[i][pa] : 0ull;
-        uint64_t best = (wave == 0 && lane == 0) ? kkey : 0ull;
+        uint64_t best = 0;
+        int bent = -1;
         const int nt = sh.n_t;
         for (int e = tid; e < nt; e += kResolveThreads) {
             const uint32_t t1 = eval_total1(a.c, p, t_node(sh, e));
             const uint64_t k = make_key(t1, (uint32_t)sh.tnode[e]);
-            best = best > k ? best : k;
+            if (k > best) { best = k; bent = e; }
         }
-        best = wave_max_u64(best);
-        if (lane == 0) sh.red[wave] = best;
+        // wave max of (key, entry); the list candidate (entry -1) competes in wave 0
+        const uint64_t wbest = wave_max_u64(best);
+        const uint64_t who = __ballot(best == wbest && wbest != 0);
+        int went = who ? __builtin_amdgcn_readlane(bent, __ffsll((unsigned long long)who) - 1) : -1;
+        uint64_t wkey = wbest;
+        if (wave == 0 && kkey > wkey) { wkey = kkey; went = -1; }
+        if (lane == 0) { sh.red[wave] = wkey; sh.red_e[wave] = went; }
+        KS_STAMP(s3);
         __syncthreads();
+        KS_STAMP(s4);
 
         // ---- phase C (wave 0): argmax, CreatePod admission, bind; prefetch for pod i+1
         if (wave == 0) {
-            uint64_t v = lane < kResolveWaves ? sh.red[lane] : 0ull;
-            v = wave_max_u64(v);
+            const uint64_t rv = lane < kResolveWaves ? sh.red[lane] : 0ull;
+            const uint64_t v = wave_max_u64(rv);
+            const uint64_t wl = __ballot(rv == v && v != 0);
+            const int went = wl ? sh.red_e[__ffsll((unsigned long long)wl) - 1] : -1;
             if (pa < 0 && pfull) {
                 // every list entry is touched: the untouched maximum is unknown -> rescan
                 if (lane == 0) { sh.stop = 1; sh.committed = i; }
@@ -402,14 +456,13 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
             } else {
                 const int32_t nd = key_node(v);
                 int t;
-                if (v == kkey) {
+                if (went < 0) {
                     // the untouched list candidate: becomes a touched entry with its snapshot state
                     t = sh.n_t;
                     if (lane < 10) t_store_field(sh, t, lane, fa);
                     if (lane == 0) { sh.tnode[t] = nd; h_insert(sh, nd, t); sh.n_t = t + 1; }
-                    lds_fence();
                 } else {
-                    t = h_find(sh, nd);
+                    t = went;
                 }
                 const NodeV n = t_node(sh, t);
                 const bool ok = fits(p, n);
@@ -421,19 +474,29 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
                         sh.ts[6][t] += p.req[2]; sh.ts[7][t] += 1;
                     }
                     sh.lb_node[i] = nd;
+                    sh.lb_entry[i] = t;
                     sh.lb_stat[i] = ok ? 0 : 1;
                     a.b_node[j] = nd;
                     a.b_status[j] = ok ? 0 : 1;
                 }
-                lds_fence();
             }
             if (i + 1 < nb) {
                 pa = first_untouched(sh, i + 1, lane, pfull);
                 if (pa >= 0 && lane < 10) fa = node_field(a.s, lane, key_node(sh.cand[i + 1][pa]));
             }
         }
+        KS_STAMP(s5);
+        KS_ACC(0, s0, s1);   // phase A
+        KS_ACC(1, s2, s3);   // phase B (own work)
+        KS_ACC(2, s3, s4);   // barrier wait after B
+        KS_ACC(3, s4, s5);   // phase C
     }
     __syncthreads();
+#ifdef KS_STAMPS
+    if (tid == 0)
+        for (int k = 0; k < 4; ++k) atomicAdd((unsigned long long*)&a.ctr[8 + k], (unsigned long long)acc[k]);
+    if (tid == 0) atomicAdd((unsigned long long*)&a.ctr[12], (unsigned long long)nb);
+#endif
 
     // ---- write back the mutable fields of every touched node
     for (int e = tid; e < sh.n_t; e += kResolveThreads) {
@@ -509,6 +572,18 @@ __global__ __launch_bounds__(256) void usage_kernel(int64_t q_lo, int64_t q_hi, 
     }
 }
 
+// Switch the device's memory unit from bytes to milli-bytes (x1000): node capacity and
+// requested totals, and every pod's memory request.  Runs at most once per engine, when a pod
+// with a fractional-byte memory request arrives (see ks_engine.cpp, memory scale).
+__global__ __launch_bounds__(256) void rescale_memory_kernel(NodeSoA s, int64_t n_pad, PodRec* pods, int64_t P) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad; i += stride) {
+        if (s.am[i] >= 0) s.am[i] *= 1000;
+        s.rm[i] *= 1000;
+    }
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < P; q += stride) pods[q].req[1] *= 1000;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Launchers, called by ks_engine.cpp.
 // ---------------------------------------------------------------------------------------------
@@ -526,6 +601,11 @@ hipError_t launch_batch(const EngineArgs& a, hipStream_t st, hipEvent_t e_scan0,
     if (e_scan1) (void)hipEventRecord(e_scan1, st);
     hipLaunchKernelGGL(resolve_kernel, dim3(1), dim3(kResolveThreads), 0, st, a);
     if (e_res1) (void)hipEventRecord(e_res1, st);
+    return hipGetLastError();
+}
+
+hipError_t launch_rescale_memory(const NodeSoA& s, int64_t n_pad, PodRec* pods, int64_t P, hipStream_t st) {
+    hipLaunchKernelGGL(rescale_memory_kernel, dim3(1024), dim3(256), 0, st, s, n_pad, pods, P);
     return hipGetLastError();
 }
 

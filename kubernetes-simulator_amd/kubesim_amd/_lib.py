@@ -25,7 +25,7 @@ STATUS_NAMES = {KS_OK: "OK", KS_EINVAL: "InvalidArgument", KS_ENOTFOUND: "NotFou
 # every symbol include/ks_engine.h declares
 EXPORTED_SYMBOLS = ("ks_create", "ks_destroy", "ks_load_nodes", "ks_submit_pods", "ks_step",
                     "ks_filter", "ks_score", "ks_usage", "ks_current_tick", "ks_queued_pods",
-                    "ks_last_error", "ks_last_step_stats", "ks_set_profiling")
+                    "ks_last_error", "ks_last_step_stats", "ks_set_profiling", "ks_debug_counters")
 
 
 class KsScorer(C.Structure):
@@ -79,6 +79,8 @@ def load():
     L.ks_last_error.restype = C.c_char_p
     L.ks_last_step_stats.argtypes = [p, C.POINTER(KsStepStats)]
     L.ks_last_step_stats.restype = C.c_int
+    L.ks_debug_counters.argtypes = [p, p]
+    L.ks_debug_counters.restype = C.c_int
     L.ks_set_profiling.argtypes = [p, C.c_int]
     L.ks_set_profiling.restype = None
     _lib = L

@@ -142,6 +142,11 @@ class Engine:
         return dict(step_ms=s.step_ms, scan_ms=s.scan_ms, resolve_ms=s.resolve_ms, launches=s.launches,
                     pods=s.pods)
 
+    def debug_counters(self):
+        out = np.zeros(16, np.int64)
+        self._check(self._L.ks_debug_counters(self.h, _p(out)))
+        return out
+
     def set_profiling(self, on: bool):
         self._L.ks_set_profiling(self.h, 1 if on else 0)
 

@@ -92,7 +92,7 @@ def test_short_pods_many_expiries():
     tr = small_trace(11, n_nodes=2000, n_pods=6000, taints=False, selectors=False, tolerations=False)
     p = tr["pods"]
     p["phase_sec"][:] = 1 + (np.arange(len(p["phase_sec"])) % 12)
-    _lockstep(tr, "feeds_all_lrba", 6000, batch_pods=512, chunk=1500)
+    _lockstep(tr, "feeds_all_lrba", 6000, batch_pods=256, chunk=1500)
 
 
 def test_filter_score_match_oracle():
@@ -119,9 +119,10 @@ def test_list_exhaustion_forces_rescan():
     tr = small_trace(21, n_nodes=300, n_pods=900, taints=False, labels=False, tolerations=False,
                      selectors=False)
     nd, p = tr["nodes"], tr["pods"]
-    nd["alloc"][:] = nd["alloc"][0]
-    nd["alloc_has"][:] = 15
     p["req"][:] = p["req"][0]
+    nd["alloc"][:, :3] = 4 * p["req"][0]   # each bind drops the node's LeastRequested score
+    nd["alloc"][:, 3] = 110
+    nd["alloc_has"][:] = 15
     mode = "feeds_fit_lr"
     enc = encoded(tr)
     eng = make_engine(tr, enc, mode, 256)
@@ -133,3 +134,25 @@ def test_list_exhaustion_forces_rescan():
     assert_same_binds(eb, ob)
     assert erc == orc
     assert eng.last_step_stats()["launches"] > 900 // 256 + 2  # early commits happened
+
+
+def test_memory_unit_rescale_mid_run():
+    """Memory is held in bytes while every quantity is whole bytes; a later pod requesting a
+    fractional byte (e.g. memory "1.5") switches the device to milli-bytes mid-run.  Results
+    must not change."""
+    tr = small_trace(31, n_nodes=500, n_pods=1200, taints=False, selectors=False, tolerations=False)
+    tr["pods"]["req"][700:, 1] += 1  # +1 milli-byte: not a whole byte
+    mode = "feeds_all_lrba"
+    enc = encoded(tr)
+    eng = make_engine(tr, enc, mode, 256)
+    ora = make_oracle(tr, mode)
+    from kubesim_amd import encode as E
+    for lo, hi in ((0, 600), (600, 1200)):
+        part = tracegen.slice_pods(tr, lo, hi)
+        eng.submit(E.encode_pods(part["pods"], enc["taint_dict"], enc["label_dict"]))
+        ora.submit(part)
+        eb, erc = engine_run(eng, 600, 600)
+        ob, orc = oracle_run(ora, 600)
+        assert_same_binds(eb, ob)
+        assert erc == orc
+        np.testing.assert_array_equal(eng.usage(), ora.usage())
