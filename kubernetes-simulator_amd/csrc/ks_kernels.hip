@@ -187,6 +187,19 @@ __global__ __launch_bounds__(256) void merge_kernel(EngineArgs a) {
 
 // ------------------------------------------------------------------------------------------
 // resolve: one workgroup, sequential over the batch in FIFO order (one bind per tick).
+//
+// One barrier per pod.  After the barrier every wave derives pod i's winner from the
+// double-buffered partial maxima red[i&1] (identical decision in every wave, including
+// NotFound / InvalidArgument / exhausted-list stops).  Then, until the next barrier, the waves
+// split the bind of pod i and the evaluation of pod i+1:
+//   wave 0   table insert of an untouched winner; walk pod i+1's top-L list against the
+//            table; stage the snapshot fields of its best untouched node in LDS
+//   wave 1   CreatePod admission + bind on the winner's entry (and pod i+1's expiries that
+//            land on it); outputs; pod i+1's exact key on that entry
+//   wave 2   pod i+1's other expiries; pod i+1's exact keys on those entries
+//   3..15    pod i+1's exact keys on every other touched entry
+// The writers (waves 1, 2) touch disjoint entries and every reader skips them, so the
+// overlap is race-free.
 // ------------------------------------------------------------------------------------------
 struct ResolveShared {
     int64_t ts[8][kTMax];       // touched-node state: ac am ag ap rc rm rg nr
@@ -194,28 +207,30 @@ struct ResolveShared {
     int32_t tnode[kTMax];
     int32_t hkey[kHash];        // node id or -1
     int32_t hval[kHash];        // entry index
+    uint32_t tfilt[kFilterBits / 32];
     PodRec pod[kMaxBatchR];
     int32_t dur[kMaxBatchR];
     uint64_t cand[kMaxBatchR][kL];
     int32_t lb_node[kMaxBatchR];
     int32_t lb_stat[kMaxBatchR];
+    int32_t lb_entry[kMaxBatchR];
     int32_t ex_off[kMaxBatchR + 1];
     int32_t ex_q[kMaxExp];
     int32_t ex_node[kMaxExp];
     int32_t ex_ok[kMaxExp];
     int32_t ex_entry[kMaxExp];  // table entry of the expiry's node (q bound before the batch)
     int64_t ex_req[kMaxExp][3];
-    int32_t lb_entry[kMaxBatchR];
-    uint32_t tfilt[kFilterBits / 32];
-    uint64_t red[kResolveWaves];
-    int32_t red_e[kResolveWaves];
-    int32_t n_t, stop, committed, err_code, err_pod, nb;
+    // per-pod hand-offs, double-buffered by pod parity
+    uint64_t red[2][kResolveWaves];
+    int32_t red_e[2][kResolveWaves];
+    int64_t stage[2][10];       // snapshot fields of the pod's best untouched list node
+    int32_t kfull[2];           // every entry of a full list touched: the batch must stop
+    int32_t ntab[2];            // table size when the pod is evaluated
+    int32_t n_t, committed, err_code, err_pod, nb;
 };
 
-__device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-
-// Diagnostic build only (-DKS_STAMPS): per-phase cycle sums of the resolver's wave 0, written
-// to ctr[8..15]; the real kernel executes no stamp.
+// Diagnostic build only (-DKS_STAMPS): per-iteration cycle sums of waves 0, 1 and 3, written
+// to ctr[8..12]; the real kernel executes no stamp.
 #ifdef KS_STAMPS
 __device__ __forceinline__ uint64_t stamp() {
     uint64_t t;
@@ -225,10 +240,8 @@ __device__ __forceinline__ uint64_t stamp() {
     return t;
 }
 #define KS_STAMP(var) uint64_t var = stamp()
-#define KS_ACC(slot, a, b) acc[slot] += (b) - (a)
 #else
 #define KS_STAMP(var)
-#define KS_ACC(slot, a, b)
 #endif
 
 __device__ __forceinline__ uint32_t hslot(int32_t node) { return ((uint32_t)node * 2654435761u) >> (32 - 11); }
@@ -270,16 +283,20 @@ __device__ __forceinline__ NodeV t_node(const ResolveShared& sh, int e) {
     return v;
 }
 
+__device__ __forceinline__ NodeV stage_node(const ResolveShared& sh, int b) {
+    NodeV v;
+    v.ac = sh.stage[b][0]; v.am = sh.stage[b][1]; v.ag = sh.stage[b][2]; v.ap = sh.stage[b][3];
+    v.rc = sh.stage[b][4]; v.rm = sh.stage[b][5]; v.rg = sh.stage[b][6]; v.nr = sh.stage[b][7];
+    v.taint = (uint64_t)sh.stage[b][8]; v.label = (uint64_t)sh.stage[b][9];
+    return v;
+}
+
 __device__ __forceinline__ int64_t node_field(const NodeSoA& s, int f, int64_t i) {
     switch (f) {
         case 0: return s.ac[i]; case 1: return s.am[i]; case 2: return s.ag[i]; case 3: return s.ap[i];
         case 4: return s.rc[i]; case 5: return s.rm[i]; case 6: return s.rg[i]; case 7: return s.nr[i];
         case 8: return (int64_t)s.taint[i]; default: return (int64_t)s.label[i];
     }
-}
-
-__device__ __forceinline__ void t_store_field(ResolveShared& sh, int e, int f, int64_t v) {
-    if (f < 8) sh.ts[f][e] = v; else sh.tu[f - 8][e] = (uint64_t)v;
 }
 
 __device__ __forceinline__ int32_t key_node(uint64_t key) { return (int32_t)(0xFFFFFFFFu - (uint32_t)key); }
@@ -292,6 +309,28 @@ __device__ __forceinline__ int first_untouched(const ResolveShared& sh, int i, i
     const uint64_t m = __ballot(ok);
     full = __popcll(__ballot(c != 0)) == kL;
     return m ? __ffsll((unsigned long long)m) - 1 : -1;
+}
+
+// Table entry an expiry of the window lands on and whether it applies (the pod bound Ok and
+// not yet expired).  Not for the pod bound in the current iteration (its lb_* are pending).
+__device__ __forceinline__ void expiry_target(const ResolveShared& sh, int e, int64_t start, int& t, bool& ok) {
+    const int32_t q = sh.ex_q[e];
+    if (q >= start) { t = sh.lb_entry[q - start]; ok = sh.lb_stat[q - start] == 0; }
+    else { t = sh.ex_entry[e]; ok = sh.ex_ok[e] != 0; }
+}
+
+__device__ __forceinline__ void expiry_req(const ResolveShared& sh, int e, int64_t start, int64_t& r0, int64_t& r1,
+                                           int64_t& r2) {
+    const int32_t q = sh.ex_q[e];
+    if (q >= start) { r0 = sh.pod[q - start].req[0]; r1 = sh.pod[q - start].req[1]; r2 = sh.pod[q - start].req[2]; }
+    else { r0 = sh.ex_req[e][0]; r1 = sh.ex_req[e][1]; r2 = sh.ex_req[e][2]; }
+}
+
+// wave-wide max of (key, entry) pairs: the key decides, the entry follows it
+__device__ __forceinline__ void wave_best_entry(uint64_t key, int ent, uint64_t& wkey, int& went) {
+    wkey = wave_max_u64(key);
+    const uint64_t who = __ballot(key == wkey && wkey != 0);
+    went = who ? __builtin_amdgcn_readlane(ent, __ffsll((unsigned long long)who) - 1) : -1;
 }
 
 __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) {
@@ -312,7 +351,7 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
             if (a.exp_off[start + mid] - e_base <= kMaxExp) lo = mid; else hi = mid - 1;
         }
         sh.nb = lo;
-        sh.n_t = 0; sh.stop = 0; sh.committed = lo; sh.err_code = 0; sh.err_pod = -1;
+        sh.n_t = 0; sh.committed = lo; sh.err_code = 0; sh.err_pod = -1;
     }
     for (int h = tid; h < kHash; h += kResolveThreads) sh.hkey[h] = -1;
     for (int w = tid; w < kFilterBits / 32; w += kResolveThreads) sh.tfilt[w] = 0;
@@ -330,6 +369,7 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
     for (int e = tid; e < e_cnt; e += kResolveThreads) {
         const int32_t q = a.exp_pod[e_base + e];
         sh.ex_q[e] = q;
+        sh.ex_entry[e] = -1;
         if (q < start) {
             sh.ex_node[e] = a.b_node[q];
             sh.ex_ok[e] = (a.b_status[q] == 0) && !a.expired[q];
@@ -376,130 +416,187 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
     }
     __syncthreads();
 
-    // Wave 0 keeps the next pod's best untouched list entry and, in lanes 0-9, its snapshot
-    // fields — fetched one pod ahead, so the bind of an untouched node never waits on HBM.
-    // The touched table only grows at a bind, and the prefetch runs after the bind, so the
-    // entry is exact when the pod is resolved.
-    int pa = -1;
-    bool pfull = false;
-    int64_t fa = 0;
+    // ---- prologue: pod 0's partial maxima
     if (wave == 0) {
-        pa = first_untouched(sh, 0, lane, pfull);
-        if (pa >= 0 && lane < 10) fa = node_field(a.s, lane, key_node(sh.cand[0][pa]));
+        bool full;
+        const int pa = first_untouched(sh, 0, lane, full);
+        if (pa >= 0 && lane < 10) sh.stage[0][lane] = node_field(a.s, lane, key_node(sh.cand[0][pa]));
+        if (lane == 0) {
+            sh.red[0][0] = pa >= 0 ? sh.cand[0][pa] : 0ull;
+            sh.red_e[0][0] = -1;
+            sh.kfull[0] = pa < 0 && full;
+            sh.ntab[0] = sh.n_t;
+        }
+    } else {
+        const PodRec p0 = sh.pod[0];
+        const int nt0 = sh.n_t;
+        uint64_t best = 0;
+        int bent = -1;
+        for (int e = tid - kWave; e < nt0; e += kResolveThreads - kWave) {
+            const uint64_t k = make_key(eval_total1(a.c, p0, t_node(sh, e)), (uint32_t)sh.tnode[e]);
+            if (k > best) { best = k; bent = e; }
+        }
+        uint64_t wk;
+        int we;
+        wave_best_entry(best, bent, wk, we);
+        if (lane == 0) { sh.red[0][wave] = wk; sh.red_e[0][wave] = we; }
     }
+    __syncthreads();
 
 #ifdef KS_STAMPS
-    uint64_t acc[4] = {0, 0, 0, 0};
+    uint64_t acc_work = 0, acc_wait = 0;
 #endif
-    for (int i = 0; i < nb; ++i) {
-        const int64_t j = start + i;
+    int i = 0;
+    for (; i < nb; ++i) {
         KS_STAMP(s0);
-        // ---- phase A (wave 0): the expiries due before pod j binds (nodes already in the table)
-        if (wave == 0 && i > 0 && !sh.stop) {
-            for (int e = sh.ex_off[i]; e < sh.ex_off[i + 1]; ++e) {
-                const int32_t q = sh.ex_q[e];
-                int t;
-                bool ok;
-                if (q >= start) { t = sh.lb_entry[q - start]; ok = sh.lb_stat[q - start] == 0; }
-                else { t = sh.ex_entry[e]; ok = sh.ex_ok[e] != 0; }
-                if (!ok) continue;
+        const int64_t j = start + i;
+        const int cur = i & 1, nxt = cur ^ 1;
+        // ---- every wave: pod i's winner and the stop decision (identical in all waves)
+        const uint64_t rv = lane < kResolveWaves ? sh.red[cur][lane] : 0ull;
+        const uint64_t v = wave_max_u64(rv);
+        const uint64_t wl = __ballot(rv == v && v != 0);
+        const int went = wl ? sh.red_e[cur][__ffsll((unsigned long long)wl) - 1] : -1;
+        const PodRec p = sh.pod[i];
+        int stop = 0;
+        if (sh.kfull[cur]) stop = 1;                                       // list exhausted: rescan
+        else if (v == 0) stop = 2;                                         // NotFound
+        else if (p.flags & (kFlagBadKey | kFlagBadSpec)) stop = 3;         // InvalidArgument
+        if (stop) {
+            if (tid == 0) {
+                sh.committed = i;
+                if (stop > 1) { sh.err_code = stop == 2 ? kErrNotFound : kErrEinval; sh.err_pod = (int32_t)j; }
+            }
+            break;
+        }
+        const int nt = sh.ntab[cur];
+        const int32_t nd = key_node(v);
+        const int t = went >= 0 ? went : nt;  // an untouched winner becomes entry nt
+        const bool has_next = i + 1 < nb;
+        const int e0 = has_next ? sh.ex_off[i + 1] : 0, e1 = has_next ? sh.ex_off[i + 2] : 0;
+
+        if (wave == 0) {
+            if (lane == 0) {
+                if (went < 0) { sh.tnode[t] = nd; h_insert(sh, nd, t); }
+                sh.ntab[nxt] = went < 0 ? nt + 1 : nt;
+            }
+            if (has_next) {
+                bool full;
+                const int pa = first_untouched(sh, i + 1, lane, full);
+                if (pa >= 0 && lane < 10) sh.stage[nxt][lane] = node_field(a.s, lane, key_node(sh.cand[i + 1][pa]));
                 if (lane == 0) {
-                    int64_t r0, r1, r2;
-                    if (q >= start) { r0 = sh.pod[q - start].req[0]; r1 = sh.pod[q - start].req[1]; r2 = sh.pod[q - start].req[2]; }
-                    else { r0 = sh.ex_req[e][0]; r1 = sh.ex_req[e][1]; r2 = sh.ex_req[e][2]; }
-                    sh.ts[4][t] -= r0; sh.ts[5][t] -= r1; sh.ts[6][t] -= r2; sh.ts[7][t] -= 1;
-                    a.expired[q] = 1;
+                    sh.red[nxt][0] = pa >= 0 ? sh.cand[i + 1][pa] : 0ull;
+                    sh.red_e[nxt][0] = -1;
+                    sh.kfull[nxt] = pa < 0 && full;
                 }
             }
+        } else if (wave == 1) {
+            NodeV n = went >= 0 ? t_node(sh, t) : stage_node(sh, cur);
+            const bool ok = fits(p, n);  // CreatePod admission (kubesim/node/node.go:44-47)
+            if (ok && sh.dur[i] > 0) { n.rc += p.req[0]; n.rm += p.req[1]; n.rg += p.req[2]; n.nr += 1; }
+            for (int e = e0; e < e1; ++e) {  // pod i+1's expiries on this entry (pod i's own included)
+                const int32_t q = sh.ex_q[e];
+                int tq;
+                bool okq;
+                if (q == j) { tq = t; okq = ok; }
+                else expiry_target(sh, e, start, tq, okq);
+                if (tq != t || !okq) continue;
+                int64_t r0, r1, r2;
+                if (q == j) { r0 = p.req[0]; r1 = p.req[1]; r2 = p.req[2]; }
+                else expiry_req(sh, e, start, r0, r1, r2);
+                n.rc -= r0; n.rm -= r1; n.rg -= r2; n.nr -= 1;
+                if (lane == 0) a.expired[q] = 1;
+            }
+            if (lane == 0) {
+                if (went < 0) {
+                    sh.ts[0][t] = n.ac; sh.ts[1][t] = n.am; sh.ts[2][t] = n.ag; sh.ts[3][t] = n.ap;
+                    sh.tu[0][t] = n.taint; sh.tu[1][t] = n.label;
+                }
+                sh.ts[4][t] = n.rc; sh.ts[5][t] = n.rm; sh.ts[6][t] = n.rg; sh.ts[7][t] = n.nr;
+                sh.lb_node[i] = nd; sh.lb_entry[i] = t; sh.lb_stat[i] = ok ? 0 : 1;
+                a.b_node[j] = nd;
+                a.b_status[j] = ok ? 0 : 1;
+            }
+            if (has_next) {
+                const uint32_t t1 = eval_total1(a.c, sh.pod[i + 1], n);
+                if (lane == 0) { sh.red[nxt][1] = make_key(t1, (uint32_t)nd); sh.red_e[nxt][1] = t; }
+            }
+        } else if (wave == 2) {
+            if (has_next) {
+                if (lane == 0) {
+                    for (int e = e0; e < e1; ++e) {
+                        const int32_t q = sh.ex_q[e];
+                        if (q == j) continue;
+                        int tq;
+                        bool okq;
+                        expiry_target(sh, e, start, tq, okq);
+                        if (tq < 0 || tq == t || !okq) continue;
+                        int64_t r0, r1, r2;
+                        expiry_req(sh, e, start, r0, r1, r2);
+                        sh.ts[4][tq] -= r0; sh.ts[5][tq] -= r1; sh.ts[6][tq] -= r2; sh.ts[7][tq] -= 1;
+                        a.expired[q] = 1;
+                    }
+                }
+                const PodRec pn = sh.pod[i + 1];
+                uint64_t best = 0;
+                int bent = -1;
+                for (int e = e0 + lane; e < e1; e += kWave) {
+                    if (sh.ex_q[e] == j) continue;
+                    int tq;
+                    bool okq;
+                    expiry_target(sh, e, start, tq, okq);
+                    if (tq < 0 || tq == t) continue;
+                    const uint64_t k = make_key(eval_total1(a.c, pn, t_node(sh, tq)), (uint32_t)sh.tnode[tq]);
+                    if (k > best) { best = k; bent = tq; }
+                }
+                uint64_t wk;
+                int we;
+                wave_best_entry(best, bent, wk, we);
+                if (lane == 0) { sh.red[nxt][2] = wk; sh.red_e[nxt][2] = we; }
+            }
+        } else if (has_next) {
+            const PodRec pn = sh.pod[i + 1];
+            uint64_t best = 0;
+            int bent = -1;
+            for (int e = tid - 3 * kWave; e < nt; e += kResolveThreads - 3 * kWave) {
+                if (e == went) continue;  // wave 1 owns the winner's entry
+                bool mine = true;          // wave 2 owns the entries pod i+1's expiries land on
+                for (int x = e0; x < e1 && mine; ++x) {
+                    if (sh.ex_q[x] == j) continue;
+                    int tq;
+                    bool okq;
+                    expiry_target(sh, x, start, tq, okq);
+                    mine = tq != e;
+                }
+                if (!mine) continue;
+                const uint64_t k = make_key(eval_total1(a.c, pn, t_node(sh, e)), (uint32_t)sh.tnode[e]);
+                if (k > best) { best = k; bent = e; }
+            }
+            uint64_t wk;
+            int we;
+            wave_best_entry(best, bent, wk, we);
+            if (lane == 0) { sh.red[nxt][wave] = wk; sh.red_e[nxt][wave] = we; }
         }
         KS_STAMP(s1);
         __syncthreads();
-        if (sh.stop) break;
         KS_STAMP(s2);
-
-        // ---- phase B (all waves): exact keys of the touched nodes; wave 0 adds the list's
-        // best untouched key
-        const PodRec p = sh.pod[i];
-        const uint64_t kkey = (wave == 0 && pa >= 0) ? sh.cand[i][pa] : 0ull;
-        uint64_t best = 0;
-        int bent = -1;
-        const int nt = sh.n_t;
-        for (int e = tid; e < nt; e += kResolveThreads) {
-            const uint32_t t1 = eval_total1(a.c, p, t_node(sh, e));
-            const uint64_t k = make_key(t1, (uint32_t)sh.tnode[e]);
-            if (k > best) { best = k; bent = e; }
-        }
-        // wave max of (key, entry); the list candidate (entry -1) competes in wave 0
-        const uint64_t wbest = wave_max_u64(best);
-        const uint64_t who = __ballot(best == wbest && wbest != 0);
-        int went = who ? __builtin_amdgcn_readlane(bent, __ffsll((unsigned long long)who) - 1) : -1;
-        uint64_t wkey = wbest;
-        if (wave == 0 && kkey > wkey) { wkey = kkey; went = -1; }
-        if (lane == 0) { sh.red[wave] = wkey; sh.red_e[wave] = went; }
-        KS_STAMP(s3);
-        __syncthreads();
-        KS_STAMP(s4);
-
-        // ---- phase C (wave 0): argmax, CreatePod admission, bind; prefetch for pod i+1
-        if (wave == 0) {
-            const uint64_t rv = lane < kResolveWaves ? sh.red[lane] : 0ull;
-            const uint64_t v = wave_max_u64(rv);
-            const uint64_t wl = __ballot(rv == v && v != 0);
-            const int went = wl ? sh.red_e[__ffsll((unsigned long long)wl) - 1] : -1;
-            if (pa < 0 && pfull) {
-                // every list entry is touched: the untouched maximum is unknown -> rescan
-                if (lane == 0) { sh.stop = 1; sh.committed = i; }
-            } else if (v == 0) {
-                if (lane == 0) { sh.stop = 1; sh.committed = i; sh.err_code = kErrNotFound; sh.err_pod = (int32_t)j; }
-            } else if (p.flags & kFlagBadKey) {
-                if (lane == 0) { sh.stop = 1; sh.committed = i; sh.err_code = kErrEinval; sh.err_pod = (int32_t)j; }
-            } else {
-                const int32_t nd = key_node(v);
-                int t;
-                if (went < 0) {
-                    // the untouched list candidate: becomes a touched entry with its snapshot state
-                    t = sh.n_t;
-                    if (lane < 10) t_store_field(sh, t, lane, fa);
-                    if (lane == 0) { sh.tnode[t] = nd; h_insert(sh, nd, t); sh.n_t = t + 1; }
-                } else {
-                    t = went;
-                }
-                const NodeV n = t_node(sh, t);
-                const bool ok = fits(p, n);
-                if (p.flags & kFlagBadSpec) {
-                    if (lane == 0) { sh.stop = 1; sh.committed = i; sh.err_code = kErrEinval; sh.err_pod = (int32_t)j; }
-                } else if (lane == 0) {
-                    if (ok && sh.dur[i] > 0) {
-                        sh.ts[4][t] += p.req[0]; sh.ts[5][t] += p.req[1];
-                        sh.ts[6][t] += p.req[2]; sh.ts[7][t] += 1;
-                    }
-                    sh.lb_node[i] = nd;
-                    sh.lb_entry[i] = t;
-                    sh.lb_stat[i] = ok ? 0 : 1;
-                    a.b_node[j] = nd;
-                    a.b_status[j] = ok ? 0 : 1;
-                }
-            }
-            if (i + 1 < nb) {
-                pa = first_untouched(sh, i + 1, lane, pfull);
-                if (pa >= 0 && lane < 10) fa = node_field(a.s, lane, key_node(sh.cand[i + 1][pa]));
-            }
-        }
-        KS_STAMP(s5);
-        KS_ACC(0, s0, s1);   // phase A
-        KS_ACC(1, s2, s3);   // phase B (own work)
-        KS_ACC(2, s3, s4);   // barrier wait after B
-        KS_ACC(3, s4, s5);   // phase C
+#ifdef KS_STAMPS
+        acc_work += s1 - s0;
+        acc_wait += s2 - s1;
+#endif
     }
     __syncthreads();
 #ifdef KS_STAMPS
-    if (tid == 0)
-        for (int k = 0; k < 4; ++k) atomicAdd((unsigned long long*)&a.ctr[8 + k], (unsigned long long)acc[k]);
-    if (tid == 0) atomicAdd((unsigned long long*)&a.ctr[12], (unsigned long long)nb);
+    if (lane == 0 && (wave == 0 || wave == 1 || wave == 3)) {
+        const int slot = wave == 0 ? 8 : (wave == 1 ? 10 : 11);
+        atomicAdd((unsigned long long*)&a.ctr[slot], (unsigned long long)acc_work);
+        if (wave == 0) atomicAdd((unsigned long long*)&a.ctr[9], (unsigned long long)acc_wait);
+    }
+    if (tid == 0) atomicAdd((unsigned long long*)&a.ctr[12], (unsigned long long)i);
 #endif
 
     // ---- write back the mutable fields of every touched node
-    for (int e = tid; e < sh.n_t; e += kResolveThreads) {
+    const int n_final = sh.ntab[sh.committed & 1];
+    for (int e = tid; e < n_final; e += kResolveThreads) {
         const int64_t nd = sh.tnode[e];
         a.s.rc[nd] = sh.ts[4][e];
         a.s.rm[nd] = sh.ts[5][e];

@@ -20,5 +20,5 @@ c1 = eng.debug_counters()
 d = c1 - c0
 pods = d[12]
 print(f"B={B} pods={pods} wall {dt*1e3:.1f} ms  -> {32768/dt:.0f} pods/s")
-for k, name in enumerate(["phaseA", "phaseB", "barrierB", "phaseC"]):
-    print(f"  {name:9s} {d[8+k]/max(pods,1):9.0f} cycles/pod")
+for k, name in enumerate(["wave0 work", "wave0 wait", "wave1 work", "wave3 work"]):
+    print(f"  {name:11s} {d[8+k]/max(pods,1):9.0f} cycles/pod")
