@@ -444,7 +444,7 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
     __syncthreads();
 
 #ifdef KS_STAMPS
-    uint64_t acc_work = 0, acc_wait = 0;
+    uint64_t acc_work = 0, acc_wait = 0, acc_sub[4] = {0, 0, 0, 0};
 #endif
     int i = 0;
     for (; i < nb; ++i) {
@@ -468,6 +468,10 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
             }
             break;
         }
+        KS_STAMP(sw);
+#ifdef KS_STAMPS
+        acc_sub[0] += sw - s0;
+#endif
         const int nt = sh.ntab[cur];
         const int32_t nd = key_node(v);
         const int t = went >= 0 ? went : nt;  // an untouched winner becomes entry nt
@@ -568,13 +572,27 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
                     mine = tq != e;
                 }
                 if (!mine) continue;
+#ifdef KS_STAMPS
+                const NodeV nn = t_node(sh, e);
+                KS_STAMP(sa);
+                const uint32_t tt1 = eval_total1(a.c, pn, nn);
+                KS_STAMP(sb);
+                if (wave == 3 && e == tid - 3 * kWave) { acc_sub[1] += sa - sw; acc_sub[2] += sb - sa; }
+                const uint64_t k = make_key(tt1, (uint32_t)sh.tnode[e]);
+#else
                 const uint64_t k = make_key(eval_total1(a.c, pn, t_node(sh, e)), (uint32_t)sh.tnode[e]);
+#endif
                 if (k > best) { best = k; bent = e; }
             }
+            KS_STAMP(sc);
             uint64_t wk;
             int we;
             wave_best_entry(best, bent, wk, we);
             if (lane == 0) { sh.red[nxt][wave] = wk; sh.red_e[nxt][wave] = we; }
+            KS_STAMP(sd);
+#ifdef KS_STAMPS
+            acc_sub[3] += sd - sc;
+#endif
         }
         KS_STAMP(s1);
         __syncthreads();
@@ -592,6 +610,9 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
         if (wave == 0) atomicAdd((unsigned long long*)&a.ctr[9], (unsigned long long)acc_wait);
     }
     if (tid == 0) atomicAdd((unsigned long long*)&a.ctr[12], (unsigned long long)i);
+    if (tid == 3 * kWave)
+        for (int k = 0; k < 3; ++k) atomicAdd((unsigned long long*)&a.ctr[13 + k], (unsigned long long)acc_sub[k + 1]);
+    if (tid == 3 * kWave) atomicAdd((unsigned long long*)&a.ctr[7], (unsigned long long)acc_sub[0]);
 #endif
 
     // ---- write back the mutable fields of every touched node

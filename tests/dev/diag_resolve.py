@@ -22,3 +22,5 @@ pods = d[12]
 print(f"B={B} pods={pods} wall {dt*1e3:.1f} ms  -> {32768/dt:.0f} pods/s")
 for k, name in enumerate(["wave0 work", "wave0 wait", "wave1 work", "wave3 work"]):
     print(f"  {name:11s} {d[8+k]/max(pods,1):9.0f} cycles/pod")
+for k, name in ((7, "w3 winner"), (13, "w3 excl+ld"), (14, "w3 eval"), (15, "w3 reduce")):
+    print(f"  {name:11s} {d[k]/max(pods,1):9.0f} cycles/pod")
