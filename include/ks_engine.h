@@ -81,8 +81,13 @@ typedef struct {
     ks_scorer scorers[8];
     int32_t device;       /* HIP device ordinal */
     int32_t batch_pods;   /* pods resolved per scan (0 = default) */
-    int32_t reserved[8];
+    uint32_t engine_flags; /* KS_ENGINE_* */
+    int32_t reserved[7];
 } ks_config;
+
+/* engine_flags: FORCE_WIDE keeps the 64/128-bit evaluator even when every scaled capacity fits
+ * the 32-bit one (both are exact; this exists to test them against each other). */
+enum { KS_ENGINE_FORCE_WIDE = 1 };
 
 typedef struct {
     int64_t pod;    /* FIFO index (submission order) */

@@ -147,7 +147,79 @@ __host__ __device__ __forceinline__ uint32_t eval_total1(const Cfg& c, const Pod
     return (uint32_t)total + 1u;
 }
 
-__device__ __forceinline__ uint64_t make_key(uint32_t total1, uint32_t node) {
+// ---------------------------------------------------------------------------------------------
+// Narrow evaluator.  The host holds every resource in units of the gcd of all its quantities
+// (exact: every fit / LeastRequested / BalancedAllocation result is unit-free) and selects this
+// variant when every scaled capacity is below 2^29 (ks_engine.cpp, resource scale).  Requests
+// are clamped to 2^30 — any request above every capacity behaves identically — so sums stay in
+// int32, the 32x32 products in 64 bits, and each integer floor is a float estimate (error far
+// below 1) corrected exactly by one 64-bit compare on each side.
+// ---------------------------------------------------------------------------------------------
+constexpr int64_t kNarrowCap = 1LL << 29;
+constexpr int64_t kNarrowReq = 1LL << 30;
+
+__host__ __device__ __forceinline__ int32_t clamp_req(int64_t q) { return (int32_t)(q < kNarrowReq ? q : kNarrowReq); }
+
+// floor(10 x / A) for 0 <= x <= A < 2^29
+__host__ __device__ __forceinline__ int32_t lr_frac10(uint32_t x, uint32_t A) {
+    int32_t q = (int32_t)(10.0f * (float)x / (float)A);
+    q = q < 0 ? 0 : (q > 10 ? 10 : q);
+    const uint64_t y = (uint64_t)x * 10u, t = (uint64_t)(uint32_t)q * A;
+    if (y < t) q -= 1;
+    else if (y >= t + A) q += 1;
+    return q;
+}
+
+__host__ __device__ __forceinline__ int32_t lr_one_n(int32_t A, int32_t u) {
+    if (A <= 0 || u > A) return 0;
+    return lr_frac10((uint32_t)(A - u), (uint32_t)A);
+}
+
+// floor(10 (D - X) / D), D = Ac Am < 2^58, X = |uc Am - um Ac| < D
+__host__ __device__ __forceinline__ int32_t ba_score_n(int32_t Ac, int32_t Am, int32_t uc, int32_t um) {
+    if (Ac <= 0 || Am <= 0 || uc >= Ac || um >= Am) return 0;
+    const uint64_t D = (uint64_t)(uint32_t)Ac * (uint32_t)Am;
+    const uint64_t a = (uint64_t)(uint32_t)uc * (uint32_t)Am, b = (uint64_t)(uint32_t)um * (uint32_t)Ac;
+    const uint64_t X = a > b ? a - b : b - a;
+    int32_t q = (int32_t)(10.0f - 10.0f * ((float)X / (float)D));
+    q = q < 0 ? 0 : (q > 10 ? 10 : q);
+    const uint64_t y = (D - X) * 10u, t = (uint64_t)(uint32_t)q * D;
+    if (y < t) q -= 1;
+    else if (y >= t + D) q += 1;
+    return q;
+}
+
+__host__ __device__ __forceinline__ uint32_t eval_total1_narrow(const Cfg& c, const PodRec& p, const NodeV& n) {
+    if (!c.has_scorers) return 0;
+    const int32_t ac = (int32_t)n.ac, am = (int32_t)n.am, ag = (int32_t)n.ag;
+    const int32_t rc = (int32_t)n.rc, rm = (int32_t)n.rm, rg = (int32_t)n.rg;
+    const int32_t qc = clamp_req(p.req[0]), qm = clamp_req(p.req[1]), qg = clamp_req(p.req[2]);
+    if (c.filter_feeds) {
+        bool ok = true;
+        if (c.filters & kFilterFit) {
+            ok &= n.nr < n.ap;
+            if (p.keymask & 1) ok &= rc + qc <= ac;
+            if (p.keymask & 2) ok &= rm + qm <= am;
+            if (p.keymask & 4) ok &= rg + qg <= ag;
+        }
+        if (c.filters & kFilterTaint) ok &= (n.taint & ~p.tol) == 0;
+        if (c.filters & kFilterSelector) ok &= (n.label & p.sel) == p.sel;
+        if (!ok) return 0;
+    }
+    const int32_t uc = rc + qc, um = rm + qm;
+    int32_t total = c.const_total;
+    if (c.w_lr) total += c.w_lr * ((lr_one_n(ac, uc) + lr_one_n(am, um)) >> 1);
+    if (c.w_ba) total += c.w_ba * ba_score_n(ac, am, uc, um);
+    return (uint32_t)total + 1u;
+}
+
+template <bool kNarrow>
+__host__ __device__ __forceinline__ uint32_t eval_t(const Cfg& c, const PodRec& p, const NodeV& n) {
+    if constexpr (kNarrow) return eval_total1_narrow(c, p, n);
+    else return eval_total1(c, p, n);
+}
+
+__host__ __device__ __forceinline__ uint64_t make_key(uint32_t total1, uint32_t node) {
     return total1 ? (((uint64_t)total1 << 32) | (uint64_t)(0xFFFFFFFFu - node)) : 0ull;
 }
 
@@ -190,6 +262,7 @@ struct EngineArgs {
     const int32_t* dur;      // ticks a bound-Ok pod runs (0: never counted)
     const int64_t* exp_off;  // [P+1]: expiries due before pod j binds
     const int32_t* exp_pod;
+    const int64_t* exp_pos;  // [P]: index in exp_pod of pod q's own expiry, -1 if none yet
     int32_t* b_node;
     int32_t* b_status;
     uint8_t* expired;
@@ -205,11 +278,11 @@ struct EngineArgs {
 int max_batch_pods();
 int max_pods_per_scan_wg();
 int block_nodes();
-hipError_t launch_batch(const EngineArgs& a, hipStream_t st, hipEvent_t e_scan0, hipEvent_t e_scan1,
+hipError_t launch_batch(const EngineArgs& a, bool narrow, hipStream_t st, hipEvent_t e_scan0, hipEvent_t e_scan1,
                         hipEvent_t e_res1);
-hipError_t launch_rescale_memory(const NodeSoA& s, int64_t n_pad, PodRec* pods, int64_t P, hipStream_t st);
+hipError_t launch_rescale(const NodeSoA& s, int64_t n_pad, PodRec* pods, int64_t P, const int64_t f[3], hipStream_t st);
 hipError_t launch_eval_pod(const Cfg& c, const NodeSoA& s, const PodRec* pod, uint32_t filters, uint8_t* mask,
-                           int64_t* score, hipStream_t st);
+                           int64_t* score, bool narrow, hipStream_t st);
 hipError_t launch_flush(const NodeSoA& s, const PodRec* pods, const int64_t* fin, int64_t t, int64_t n_done,
                         const int32_t* b_node, const int32_t* b_status, uint8_t* expired, hipStream_t st);
 hipError_t launch_usage(int64_t q_lo, int64_t q_hi, int64_t t, int32_t tick_s, const int32_t* b_node,

@@ -8,17 +8,18 @@
 //    (kubesim/pod/pod.go:67-69), i.e. for dur = ceil(S / tick) ticks.  Its expiry is attached
 //    to the first later pod whose bind tick reaches t0 + dur; the device applies it (if q was
 //    bound Ok) right before that pod is scheduled.
-//  * memory scale: memory quantities arrive in milli-bytes; while every node capacity and pod
-//    request is a whole number of bytes the device holds bytes instead (x1/1000 — exact, and
-//    every fit / LeastRequested / BalancedAllocation result is unit-free), which keeps the
-//    BalancedAllocation products inside 64 bits.  A later fractional-byte request switches the
-//    device back to milli-bytes once (rescale_memory_kernel).
+//  * resource scale: quantities arrive in milli-units; the device holds resource k in units of
+//    g_k = gcd of every capacity and request of k seen so far (exact: every fit / LeastRequested
+//    / BalancedAllocation result is unit-free).  A pod whose request g_k does not divide shrinks
+//    the unit (rescale_kernel multiplies the device state by g_k / g_k').  When every scaled
+//    capacity is < 2^29 the kernels use the narrow (32-bit) evaluator, else the 64/128-bit one.
 //  * batching: launches (expire_head, scan, resolve) triples until the device counter says
 //    every pod due in [tick+1, tick+ticks] is bound, then copies the binds back.
 // Placements themselves are decided on the device only.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <numeric>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -94,7 +95,7 @@ struct ks_engine {
     // pods (device)
     DVec<ks::PodRec> pods;
     DVec<int32_t> dur, b_node, b_status, phase_off, cum_sec, exp_pod;
-    DVec<int64_t> exp_off, t0, fin, use;
+    DVec<int64_t> exp_off, t0, fin, use, exp_pos;
     DVec<uint8_t> expired;
     // pods (host mirror of placement-independent facts)
     std::vector<int64_t> h_bind_tick, h_fin;
@@ -105,7 +106,11 @@ struct ks_engine {
         pending;  // (finish tick, pod) not yet attached to a later pod
     int64_t P = 0, F = 0;
     int64_t last_arrival = 0;
-    int64_t mem_div = 1000;  // device memory unit = milli-bytes / mem_div
+    int64_t scale[3] = {1, 1, 1};   // device unit of cpu / memory / gpu, in milli-units
+    int64_t max_alloc[3] = {0, 0, 0};  // largest capacity per resource, milli-units
+    bool narrow = false;
+    bool force_wide = false;
+    std::vector<int64_t> h_exp_pos;  // global exp_pod index holding pod q's own expiry, or -1
 
     // progress
     int64_t tick = 0, done = 0, usage_lo = 0;
@@ -156,6 +161,7 @@ ks::EngineArgs make_args(ks_engine* e) {
     a.dur = e->dur.p;
     a.exp_off = e->exp_off.p;
     a.exp_pod = e->exp_pod.p;
+    a.exp_pos = e->exp_pos.p;
     a.b_node = e->b_node.p;
     a.b_status = e->b_status.p;
     a.expired = e->expired.p;
@@ -166,6 +172,12 @@ ks::EngineArgs make_args(ks_engine* e) {
     a.B = e->B;
     a.PG = e->PG;
     return a;
+}
+
+void update_narrow(ks_engine* e) {
+    bool ok = !e->force_wide;
+    for (int k = 0; k < 3; k++) ok &= e->max_alloc[k] / e->scale[k] < ks::kNarrowCap;
+    e->narrow = ok;
 }
 
 }  // namespace
@@ -182,6 +194,7 @@ ks_status ks_create(const ks_config* cfg, ks_engine** out) {
     if (cfg->filters & ~7u) return KS_EINVAL;
     if (cfg->n_scorers < 0 || cfg->n_scorers > 8) return KS_EINVAL;
     if (cfg->batch_pods < 0 || cfg->batch_pods > kMaxBatch) return KS_EINVAL;
+    if (cfg->engine_flags & ~(uint32_t)KS_ENGINE_FORCE_WIDE) return KS_EINVAL;
     int64_t const_total = 0, w_lr = 0, w_ba = 0;
     for (int i = 0; i < cfg->n_scorers; i++) {
         const ks_scorer& sc = cfg->scorers[i];
@@ -202,6 +215,7 @@ ks_status ks_create(const ks_config* cfg, ks_engine** out) {
     e->cfg = *cfg;
     e->device = cfg->device;
     e->B = cfg->batch_pods ? cfg->batch_pods : kDefaultBatch;
+    e->force_wide = (cfg->engine_flags & KS_ENGINE_FORCE_WIDE) != 0;
     e->dc.filter_feeds = cfg->filter_mode == KS_FILTER_FEEDS_SCORE;
     e->dc.filters = cfg->filters;
     e->dc.has_scorers = cfg->n_scorers > 0;
@@ -230,7 +244,7 @@ void ks_destroy(ks_engine* e) {
     if (e->st) (void)hipStreamSynchronize(e->st);
     e->pods.release(); e->dur.release(); e->b_node.release(); e->b_status.release();
     e->phase_off.release(); e->cum_sec.release(); e->exp_pod.release(); e->exp_off.release();
-    e->t0.release(); e->fin.release(); e->use.release(); e->expired.release();
+    e->t0.release(); e->fin.release(); e->use.release(); e->expired.release(); e->exp_pos.release();
     if (e->node_mem) (void)hipFree(e->node_mem);
     if (e->lists) (void)hipFree(e->lists);
     if (e->cand) (void)hipFree(e->cand);
@@ -263,14 +277,22 @@ ks_status ks_load_nodes(ks_engine* e, int64_t n, const int64_t* alloc, const uin
     e->nwb = (int)(e->n_pad / 64);
     const int64_t np = e->n_pad;
     // host staging in SoA order: ac am ag ap rc rm rg nr taint label
-    e->mem_div = 1000;
-    for (int64_t i = 0; i < n; i++)
-        if (alloc[i * 4 + 1] > 0 && alloc[i * 4 + 1] % 1000 != 0) e->mem_div = 1;
+    for (int k = 0; k < 3; k++) {
+        int64_t g = 0, mx = 0;
+        for (int64_t i = 0; i < n; i++) {
+            const int64_t v = alloc[i * 4 + k];
+            if (v > 0) { g = std::gcd(g, v); mx = std::max(mx, v); }
+        }
+        e->scale[k] = g > 0 ? g : 1;
+        e->max_alloc[k] = mx;
+    }
+    update_narrow(e);
     std::vector<int64_t> h(10 * np, 0);
     for (int64_t i = 0; i < np; i++) {
         const bool real = i < n;
         for (int k = 0; k < 4; k++) h[k * np + i] = real ? alloc[i * 4 + k] : (k == 3 ? 0 : -1);
-        if (real && h[np + i] > 0) h[np + i] /= e->mem_div;
+        for (int k = 0; k < 3; k++)
+            if (real && h[k * np + i] > 0) h[k * np + i] /= e->scale[k];
         h[8 * np + i] = real ? (int64_t)taint[i] : 0;
         h[9 * np + i] = real ? (int64_t)label[i] : 0;
     }
@@ -325,14 +347,22 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
     for (int64_t f = 0; f < nf * 3; f++)
         if (phase_use[f] < 0 || phase_use[f] >= kMaxValue) return fail(e, KS_EINVAL, "usage out of range");
 
-    if (e->mem_div != 1) {
-        bool frac = false;
-        for (int64_t i = 0; i < m && !frac; i++) frac = (keymask[i] & 2) && req[i * 3 + 1] % e->mem_div != 0;
-        if (frac) {
+    {
+        int64_t f[3] = {1, 1, 1};
+        bool any = false;
+        for (int k = 0; k < 3; k++) {
+            int64_t g = e->scale[k];
+            for (int64_t i = 0; i < m; i++)
+                if ((keymask[i] >> k & 1) && req[i * 3 + k] > 0) g = std::gcd(g, req[i * 3 + k]);
+            f[k] = e->scale[k] / g;
+            any |= f[k] != 1;
+            e->scale[k] = g;
+        }
+        if (any) {
             HIPCHK(e, hipSetDevice(e->device));
-            HIPCHK(e, ks::launch_rescale_memory(e->s, e->n_pad, e->pods.p, e->P, e->st));
+            HIPCHK(e, ks::launch_rescale(e->s, e->n_pad, e->pods.p, e->P, f, e->st));
             HIPCHK(e, hipStreamSynchronize(e->st));
-            e->mem_div = 1;
+            update_narrow(e);
         }
     }
     std::vector<ks::PodRec> recs(m);
@@ -340,13 +370,15 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
     std::vector<int64_t> t0(m), fin(m), eoff(m);
     std::vector<int32_t> epod;
     epod.reserve(m);
+    const int64_t epod_base = e->exp_pod.n;
+    e->h_exp_pos.resize(e->P + m, -1);
+    int64_t pos_lo = e->P;  // lowest pod whose expiry position changed
     int64_t prev_bind = e->P ? e->h_bind_tick[e->P - 1] : e->tick;
     for (int64_t i = 0; i < m; i++) {
         const int64_t j = e->P + i;
         ks::PodRec& r = recs[i];
         const uint8_t km = keymask[i] & 7;
-        for (int k = 0; k < 3; k++) r.req[k] = (km >> k & 1) ? req[i * 3 + k] : 0;
-        r.req[1] /= e->mem_div;
+        for (int k = 0; k < 3; k++) r.req[k] = (km >> k & 1) ? req[i * 3 + k] / e->scale[k] : 0;
         r.tol = tol[i];
         r.sel = sel[i];
         r.keymask = km;
@@ -367,7 +399,10 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
         poff[i] = (int32_t)(e->F + phase_off[i]);
         // expiries due before pod j binds: finish tick in (bind_tick[j-1], bind_tick[j]]
         while (!e->pending.empty() && e->pending.top().first <= bt) {
-            epod.push_back((int32_t)e->pending.top().second);
+            const int64_t q = e->pending.top().second;
+            e->h_exp_pos[q] = epod_base + (int64_t)epod.size();
+            pos_lo = std::min(pos_lo, q);
+            epod.push_back((int32_t)q);
             e->pending.pop();
         }
         eoff[i] = e->h_exp_off.back() + (int64_t)epod.size();
@@ -398,6 +433,10 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
     }
     HIPCHK(e, e->exp_off.append(eoff.data(), m, st));
     HIPCHK(e, e->exp_pod.append(epod.data(), (int64_t)epod.size(), st));
+    HIPCHK(e, e->exp_pos.reserve(e->P + m, st));
+    HIPCHK(e, hipMemcpyAsync(e->exp_pos.p + pos_lo, e->h_exp_pos.data() + pos_lo, sizeof(int64_t) * (e->P + m - pos_lo),
+                             hipMemcpyHostToDevice, st));
+    e->exp_pos.n = e->P + m;
     HIPCHK(e, hipStreamSynchronize(st));  // host staging vectors die here
     e->h_bind_tick.insert(e->h_bind_tick.end(), t0.begin(), t0.end());
     e->h_fin.insert(e->h_fin.end(), fin.begin(), fin.end());
@@ -450,7 +489,7 @@ ks_status ks_step(ks_engine* e, int64_t ticks, ks_bind* out, int64_t cap, int64_
                 e1 = e->prof_ev[3 * launches + 1];
                 e2 = e->prof_ev[3 * launches + 2];
             }
-            HIPCHK(e, ks::launch_batch(a, st, e0, e1, e2));
+            HIPCHK(e, ks::launch_batch(a, e->narrow, st, e0, e1, e2));
             launches++;
         }
         HIPCHK(e, hipMemcpyAsync(e->h_ctr, e->d_ctr, 5 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
@@ -519,7 +558,7 @@ static ks_status eval_pod(ks_engine* e, int64_t pod) {
     ks_status r = flush_expiries(e);
     if (r != KS_OK) return r;
     if (e->n == 0) return KS_OK;
-    HIPCHK(e, ks::launch_eval_pod(e->dc, e->s, e->pods.p + pod, e->cfg.filters, e->d_mask, e->d_score, e->st));
+    HIPCHK(e, ks::launch_eval_pod(e->dc, e->s, e->pods.p + pod, e->cfg.filters, e->d_mask, e->d_score, e->narrow, e->st));
     return KS_OK;
 }
 

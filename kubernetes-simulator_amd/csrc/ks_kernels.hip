@@ -18,6 +18,9 @@
 //                list scores below every list entry.  winner = max(those).  If all L entries
 //                are touched the batch commits early and the next batch rescans.
 //
+// Every kernel that evaluates exists twice: kNarrow = true is the 32-bit evaluator, used when
+// every scaled capacity fits (ks_device.h); kNarrow = false the general 64/128-bit one.
+//
 // Packed key: (total + 1) << 32 | (0xFFFFFFFF - node); 0 = no candidate (NotFound).  Max key =
 // highest total, ties to the lowest node index.
 #include "ks_device.h"
@@ -30,12 +33,15 @@ constexpr int kL = kTopL;                // candidate list length per pod
 constexpr int kMaxPG = 32;               // pods per scan workgroup (LDS list staging)
 constexpr int kResolveThreads = 1024;    // 16 waves
 constexpr int kResolveWaves = kResolveThreads / kWave;
-constexpr int kTMax = 768;               // touched-node table (LDS)
+constexpr int kOwnerWave0 = 3;           // waves 3..15 own the touched entries
+constexpr int kOwners = kResolveThreads - kOwnerWave0 * kWave;
+constexpr int kTMax = 768;               // touched-node table (LDS); <= kOwners
 constexpr int kHash = 2048;              // open-addressing node -> entry map (LDS)
 constexpr int kMaxBatchR = 256;          // pods per resolve launch
 constexpr int kMaxExp = kTMax - kMaxBatchR;  // expiries pre-inserted per batch
 constexpr int kFilterBits = 1 << 16;     // touched filter indexed by node & 0xFFFF (no false
                                          // negatives; exact below 65,536 nodes)
+static_assert(kTMax <= kOwners, "one touched entry per owner thread");
 
 enum : int64_t { kCtrStart = 0, kCtrEnd = 1, kCtrErr = 2, kCtrErrPod = 3, kCtrEarly = 4 };
 enum : uint32_t { kFlagBadKey = 1, kFlagBadSpec = 2 };
@@ -72,6 +78,7 @@ __global__ __launch_bounds__(256) void expire_head_kernel(EngineArgs a) {
 // (lowest lanes first), repeat below it — a 32-bit wave max + ballot per class.  The four
 // wave lists are then merged by rank (each list is sorted) into the block's top-L.
 // ------------------------------------------------------------------------------------------
+template <bool kNarrow>
 __global__ __launch_bounds__(256) void scan_kernel(EngineArgs a) {
     __shared__ uint64_t wl[kMaxPG][kScanWaves][kL];  // per-pod, per-wave top-L lists
     const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
@@ -89,7 +96,7 @@ __global__ __launch_bounds__(256) void scan_kernel(EngineArgs a) {
     const int np = (int)min<int64_t>(a.PG, nb - pg0);
     for (int b = 0; b < np; ++b) {
         const PodRec p = a.pods[start + pg0 + b];
-        uint32_t rem = valid ? eval_total1(a.c, p, n) : 0u;
+        uint32_t rem = valid ? eval_t<kNarrow>(a.c, p, n) : 0u;
         int cnt = 0;
         for (int r = 0; r < kL && cnt < kL; ++r) {
             const uint32_t m = wave_max_u32(rem);
@@ -189,48 +196,52 @@ __global__ __launch_bounds__(256) void merge_kernel(EngineArgs a) {
 // resolve: one workgroup, sequential over the batch in FIFO order (one bind per tick).
 //
 // One barrier per pod.  After the barrier every wave derives pod i's winner from the
-// double-buffered partial maxima red[i&1] (identical decision in every wave, including
+// double-buffered partial maxima red[i&1] (identical decision in every wave, including the
 // NotFound / InvalidArgument / exhausted-list stops).  Then, until the next barrier, the waves
 // split the bind of pod i and the evaluation of pod i+1:
-//   wave 0   table insert of an untouched winner; walk pod i+1's top-L list against the
-//            table; stage the snapshot fields of its best untouched node in LDS
-//   wave 1   CreatePod admission + bind on the winner's entry (and pod i+1's expiries that
-//            land on it); outputs; pod i+1's exact key on that entry
-//   wave 2   pod i+1's other expiries; pod i+1's exact keys on those entries
-//   3..15    pod i+1's exact keys on every other touched entry
-// The writers (waves 1, 2) touch disjoint entries and every reader skips them, so the
-// overlap is race-free.
+//   wave 0    table insert of an untouched winner; walk pod i+1's top-L list against the
+//             table; stage the snapshot fields of its best untouched node in LDS
+//   wave 1    CreatePod admission + bind on the winner's entry (and pod i+1's expiries that
+//             land on it); outputs; pod i+1's exact key on that entry
+//   wave 2    pod i+1's other expiries; pod i+1's exact keys on those entries
+//   3..15     owner threads: thread r keeps touched entry r in registers (reloading the
+//             mutable fields when an entry was modified the iteration before) and computes pod
+//             i+1's exact key on it, unless wave 1 or 2 owns the entry this iteration
+// Writers (waves 1, 2) touch disjoint entries and every reader of those skips them.
 // ------------------------------------------------------------------------------------------
+struct alignas(16) RedSlot {
+    uint64_t key;
+    int32_t ent;  // touched-table entry, -1 = the list candidate
+    int32_t pad;
+};
+
 struct ResolveShared {
     int64_t ts[8][kTMax];       // touched-node state: ac am ag ap rc rm rg nr
     uint64_t tu[2][kTMax];      // taint label
     int32_t tnode[kTMax];
+    int32_t dirty[kTMax];       // iteration at which the owner must reload the mutable fields
     int32_t hkey[kHash];        // node id or -1
     int32_t hval[kHash];        // entry index
     uint32_t tfilt[kFilterBits / 32];
     PodRec pod[kMaxBatchR];
     int32_t dur[kMaxBatchR];
+    int32_t exp_slot[kMaxBatchR];  // window slot of an in-batch pod's own expiry, or -1
     uint64_t cand[kMaxBatchR][kL];
-    int32_t lb_node[kMaxBatchR];
-    int32_t lb_stat[kMaxBatchR];
-    int32_t lb_entry[kMaxBatchR];
     int32_t ex_off[kMaxBatchR + 1];
     int32_t ex_q[kMaxExp];
     int32_t ex_node[kMaxExp];
-    int32_t ex_ok[kMaxExp];
-    int32_t ex_entry[kMaxExp];  // table entry of the expiry's node (q bound before the batch)
+    int32_t ex_ok[kMaxExp];     // the expiring pod was bound Ok and has not expired yet
+    int32_t ex_entry[kMaxExp];  // table entry of its node (set at the bind for in-batch pods)
     int64_t ex_req[kMaxExp][3];
-    // per-pod hand-offs, double-buffered by pod parity
-    uint64_t red[2][kResolveWaves];
-    int32_t red_e[2][kResolveWaves];
+    RedSlot red[2][kResolveWaves];  // per-pod hand-offs, double-buffered by pod parity
     int64_t stage[2][10];       // snapshot fields of the pod's best untouched list node
     int32_t kfull[2];           // every entry of a full list touched: the batch must stop
     int32_t ntab[2];            // table size when the pod is evaluated
     int32_t n_t, committed, err_code, err_pod, nb;
 };
 
-// Diagnostic build only (-DKS_STAMPS): per-iteration cycle sums of waves 0, 1 and 3, written
-// to ctr[8..12]; the real kernel executes no stamp.
+// Diagnostic build only (-DKS_STAMPS): per-iteration cycle sums of waves 0-3, written to
+// ctr[8..13]; the real kernel executes no stamp.
 #ifdef KS_STAMPS
 __device__ __forceinline__ uint64_t stamp() {
     uint64_t t;
@@ -311,28 +322,17 @@ __device__ __forceinline__ int first_untouched(const ResolveShared& sh, int i, i
     return m ? __ffsll((unsigned long long)m) - 1 : -1;
 }
 
-// Table entry an expiry of the window lands on and whether it applies (the pod bound Ok and
-// not yet expired).  Not for the pod bound in the current iteration (its lb_* are pending).
-__device__ __forceinline__ void expiry_target(const ResolveShared& sh, int e, int64_t start, int& t, bool& ok) {
-    const int32_t q = sh.ex_q[e];
-    if (q >= start) { t = sh.lb_entry[q - start]; ok = sh.lb_stat[q - start] == 0; }
-    else { t = sh.ex_entry[e]; ok = sh.ex_ok[e] != 0; }
-}
-
-__device__ __forceinline__ void expiry_req(const ResolveShared& sh, int e, int64_t start, int64_t& r0, int64_t& r1,
-                                           int64_t& r2) {
-    const int32_t q = sh.ex_q[e];
-    if (q >= start) { r0 = sh.pod[q - start].req[0]; r1 = sh.pod[q - start].req[1]; r2 = sh.pod[q - start].req[2]; }
-    else { r0 = sh.ex_req[e][0]; r1 = sh.ex_req[e][1]; r2 = sh.ex_req[e][2]; }
-}
-
 // wave-wide max of (key, entry) pairs: the key decides, the entry follows it
-__device__ __forceinline__ void wave_best_entry(uint64_t key, int ent, uint64_t& wkey, int& went) {
-    wkey = wave_max_u64(key);
-    const uint64_t who = __ballot(key == wkey && wkey != 0);
-    went = who ? __builtin_amdgcn_readlane(ent, __ffsll((unsigned long long)who) - 1) : -1;
+__device__ __forceinline__ RedSlot wave_best_entry(uint64_t key, int ent) {
+    RedSlot r;
+    r.key = wave_max_u64(key);
+    const uint64_t who = __ballot(key == r.key && r.key != 0);
+    r.ent = who ? __builtin_amdgcn_readlane(ent, __ffsll((unsigned long long)who) - 1) : -1;
+    r.pad = 0;
+    return r;
 }
 
+template <bool kNarrow>
 __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) {
     __shared__ ResolveShared sh;
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid >> 6;
@@ -362,23 +362,24 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
     for (int i = tid; i < nb; i += kResolveThreads) {
         sh.pod[i] = a.pods[start + i];
         sh.dur[i] = a.dur[start + i];
+        const int64_t pos = a.exp_pos[start + i];
+        sh.exp_slot[i] = (pos >= e_base && pos - e_base < e_cnt) ? (int32_t)(pos - e_base) : -1;
     }
     for (int i = tid; i < nb * kL; i += kResolveThreads) sh.cand[i / kL][i % kL] = a.cand[i];
     for (int i = tid; i <= nb; i += kResolveThreads)
         sh.ex_off[i] = i <= 1 ? 0 : (int32_t)(a.exp_off[start + i] - e_base);
     for (int e = tid; e < e_cnt; e += kResolveThreads) {
         const int32_t q = a.exp_pod[e_base + e];
+        const PodRec& pq = a.pods[q];
         sh.ex_q[e] = q;
         sh.ex_entry[e] = -1;
+        sh.ex_req[e][0] = pq.req[0]; sh.ex_req[e][1] = pq.req[1]; sh.ex_req[e][2] = pq.req[2];
         if (q < start) {
             sh.ex_node[e] = a.b_node[q];
             sh.ex_ok[e] = (a.b_status[q] == 0) && !a.expired[q];
-            sh.ex_req[e][0] = a.pods[q].req[0];
-            sh.ex_req[e][1] = a.pods[q].req[1];
-            sh.ex_req[e][2] = a.pods[q].req[2];
         } else {
             sh.ex_node[e] = -1;
-            sh.ex_ok[e] = 0;
+            sh.ex_ok[e] = 0;  // set when the pod binds
         }
     }
     __syncthreads();
@@ -408,6 +409,7 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
         }
     }
     __syncthreads();
+    for (int e = tid; e < kTMax; e += kResolveThreads) sh.dirty[e] = -1;
     for (int e = tid; e < sh.n_t; e += kResolveThreads) {
         const NodeV v = load_node(a.s, sh.tnode[e]);
         sh.ts[0][e] = v.ac; sh.ts[1][e] = v.am; sh.ts[2][e] = v.ag; sh.ts[3][e] = v.ap;
@@ -416,35 +418,40 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
     }
     __syncthreads();
 
+    // owner registers (waves 3..15): entry r = tid - 192
+    const int r = tid - kOwnerWave0 * kWave;
+    bool loaded = false;
+    NodeV own{};
+    int32_t own_node = 0;
+
     // ---- prologue: pod 0's partial maxima
     if (wave == 0) {
         bool full;
         const int pa = first_untouched(sh, 0, lane, full);
         if (pa >= 0 && lane < 10) sh.stage[0][lane] = node_field(a.s, lane, key_node(sh.cand[0][pa]));
         if (lane == 0) {
-            sh.red[0][0] = pa >= 0 ? sh.cand[0][pa] : 0ull;
-            sh.red_e[0][0] = -1;
+            sh.red[0][0].key = pa >= 0 ? sh.cand[0][pa] : 0ull;
+            sh.red[0][0].ent = -1;
             sh.kfull[0] = pa < 0 && full;
             sh.ntab[0] = sh.n_t;
         }
+    } else if (wave < kOwnerWave0) {
+        if (lane == 0) { sh.red[0][wave].key = 0; sh.red[0][wave].ent = -1; }
     } else {
-        const PodRec p0 = sh.pod[0];
-        const int nt0 = sh.n_t;
-        uint64_t best = 0;
-        int bent = -1;
-        for (int e = tid - kWave; e < nt0; e += kResolveThreads - kWave) {
-            const uint64_t k = make_key(eval_total1(a.c, p0, t_node(sh, e)), (uint32_t)sh.tnode[e]);
-            if (k > best) { best = k; bent = e; }
+        uint64_t k = 0;
+        if (r < sh.n_t) {
+            own = t_node(sh, r);
+            own_node = sh.tnode[r];
+            loaded = true;
+            k = make_key(eval_t<kNarrow>(a.c, sh.pod[0], own), (uint32_t)own_node);
         }
-        uint64_t wk;
-        int we;
-        wave_best_entry(best, bent, wk, we);
-        if (lane == 0) { sh.red[0][wave] = wk; sh.red_e[0][wave] = we; }
+        const RedSlot w = wave_best_entry(k, r);
+        if (lane == 0) sh.red[0][wave] = w;
     }
     __syncthreads();
 
 #ifdef KS_STAMPS
-    uint64_t acc_work = 0, acc_wait = 0, acc_sub[4] = {0, 0, 0, 0};
+    uint64_t acc_work = 0, acc_wait = 0;
 #endif
     int i = 0;
     for (; i < nb; ++i) {
@@ -452,15 +459,17 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
         const int64_t j = start + i;
         const int cur = i & 1, nxt = cur ^ 1;
         // ---- every wave: pod i's winner and the stop decision (identical in all waves)
-        const uint64_t rv = lane < kResolveWaves ? sh.red[cur][lane] : 0ull;
-        const uint64_t v = wave_max_u64(rv);
-        const uint64_t wl = __ballot(rv == v && v != 0);
-        const int went = wl ? sh.red_e[cur][__ffsll((unsigned long long)wl) - 1] : -1;
-        const PodRec p = sh.pod[i];
+        RedSlot rs;
+        rs.key = 0; rs.ent = -1;
+        if (lane < kResolveWaves) rs = sh.red[cur][lane];
+        const uint64_t v = wave_max_u64(rs.key);
+        const uint64_t wl = __ballot(rs.key == v && v != 0);
+        const int went = wl ? __builtin_amdgcn_readlane(rs.ent, __ffsll((unsigned long long)wl) - 1) : -1;
+        const uint32_t pflags = sh.pod[i].flags;
         int stop = 0;
-        if (sh.kfull[cur]) stop = 1;                                       // list exhausted: rescan
-        else if (v == 0) stop = 2;                                         // NotFound
-        else if (p.flags & (kFlagBadKey | kFlagBadSpec)) stop = 3;         // InvalidArgument
+        if (sh.kfull[cur]) stop = 1;                                  // list exhausted: rescan
+        else if (v == 0) stop = 2;                                    // NotFound
+        else if (pflags & (kFlagBadKey | kFlagBadSpec)) stop = 3;     // InvalidArgument
         if (stop) {
             if (tid == 0) {
                 sh.committed = i;
@@ -468,10 +477,6 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
             }
             break;
         }
-        KS_STAMP(sw);
-#ifdef KS_STAMPS
-        acc_sub[0] += sw - s0;
-#endif
         const int nt = sh.ntab[cur];
         const int32_t nd = key_node(v);
         const int t = went >= 0 ? went : nt;  // an untouched winner becomes entry nt
@@ -488,26 +493,21 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
                 const int pa = first_untouched(sh, i + 1, lane, full);
                 if (pa >= 0 && lane < 10) sh.stage[nxt][lane] = node_field(a.s, lane, key_node(sh.cand[i + 1][pa]));
                 if (lane == 0) {
-                    sh.red[nxt][0] = pa >= 0 ? sh.cand[i + 1][pa] : 0ull;
-                    sh.red_e[nxt][0] = -1;
+                    sh.red[nxt][0].key = pa >= 0 ? sh.cand[i + 1][pa] : 0ull;
+                    sh.red[nxt][0].ent = -1;
                     sh.kfull[nxt] = pa < 0 && full;
                 }
             }
         } else if (wave == 1) {
+            const PodRec p = sh.pod[i];
             NodeV n = went >= 0 ? t_node(sh, t) : stage_node(sh, cur);
             const bool ok = fits(p, n);  // CreatePod admission (kubesim/node/node.go:44-47)
             if (ok && sh.dur[i] > 0) { n.rc += p.req[0]; n.rm += p.req[1]; n.rg += p.req[2]; n.nr += 1; }
-            for (int e = e0; e < e1; ++e) {  // pod i+1's expiries on this entry (pod i's own included)
-                const int32_t q = sh.ex_q[e];
-                int tq;
-                bool okq;
-                if (q == j) { tq = t; okq = ok; }
-                else expiry_target(sh, e, start, tq, okq);
-                if (tq != t || !okq) continue;
-                int64_t r0, r1, r2;
-                if (q == j) { r0 = p.req[0]; r1 = p.req[1]; r2 = p.req[2]; }
-                else expiry_req(sh, e, start, r0, r1, r2);
-                n.rc -= r0; n.rm -= r1; n.rg -= r2; n.nr -= 1;
+            for (int x = e0; x < e1; ++x) {  // pod i+1's expiries on this entry (pod i's own included)
+                const int32_t q = sh.ex_q[x];
+                const bool hit = q == j ? ok : (sh.ex_entry[x] == t && sh.ex_ok[x] != 0);
+                if (!hit) continue;
+                n.rc -= sh.ex_req[x][0]; n.rm -= sh.ex_req[x][1]; n.rg -= sh.ex_req[x][2]; n.nr -= 1;
                 if (lane == 0) a.expired[q] = 1;
             }
             if (lane == 0) {
@@ -516,83 +516,57 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
                     sh.tu[0][t] = n.taint; sh.tu[1][t] = n.label;
                 }
                 sh.ts[4][t] = n.rc; sh.ts[5][t] = n.rm; sh.ts[6][t] = n.rg; sh.ts[7][t] = n.nr;
-                sh.lb_node[i] = nd; sh.lb_entry[i] = t; sh.lb_stat[i] = ok ? 0 : 1;
+                sh.dirty[t] = i + 1;
+                const int slot = sh.exp_slot[i];
+                if (slot >= 0) { sh.ex_entry[slot] = t; sh.ex_ok[slot] = ok ? 1 : 0; }
                 a.b_node[j] = nd;
                 a.b_status[j] = ok ? 0 : 1;
             }
             if (has_next) {
-                const uint32_t t1 = eval_total1(a.c, sh.pod[i + 1], n);
-                if (lane == 0) { sh.red[nxt][1] = make_key(t1, (uint32_t)nd); sh.red_e[nxt][1] = t; }
+                const uint32_t t1 = eval_t<kNarrow>(a.c, sh.pod[i + 1], n);
+                if (lane == 0) { sh.red[nxt][1].key = make_key(t1, (uint32_t)nd); sh.red[nxt][1].ent = t; }
             }
         } else if (wave == 2) {
             if (has_next) {
                 if (lane == 0) {
-                    for (int e = e0; e < e1; ++e) {
-                        const int32_t q = sh.ex_q[e];
-                        if (q == j) continue;
-                        int tq;
-                        bool okq;
-                        expiry_target(sh, e, start, tq, okq);
-                        if (tq < 0 || tq == t || !okq) continue;
-                        int64_t r0, r1, r2;
-                        expiry_req(sh, e, start, r0, r1, r2);
-                        sh.ts[4][tq] -= r0; sh.ts[5][tq] -= r1; sh.ts[6][tq] -= r2; sh.ts[7][tq] -= 1;
-                        a.expired[q] = 1;
+                    for (int x = e0; x < e1; ++x) {
+                        const int tq = sh.ex_entry[x];
+                        if (sh.ex_q[x] == j || tq < 0 || tq == t || !sh.ex_ok[x]) continue;
+                        sh.ts[4][tq] -= sh.ex_req[x][0]; sh.ts[5][tq] -= sh.ex_req[x][1];
+                        sh.ts[6][tq] -= sh.ex_req[x][2]; sh.ts[7][tq] -= 1;
+                        sh.dirty[tq] = i + 1;
+                        a.expired[sh.ex_q[x]] = 1;
                     }
                 }
                 const PodRec pn = sh.pod[i + 1];
                 uint64_t best = 0;
                 int bent = -1;
-                for (int e = e0 + lane; e < e1; e += kWave) {
-                    if (sh.ex_q[e] == j) continue;
-                    int tq;
-                    bool okq;
-                    expiry_target(sh, e, start, tq, okq);
-                    if (tq < 0 || tq == t) continue;
-                    const uint64_t k = make_key(eval_total1(a.c, pn, t_node(sh, tq)), (uint32_t)sh.tnode[tq]);
+                for (int x = e0 + lane; x < e1; x += kWave) {
+                    const int tq = sh.ex_entry[x];
+                    if (sh.ex_q[x] == j || tq < 0 || tq == t) continue;
+                    const uint64_t k = make_key(eval_t<kNarrow>(a.c, pn, t_node(sh, tq)), (uint32_t)sh.tnode[tq]);
                     if (k > best) { best = k; bent = tq; }
                 }
-                uint64_t wk;
-                int we;
-                wave_best_entry(best, bent, wk, we);
-                if (lane == 0) { sh.red[nxt][2] = wk; sh.red_e[nxt][2] = we; }
+                const RedSlot w = wave_best_entry(best, bent);
+                if (lane == 0) sh.red[nxt][2] = w;
             }
         } else if (has_next) {
-            const PodRec pn = sh.pod[i + 1];
-            uint64_t best = 0;
-            int bent = -1;
-            for (int e = tid - 3 * kWave; e < nt; e += kResolveThreads - 3 * kWave) {
-                if (e == went) continue;  // wave 1 owns the winner's entry
-                bool mine = true;          // wave 2 owns the entries pod i+1's expiries land on
-                for (int x = e0; x < e1 && mine; ++x) {
-                    if (sh.ex_q[x] == j) continue;
-                    int tq;
-                    bool okq;
-                    expiry_target(sh, x, start, tq, okq);
-                    mine = tq != e;
+            uint64_t k = 0;
+            if (r < nt) {
+                if (!loaded) {
+                    own = t_node(sh, r);
+                    own_node = sh.tnode[r];
+                    loaded = true;
+                } else if (sh.dirty[r] == i) {
+                    own.rc = sh.ts[4][r]; own.rm = sh.ts[5][r]; own.rg = sh.ts[6][r]; own.nr = sh.ts[7][r];
                 }
-                if (!mine) continue;
-#ifdef KS_STAMPS
-                const NodeV nn = t_node(sh, e);
-                KS_STAMP(sa);
-                const uint32_t tt1 = eval_total1(a.c, pn, nn);
-                KS_STAMP(sb);
-                if (wave == 3 && e == tid - 3 * kWave) { acc_sub[1] += sa - sw; acc_sub[2] += sb - sa; }
-                const uint64_t k = make_key(tt1, (uint32_t)sh.tnode[e]);
-#else
-                const uint64_t k = make_key(eval_total1(a.c, pn, t_node(sh, e)), (uint32_t)sh.tnode[e]);
-#endif
-                if (k > best) { best = k; bent = e; }
+                bool mine = r != went;  // wave 1 owns the winner's entry this iteration
+                for (int x = e0; x < e1; ++x)  // wave 2 owns the entries pod i+1's expiries land on
+                    mine &= !(sh.ex_entry[x] == r && sh.ex_q[x] != j);
+                if (mine) k = make_key(eval_t<kNarrow>(a.c, sh.pod[i + 1], own), (uint32_t)own_node);
             }
-            KS_STAMP(sc);
-            uint64_t wk;
-            int we;
-            wave_best_entry(best, bent, wk, we);
-            if (lane == 0) { sh.red[nxt][wave] = wk; sh.red_e[nxt][wave] = we; }
-            KS_STAMP(sd);
-#ifdef KS_STAMPS
-            acc_sub[3] += sd - sc;
-#endif
+            const RedSlot w = wave_best_entry(k, r);
+            if (lane == 0) sh.red[nxt][wave] = w;
         }
         KS_STAMP(s1);
         __syncthreads();
@@ -604,25 +578,22 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
     }
     __syncthreads();
 #ifdef KS_STAMPS
-    if (lane == 0 && (wave == 0 || wave == 1 || wave == 3)) {
-        const int slot = wave == 0 ? 8 : (wave == 1 ? 10 : 11);
+    if (lane == 0 && wave <= 3) {
+        const int slot = wave == 0 ? 8 : (wave == 1 ? 10 : (wave == 2 ? 13 : 11));
         atomicAdd((unsigned long long*)&a.ctr[slot], (unsigned long long)acc_work);
         if (wave == 0) atomicAdd((unsigned long long*)&a.ctr[9], (unsigned long long)acc_wait);
     }
     if (tid == 0) atomicAdd((unsigned long long*)&a.ctr[12], (unsigned long long)i);
-    if (tid == 3 * kWave)
-        for (int k = 0; k < 3; ++k) atomicAdd((unsigned long long*)&a.ctr[13 + k], (unsigned long long)acc_sub[k + 1]);
-    if (tid == 3 * kWave) atomicAdd((unsigned long long*)&a.ctr[7], (unsigned long long)acc_sub[0]);
 #endif
 
     // ---- write back the mutable fields of every touched node
     const int n_final = sh.ntab[sh.committed & 1];
     for (int e = tid; e < n_final; e += kResolveThreads) {
-        const int64_t nd = sh.tnode[e];
-        a.s.rc[nd] = sh.ts[4][e];
-        a.s.rm[nd] = sh.ts[5][e];
-        a.s.rg[nd] = sh.ts[6][e];
-        a.s.nr[nd] = sh.ts[7][e];
+        const int64_t ndx = sh.tnode[e];
+        a.s.rc[ndx] = sh.ts[4][e];
+        a.s.rm[ndx] = sh.ts[5][e];
+        a.s.rg[ndx] = sh.ts[6][e];
+        a.s.nr[ndx] = sh.ts[7][e];
     }
     if (tid == 0) {
         a.ctr[kCtrStart] = start + sh.committed;
@@ -634,6 +605,7 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
 // ------------------------------------------------------------------------------------------
 // Filter mask / score of one pod against every node (api.Filter / api.Scorer shims).
 // ------------------------------------------------------------------------------------------
+template <bool kNarrow>
 __global__ __launch_bounds__(256) void eval_pod_kernel(Cfg c, NodeSoA s, const PodRec* pod, uint32_t filters,
                                                         uint8_t* mask, int64_t* score) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -645,7 +617,7 @@ __global__ __launch_bounds__(256) void eval_pod_kernel(Cfg c, NodeSoA s, const P
     if (filters & kFilterTaint) ok &= (n.taint & ~p.tol) == 0;
     if (filters & kFilterSelector) ok &= (n.label & p.sel) == p.sel;
     mask[i] = ok ? 1 : 0;
-    const uint32_t t1 = eval_total1(c, p, n);
+    const uint32_t t1 = eval_t<kNarrow>(c, p, n);
     score[i] = t1 ? (int64_t)t1 - 1 : -1;
 }
 
@@ -690,16 +662,21 @@ __global__ __launch_bounds__(256) void usage_kernel(int64_t q_lo, int64_t q_hi, 
     }
 }
 
-// Switch the device's memory unit from bytes to milli-bytes (x1000): node capacity and
-// requested totals, and every pod's memory request.  Runs at most once per engine, when a pod
-// with a fractional-byte memory request arrives (see ks_engine.cpp, memory scale).
-__global__ __launch_bounds__(256) void rescale_memory_kernel(NodeSoA s, int64_t n_pad, PodRec* pods, int64_t P) {
+// Multiply every device quantity of resource k by f[k] (node capacity unless absent, requested
+// totals, pod requests): the unit of resource k shrinks to a divisor of the old one when a pod
+// brings a quantity the old unit does not divide (see ks_engine.cpp, resource scale).
+__global__ __launch_bounds__(256) void rescale_kernel(NodeSoA s, int64_t n_pad, PodRec* pods, int64_t P,
+                                                      int64_t f0, int64_t f1, int64_t f2) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad; i += stride) {
-        if (s.am[i] >= 0) s.am[i] *= 1000;
-        s.rm[i] *= 1000;
+        if (s.ac[i] >= 0) s.ac[i] *= f0;
+        if (s.am[i] >= 0) s.am[i] *= f1;
+        if (s.ag[i] >= 0) s.ag[i] *= f2;
+        s.rc[i] *= f0; s.rm[i] *= f1; s.rg[i] *= f2;
     }
-    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < P; q += stride) pods[q].req[1] *= 1000;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < P; q += stride) {
+        pods[q].req[0] *= f0; pods[q].req[1] *= f1; pods[q].req[2] *= f2;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -709,27 +686,36 @@ int max_batch_pods() { return kMaxBatchR; }
 int max_pods_per_scan_wg() { return kMaxPG; }
 int block_nodes() { return kBlockNodes; }
 
-hipError_t launch_batch(const EngineArgs& a, hipStream_t st, hipEvent_t e_scan0, hipEvent_t e_scan1,
-                        hipEvent_t e_res1) {
+template <bool kNarrow>
+static void launch_batch_t(const EngineArgs& a, hipStream_t st, hipEvent_t e_scan0, hipEvent_t e_scan1,
+                           hipEvent_t e_res1) {
     hipLaunchKernelGGL(expire_head_kernel, dim3(1), dim3(256), 0, st, a);
     if (e_scan0) (void)hipEventRecord(e_scan0, st);
     dim3 g(a.nblk, (a.B + a.PG - 1) / a.PG);
-    hipLaunchKernelGGL(scan_kernel, g, dim3(kBlockNodes), 0, st, a);
+    hipLaunchKernelGGL(scan_kernel<kNarrow>, g, dim3(kBlockNodes), 0, st, a);
     hipLaunchKernelGGL(merge_kernel, dim3(a.B), dim3(256), 0, st, a);
     if (e_scan1) (void)hipEventRecord(e_scan1, st);
-    hipLaunchKernelGGL(resolve_kernel, dim3(1), dim3(kResolveThreads), 0, st, a);
+    hipLaunchKernelGGL(resolve_kernel<kNarrow>, dim3(1), dim3(kResolveThreads), 0, st, a);
     if (e_res1) (void)hipEventRecord(e_res1, st);
+}
+
+hipError_t launch_batch(const EngineArgs& a, bool narrow, hipStream_t st, hipEvent_t e_scan0, hipEvent_t e_scan1,
+                        hipEvent_t e_res1) {
+    if (narrow) launch_batch_t<true>(a, st, e_scan0, e_scan1, e_res1);
+    else launch_batch_t<false>(a, st, e_scan0, e_scan1, e_res1);
     return hipGetLastError();
 }
 
-hipError_t launch_rescale_memory(const NodeSoA& s, int64_t n_pad, PodRec* pods, int64_t P, hipStream_t st) {
-    hipLaunchKernelGGL(rescale_memory_kernel, dim3(1024), dim3(256), 0, st, s, n_pad, pods, P);
+hipError_t launch_rescale(const NodeSoA& s, int64_t n_pad, PodRec* pods, int64_t P, const int64_t f[3], hipStream_t st) {
+    hipLaunchKernelGGL(rescale_kernel, dim3(1024), dim3(256), 0, st, s, n_pad, pods, P, f[0], f[1], f[2]);
     return hipGetLastError();
 }
 
 hipError_t launch_eval_pod(const Cfg& c, const NodeSoA& s, const PodRec* pod, uint32_t filters, uint8_t* mask,
-                           int64_t* score, hipStream_t st) {
-    hipLaunchKernelGGL(eval_pod_kernel, dim3((c.n_nodes + 255) / 256), dim3(256), 0, st, c, s, pod, filters, mask, score);
+                           int64_t* score, bool narrow, hipStream_t st) {
+    const dim3 g((c.n_nodes + 255) / 256);
+    if (narrow) hipLaunchKernelGGL(eval_pod_kernel<true>, g, dim3(256), 0, st, c, s, pod, filters, mask, score);
+    else hipLaunchKernelGGL(eval_pod_kernel<false>, g, dim3(256), 0, st, c, s, pod, filters, mask, score);
     return hipGetLastError();
 }
 

@@ -18,6 +18,7 @@ KS_SCORER_CONST, KS_SCORER_LEAST_REQUESTED, KS_SCORER_BALANCED = 0, 1, 2
 KS_POD_OK, KS_POD_OVER_CAPACITY = 0, 1
 KS_PODFLAG_BAD_KEY, KS_PODFLAG_BAD_SPEC = 1, 2
 KS_ABI_VERSION = 1
+KS_ENGINE_FORCE_WIDE = 1
 
 STATUS_NAMES = {KS_OK: "OK", KS_EINVAL: "InvalidArgument", KS_ENOTFOUND: "NotFound",
                 KS_EDEVICE: "DeviceError", KS_ENOMEM: "OutOfMemory"}
@@ -35,7 +36,8 @@ class KsScorer(C.Structure):
 class KsConfig(C.Structure):
     _fields_ = [("abi_version", C.c_int32), ("tick_seconds", C.c_int32), ("filter_mode", C.c_int32),
                 ("filters", C.c_uint32), ("n_scorers", C.c_int32), ("scorers", KsScorer * 8),
-                ("device", C.c_int32), ("batch_pods", C.c_int32), ("reserved", C.c_int32 * 8)]
+                ("device", C.c_int32), ("batch_pods", C.c_int32), ("engine_flags", C.c_uint32),
+                ("reserved", C.c_int32 * 7)]
 
 
 class KsBind(C.Structure):

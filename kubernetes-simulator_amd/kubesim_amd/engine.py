@@ -45,7 +45,7 @@ def _c(a, dt):
 
 class Engine:
     def __init__(self, *, tick_seconds=10, filter_mode=_lib.KS_FILTER_REFERENCE_LITERAL, filters=0,
-                 scorers=((_lib.KS_SCORER_CONST, 1, 1),), device=0, batch_pods=0):
+                 scorers=((_lib.KS_SCORER_CONST, 1, 1),), device=0, batch_pods=0, engine_flags=0):
         L = _lib.load()
         cfg = KsConfig()
         cfg.abi_version = _lib.KS_ABI_VERSION
@@ -57,6 +57,7 @@ class Engine:
             cfg.scorers[i].kind, cfg.scorers[i].weight, cfg.scorers[i].value = k, w, v
         cfg.device = device
         cfg.batch_pods = batch_pods
+        cfg.engine_flags = engine_flags
         h = C.c_void_p()
         rc = L.ks_create(C.byref(cfg), C.byref(h))
         if rc != _lib.KS_OK:

@@ -17,11 +17,11 @@ MODES = {
 }
 
 
-def make_engine(trace, enc, mode, batch_pods=0):
+def make_engine(trace, enc, mode, batch_pods=0, engine_flags=0):
     from kubesim_amd.engine import Engine
     fm, fl, sc = MODES[mode] if isinstance(mode, str) else mode
     eng = Engine(tick_seconds=trace["tick_seconds"], filter_mode=fm, filters=fl, scorers=sc,
-                 batch_pods=batch_pods)
+                 batch_pods=batch_pods, engine_flags=engine_flags)
     eng.load_nodes(enc["alloc"], enc["taint"], enc["label"])
     return eng
 

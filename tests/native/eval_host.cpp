@@ -18,3 +18,5 @@ extern "C" int ks_host_eval(const ks::Cfg* c, int64_t n, const int64_t* alloc /*
 }
 extern "C" int ks_host_lr(int64_t A, int64_t u) { return ks::lr_one(A, u); }
 extern "C" int ks_host_ba(int64_t Ac, int64_t Am, int64_t uc, int64_t um) { return ks::ba_score(Ac, Am, uc, um); }
+extern "C" int ks_host_lr_n(int32_t A, int32_t u) { return ks::lr_one_n(A, u); }
+extern "C" int ks_host_ba_n(int32_t Ac, int32_t Am, int32_t uc, int32_t um) { return ks::ba_score_n(Ac, Am, uc, um); }

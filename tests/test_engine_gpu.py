@@ -18,9 +18,9 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
-def _lockstep(trace, mode, ticks, batch_pods=0, usage_every=1, chunk=1):
+def _lockstep(trace, mode, ticks, batch_pods=0, usage_every=1, chunk=1, engine_flags=0):
     enc = encoded(trace)
-    eng = make_engine(trace, enc, mode, batch_pods)
+    eng = make_engine(trace, enc, mode, batch_pods, engine_flags)
     eng.submit(enc["pods"])
     ora = make_oracle(trace, mode)
     ora.submit(trace)
@@ -53,11 +53,21 @@ def test_c1_kat():
         np.testing.assert_array_equal(eng.usage(), np.array(kat["usage"][t - 1], dtype=np.int64))
 
 
+@pytest.mark.parametrize("wide", [0, 1])
 @pytest.mark.parametrize("mode", sorted(MODES))
 @pytest.mark.parametrize("seed", [1, 2])
-def test_lockstep_small(mode, seed):
+def test_lockstep_small(mode, seed, wide):
+    """Both evaluator variants (narrow 32-bit / forced 64-bit) against the oracle."""
     tr = small_trace(seed, n_nodes=400, n_pods=300, arrival="stream")
-    _lockstep(tr, mode, 400)
+    _lockstep(tr, mode, 400, engine_flags=wide)
+
+
+def test_wide_capacities_use_general_evaluator():
+    """Capacities beyond the narrow range (2^29 units after scaling) must still be exact."""
+    tr = small_trace(41, n_nodes=300, n_pods=600, taints=False, selectors=False, tolerations=False)
+    nd = tr["nodes"]
+    nd["alloc"][::3, 1] = (1 << 50) + 7 * np.arange(len(nd["alloc"][::3]))  # odd memory sizes, gcd 1
+    _lockstep(tr, "feeds_all_lrba", 600, batch_pods=128, chunk=150)
 
 
 def test_golden_small_traces_engine():
