@@ -69,8 +69,10 @@ enum { KS_PODFLAG_BAD_KEY = 1, KS_PODFLAG_BAD_SPEC = 2 };
 typedef struct {
     int32_t kind;   /* KS_SCORER_* */
     int32_t weight; /* >= 0 */
-    int32_t value;  /* CONST only */
+    int32_t value;  /* CONST only, >= 0 */
 } ks_scorer;
+/* ks_create rejects (KS_EINVAL) a scorer set whose maximum total
+ * sum(weight*value) + 10*sum(weight of LR/BA) is >= 2^30 - 2. */
 
 typedef struct {
     int32_t abi_version;  /* KS_ABI_VERSION */
@@ -100,6 +102,18 @@ typedef struct ks_engine ks_engine;
 
 ks_status ks_create(const ks_config* cfg, ks_engine** out);
 void ks_destroy(ks_engine* eng);
+
+/* Node sharding across ranks (the reference's argmax over all nodes,
+ * kubesim/kubesim.go:208-222, becomes an exact merge of per-shard candidate lists).  One
+ * process per GPU; every rank loads the whole cluster and submits the same pods, scans only its
+ * contiguous node range, and all-gathers the per-pod top-L candidates once per batch over RCCL.
+ * Binds are identical on every rank.  Call on every rank before ks_load_nodes; rank 0 creates
+ * the communicator id with ks_comm_unique_id and the host broadcasts it (any channel).
+ * vshards > 1 splits each rank's range further (same merge path; lets one GPU test it).
+ * id may be NULL when world == 1 (no communicator). */
+#define KS_COMM_ID_BYTES 128
+ks_status ks_comm_unique_id(uint8_t* id_out /* [KS_COMM_ID_BYTES] */);
+ks_status ks_shard(ks_engine* eng, int32_t world, int32_t rank, const uint8_t* id, int32_t vshards);
 
 /* Load the cluster (once).  alloc[n][4] = {cpu, memory, nvidia.com/gpu, pods};
  * taint[n] = OR of dictionary bits of the node's NoSchedule/NoExecute taints;
@@ -144,9 +158,9 @@ typedef struct {
 } ks_step_stats;
 ks_status ks_last_step_stats(const ks_engine* eng, ks_step_stats* out);
 /* Device counters (diagnostics): [0] next pod, [1] step end, [2] error, [3] error pod,
- * [4] batches that committed early (top-L list exhausted), [8..12] resolver phase cycle
- * sums in a -DKS_STAMPS diagnostic build. */
-ks_status ks_debug_counters(ks_engine* eng, int64_t* out16);
+ * [4] batches that committed early (top-L list exhausted), [16..31] resolver phase cycle
+ * sums in a -DKS_STAMPS diagnostic build (tests/dev/diag_resolve.py). */
+ks_status ks_debug_counters(ks_engine* eng, int64_t* out32);
 void ks_set_profiling(ks_engine* eng, int enable);
 
 #ifdef __cplusplus

@@ -160,13 +160,29 @@ constexpr int64_t kNarrowReq = 1LL << 30;
 
 __host__ __device__ __forceinline__ int32_t clamp_req(int64_t q) { return (int32_t)(q < kNarrowReq ? q : kNarrowReq); }
 
-// floor(10 x / A) for 0 <= x <= A < 2^29
+// reciprocal estimates: hardware v_rcp on the device (~1 ulp), exact division on the host
+__host__ __device__ __forceinline__ float rcp_est(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcpf(x);
+#else
+    return 1.0f / x;
+#endif
+}
+__host__ __device__ __forceinline__ double rcp_est(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcp(x);
+#else
+    return 1.0 / x;
+#endif
+}
+
+// floor(10 x / A) for 0 <= x <= A < 2^29: float estimate (error << 1), one exact step either way
 __host__ __device__ __forceinline__ int32_t lr_frac10(uint32_t x, uint32_t A) {
-    int32_t q = (int32_t)(10.0f * (float)x / (float)A);
+    int32_t q = (int32_t)((10.0f * (float)x) * rcp_est((float)A));
     q = q < 0 ? 0 : (q > 10 ? 10 : q);
     const uint64_t y = (uint64_t)x * 10u, t = (uint64_t)(uint32_t)q * A;
-    if (y < t) q -= 1;
-    else if (y >= t + A) q += 1;
+    q += (y >= t + A) ? 1 : 0;
+    q -= (y < t) ? 1 : 0;
     return q;
 }
 
@@ -175,17 +191,17 @@ __host__ __device__ __forceinline__ int32_t lr_one_n(int32_t A, int32_t u) {
     return lr_frac10((uint32_t)(A - u), (uint32_t)A);
 }
 
-// floor(10 (D - X) / D), D = Ac Am < 2^58, X = |uc Am - um Ac| < D
+// floor(10 (D - X) / D), D = Ac Am < 2^58, X = |uc Am - um Ac| < D: double estimate, exact step
 __host__ __device__ __forceinline__ int32_t ba_score_n(int32_t Ac, int32_t Am, int32_t uc, int32_t um) {
     if (Ac <= 0 || Am <= 0 || uc >= Ac || um >= Am) return 0;
     const uint64_t D = (uint64_t)(uint32_t)Ac * (uint32_t)Am;
     const uint64_t a = (uint64_t)(uint32_t)uc * (uint32_t)Am, b = (uint64_t)(uint32_t)um * (uint32_t)Ac;
     const uint64_t X = a > b ? a - b : b - a;
-    int32_t q = (int32_t)(10.0f - 10.0f * ((float)X / (float)D));
+    int32_t q = (int32_t)(10.0 - 10.0 * ((double)X * rcp_est((double)D)));
     q = q < 0 ? 0 : (q > 10 ? 10 : q);
     const uint64_t y = (D - X) * 10u, t = (uint64_t)(uint32_t)q * D;
-    if (y < t) q -= 1;
-    else if (y >= t + D) q += 1;
+    q += (y >= t + D) ? 1 : 0;
+    q -= (y < t) ? 1 : 0;
     return q;
 }
 
@@ -217,6 +233,119 @@ template <bool kNarrow>
 __host__ __device__ __forceinline__ uint32_t eval_t(const Cfg& c, const PodRec& p, const NodeV& n) {
     if constexpr (kNarrow) return eval_total1_narrow(c, p, n);
     else return eval_total1(c, p, n);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Guarded float evaluator (the common path of scan and resolve).  Feasibility stays integer;
+// the three floors — floor(10 (A - u) / A) per LeastRequested resource and
+// floor(10 (1 - |uc/Ac - um/Am|)) — are computed in float from per-node reciprocals ic = 1/Ac,
+// im = 1/Am.  Error bounds (float rounding 2^-24 per op, v_rcp 1 ulp): the LR argument is off by
+// < 3.2e-6, the BA argument by < 6.5e-6.  When the fractional part of an argument is at least
+// kGuardLR / kGuardBA away from an integer the float floor equals the exact one; otherwise
+// `need` is set and the caller re-evaluates that lane exactly (eval_t) — rare, and a wave with no
+// such lane skips the exact code entirely.
+// ---------------------------------------------------------------------------------------------
+constexpr float kGuardLR = 1.0e-5f;
+constexpr float kGuardBA = 2.0e-5f;
+
+__host__ __device__ __forceinline__ float node_rcp(int64_t A) { return A > 0 ? rcp_est((float)A) : 0.f; }
+
+__host__ __device__ __forceinline__ int32_t floor_guarded(float y, float guard, bool& need) {
+    const int32_t q = (int32_t)y;  // y >= 0
+    const float fr = y - (float)q;
+    need |= (fr < guard) | (fr > 1.f - guard);
+    return q;
+}
+
+template <bool kNarrow>
+__host__ __device__ __forceinline__ uint32_t eval_fast(const Cfg& c, const PodRec& p, const NodeV& n, float ic,
+                                                       float im, bool& need) {
+    if (!c.has_scorers) return 0;
+    int64_t uc, um;
+    if constexpr (kNarrow) {
+        const int32_t qc = clamp_req(p.req[0]), qm = clamp_req(p.req[1]);
+        const int32_t ucn = (int32_t)n.rc + qc, umn = (int32_t)n.rm + qm;
+        if (c.filter_feeds) {
+            bool ok = true;
+            if (c.filters & kFilterFit) {
+                ok &= n.nr < n.ap;
+                if (p.keymask & 1) ok &= ucn <= (int32_t)n.ac;
+                if (p.keymask & 2) ok &= umn <= (int32_t)n.am;
+                if (p.keymask & 4) ok &= (int32_t)n.rg + clamp_req(p.req[2]) <= (int32_t)n.ag;
+            }
+            if (c.filters & kFilterTaint) ok &= (n.taint & ~p.tol) == 0;
+            if (c.filters & kFilterSelector) ok &= (n.label & p.sel) == p.sel;
+            if (!ok) return 0;
+        }
+        uc = ucn;
+        um = umn;
+    } else {
+        if (c.filter_feeds) {
+            bool ok = true;
+            if (c.filters & kFilterFit) ok &= fits(p, n);
+            if (c.filters & kFilterTaint) ok &= (n.taint & ~p.tol) == 0;
+            if (c.filters & kFilterSelector) ok &= (n.label & p.sel) == p.sel;
+            if (!ok) return 0;
+        }
+        uc = n.rc + p.req[0];
+        um = n.rm + p.req[1];
+    }
+    int32_t total = c.const_total;
+    if (c.w_lr) {
+        int32_t lc = 0, lm = 0;
+        if (n.ac > 0 && uc <= n.ac) lc = floor_guarded((float)(n.ac - uc) * (10.f * ic), kGuardLR, need);
+        if (n.am > 0 && um <= n.am) lm = floor_guarded((float)(n.am - um) * (10.f * im), kGuardLR, need);
+        total += c.w_lr * ((lc + lm) >> 1);
+    }
+    if (c.w_ba && n.ac > 0 && n.am > 0 && uc < n.ac && um < n.am) {
+        const float d = fabsf((float)uc * ic - (float)um * im);
+        total += c.w_ba * floor_guarded(10.f - 10.f * d, kGuardBA, need);
+    }
+    return (uint32_t)total + 1u;
+}
+
+// eval_t through the guarded float path (exact: falls back per lane)
+template <bool kNarrow>
+__host__ __device__ __forceinline__ uint32_t eval_g(const Cfg& c, const PodRec& p, const NodeV& n, float ic, float im) {
+    bool need = false;
+    uint32_t t = eval_fast<kNarrow>(c, p, n, ic, im, need);
+    if (need) t = eval_t<kNarrow>(c, p, n);
+    return t;
+}
+
+// Pod-dependent upper bound of the total, used by the resolver to skip exact evaluations that
+// cannot reach a known lower bound.  Per entry the resolver keeps b = (A - r) / A and 1/A in
+// float; for a pod with requests q, f = b - q/A = (A - u) / A and
+//   LeastRequested  floor(10 f)              <= floor(10 f~ + kBoundLR)
+//   Balanced        floor(10 (1 - |fc - fm|)) <= floor(10 (1 - |fc~ - fm~|) + kBoundBA)
+// where f~ is the float value: |f~ - f| < 6e-7 (rounding 2^-24 per op, v_rcp 1 ulp), so the
+// slacks below cover every rounding and each bounded floor is the exact one except within the
+// slack of an integer.  LR is 0 once u > A, Balanced once uc >= Ac or um >= Am (only claimed when
+// f~ is clearly negative).  Filters are not applied (a bound).
+constexpr float kBoundLR = 1.5e-5f;
+constexpr float kBoundBA = 3.0e-5f;
+struct PruneF {
+    float bc, ic, bm, im;
+    int32_t live;  // 0: no pod can make this node a candidate
+};
+__host__ __device__ __forceinline__ PruneF prune_prep(const Cfg& c, const NodeV& n) {
+    PruneF f;
+    f.ic = n.ac > 0 ? rcp_est((float)n.ac) : 0.f;
+    f.bc = n.ac > 0 ? (float)(n.ac - n.rc) * f.ic : -1.f;
+    f.im = n.am > 0 ? rcp_est((float)n.am) : 0.f;
+    f.bm = n.am > 0 ? (float)(n.am - n.rm) * f.im : -1.f;
+    f.live = c.has_scorers && !(c.filter_feeds && (c.filters & kFilterFit) && n.nr >= n.ap);
+    return f;
+}
+__host__ __device__ __forceinline__ uint32_t prune_tmax(const Cfg& c, const PruneF& f, float qc, float qm) {
+    const float fc = fmaf(-qc, f.ic, f.bc), fm = fmaf(-qm, f.im, f.bm);
+    int32_t total = c.const_total;
+    const int32_t lc = fc > -kBoundLR ? (int32_t)(10.f * fc + kBoundLR) : 0;
+    const int32_t lm = fm > -kBoundLR ? (int32_t)(10.f * fm + kBoundLR) : 0;
+    total += c.w_lr * ((lc + lm) >> 1);
+    if (fc > -kBoundLR && fm > -kBoundLR)
+        total += c.w_ba * (int32_t)(10.f - 10.f * fabsf(fc - fm) + kBoundBA);
+    return (uint32_t)total;
 }
 
 __host__ __device__ __forceinline__ uint64_t make_key(uint32_t total1, uint32_t node) {
@@ -271,15 +400,21 @@ struct EngineArgs {
     int64_t* ctr;            // start, end, error code, error pod, early stops
     int32_t B;
     int32_t PG;              // pods per scan workgroup
-    int32_t nblk;            // 256-node scan blocks
+    int32_t nblk;            // 256-node scan blocks (whole cluster; the lists' stride)
+    int32_t blk_lo;          // this rank's scan range [blk_lo, blk_lo + blk_n) (node sharding)
+    int32_t blk_n;
 };
 
 // Launchers and limits (defined in ks_kernels.hip).
 int max_batch_pods();
 int max_pods_per_scan_wg();
 int block_nodes();
-hipError_t launch_batch(const EngineArgs& a, bool narrow, hipStream_t st, hipEvent_t e_scan0, hipEvent_t e_scan1,
-                        hipEvent_t e_res1);
+// expire_head + scan of blocks [blk_lo, blk_lo + blk_n)
+hipError_t launch_scan(const EngineArgs& a, bool narrow, hipStream_t st);
+// per pod b < batch size: exact top-L over nl sorted lists lists[b*pod_stride + k*list_stride]
+hipError_t launch_merge(const EngineArgs& a, const uint64_t* lists, int64_t pod_stride, int32_t nl,
+                        int64_t list_stride, uint64_t* out, hipStream_t st);
+hipError_t launch_resolve(const EngineArgs& a, bool narrow, hipStream_t st);
 hipError_t launch_rescale(const NodeSoA& s, int64_t n_pad, PodRec* pods, int64_t P, const int64_t f[3], hipStream_t st);
 hipError_t launch_eval_pod(const Cfg& c, const NodeSoA& s, const PodRec* pod, uint32_t filters, uint8_t* mask,
                            int64_t* score, bool narrow, hipStream_t st);

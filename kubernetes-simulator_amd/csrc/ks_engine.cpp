@@ -13,12 +13,20 @@
 //    / BalancedAllocation result is unit-free).  A pod whose request g_k does not divide shrinks
 //    the unit (rescale_kernel multiplies the device state by g_k / g_k').  When every scaled
 //    capacity is < 2^29 the kernels use the narrow (32-bit) evaluator, else the 64/128-bit one.
-//  * batching: launches (expire_head, scan, resolve) triples until the device counter says
+//  * batching: launches (expire_head, scan, merge, resolve) until the device counter says
 //    every pod due in [tick+1, tick+ticks] is bound, then copies the binds back.
+//  * node sharding (ks_shard): every rank holds the whole node state and runs
+//    the identical resolver; rank r scans only its contiguous block range, merges it to a
+//    per-pod top-L, and one RCCL all-gather per batch exchanges the [B][L] lists, which a
+//    second merge reduces to the exact global top-L (the union of exact per-shard top-L lists
+//    contains the global top-L).  Binds are then identical on every rank with no further
+//    exchange.  Virtual shards (several parts per rank) run the same merge path on one GPU.
 // Placements themselves are decided on the device only.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cmath>
 #include <numeric>
 #include <cstdarg>
 #include <cstdio>
@@ -122,6 +130,12 @@ struct ks_engine {
     uint64_t* lists = nullptr;
     uint64_t* cand = nullptr;
     int nblk = 0;
+    // node sharding
+    int world = 1, rank = 0, vsh = 1;
+    ncclComm_t comm = nullptr;
+    std::vector<int> part_lo;  // [world * vsh + 1] block boundaries of the parts
+    int blk_lo = 0, blk_n = 0;  // this rank's scan range
+    uint64_t* cand_all = nullptr;  // [world * vsh][B][L]
     int64_t* d_ctr = nullptr;
     int64_t* h_ctr = nullptr;  // pinned
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -168,6 +182,8 @@ ks::EngineArgs make_args(ks_engine* e) {
     a.lists = e->lists;
     a.cand = e->cand;
     a.nblk = e->nblk;
+    a.blk_lo = e->blk_lo;
+    a.blk_n = e->blk_n;
     a.ctr = e->d_ctr;
     a.B = e->B;
     a.PG = e->PG;
@@ -209,7 +225,7 @@ ks_status ks_create(const ks_config* cfg, ks_engine** out) {
             default: return KS_EINVAL;
         }
     }
-    if (const_total + 10 * (w_lr + w_ba) >= (1LL << 31) - 2) return KS_EINVAL;  // total + 1 fits u32 keys
+    if (const_total + 10 * (w_lr + w_ba) >= (1LL << 30) - 2) return KS_EINVAL;  // total + 1 < 2^30 (resolver ikey)
 
     ks_engine* e = new ks_engine();
     e->cfg = *cfg;
@@ -225,10 +241,10 @@ ks_status ks_create(const ks_config* cfg, ks_engine** out) {
     e->dc.tick_seconds = cfg->tick_seconds;
     hipError_t r = hipSetDevice(e->device);
     if (r == hipSuccess) r = hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking);
-    if (r == hipSuccess) r = hipMalloc(&e->d_ctr, 16 * sizeof(int64_t));
-    if (r == hipSuccess) r = hipHostMalloc(&e->h_ctr, 16 * sizeof(int64_t), hipHostMallocDefault);
+    if (r == hipSuccess) r = hipMalloc(&e->d_ctr, 32 * sizeof(int64_t));
+    if (r == hipSuccess) r = hipHostMalloc(&e->h_ctr, 32 * sizeof(int64_t), hipHostMallocDefault);
     for (int i = 0; i < 4 && r == hipSuccess; i++) r = hipEventCreate(&e->ev[i]);
-    if (r == hipSuccess) r = hipMemsetAsync(e->d_ctr, 0, 16 * sizeof(int64_t), e->st);
+    if (r == hipSuccess) r = hipMemsetAsync(e->d_ctr, 0, 32 * sizeof(int64_t), e->st);
     if (r == hipSuccess) r = hipStreamSynchronize(e->st);
     if (r != hipSuccess) {
         delete e;
@@ -248,6 +264,8 @@ void ks_destroy(ks_engine* e) {
     if (e->node_mem) (void)hipFree(e->node_mem);
     if (e->lists) (void)hipFree(e->lists);
     if (e->cand) (void)hipFree(e->cand);
+    if (e->cand_all) (void)hipFree(e->cand_all);
+    if (e->comm) (void)ncclCommDestroy(e->comm);
     if (e->d_ctr) (void)hipFree(e->d_ctr);
     if (e->h_ctr) (void)hipHostFree(e->h_ctr);
     if (e->d_mask) (void)hipFree(e->d_mask);
@@ -257,6 +275,38 @@ void ks_destroy(ks_engine* e) {
     for (auto ev : e->prof_ev) (void)hipEventDestroy(ev);
     if (e->st) (void)hipStreamDestroy(e->st);
     delete e;
+}
+
+ks_status ks_comm_unique_id(uint8_t* id_out) {
+    if (!id_out) return KS_EINVAL;
+    ncclUniqueId uid;
+    if (ncclGetUniqueId(&uid) != ncclSuccess) return KS_EDEVICE;
+    static_assert(sizeof(uid) == KS_COMM_ID_BYTES, "RCCL unique id size");
+    std::memcpy(id_out, &uid, sizeof uid);
+    return KS_OK;
+}
+
+ks_status ks_shard(ks_engine* e, int32_t world, int32_t rank, const uint8_t* id, int32_t vshards) {
+    if (!e) return KS_EINVAL;
+    if (e->nodes_loaded) return fail(e, KS_EINVAL, "ks_shard must precede ks_load_nodes");
+    if (e->comm) return fail(e, KS_EINVAL, "already sharded");
+    if (world < 1 || rank < 0 || rank >= world || vshards < 1 || (int64_t)world * vshards > 4096)
+        return fail(e, KS_EINVAL, "bad shard geometry world=%d rank=%d vshards=%d", world, rank, vshards);
+    if (world > 1 && !id) return fail(e, KS_EINVAL, "world > 1 needs a communicator id");
+    HIPCHK(e, hipSetDevice(e->device));
+    if (id) {
+        ncclUniqueId uid;
+        std::memcpy(&uid, id, sizeof uid);
+        const ncclResult_t r = ncclCommInitRank(&e->comm, world, uid, rank);
+        if (r != ncclSuccess) {
+            e->comm = nullptr;
+            return fail(e, KS_EDEVICE, "ncclCommInitRank: %s", ncclGetErrorString(r));
+        }
+    }
+    e->world = world;
+    e->rank = rank;
+    e->vsh = vshards;
+    return KS_OK;
 }
 
 ks_status ks_load_nodes(ks_engine* e, int64_t n, const int64_t* alloc, const uint64_t* taint, const uint64_t* label) {
@@ -307,13 +357,21 @@ ks_status ks_load_nodes(ks_engine* e, int64_t n, const int64_t* alloc, const uin
     // pods per scan workgroup: the most pod reuse per node load that still leaves >= ~2048
     // workgroups (8 per CU) per scan
     e->nblk = (int)((e->n_pad + ks::block_nodes() - 1) / ks::block_nodes());
+    const int G = e->world * e->vsh;
+    e->part_lo.assign(G + 1, 0);
+    for (int p = 0; p <= G; p++) e->part_lo[p] = (int)((int64_t)p * e->nblk / G);
+    e->blk_lo = e->part_lo[e->rank * e->vsh];
+    e->blk_n = e->part_lo[(e->rank + 1) * e->vsh] - e->blk_lo;
+    // pods per scan workgroup: the most pod reuse per node load that still leaves >= ~2048
+    // workgroups (8 per CU) per scan
     int pg = 1;
     while (pg < ks::max_pods_per_scan_wg() && pg < e->B &&
-           (int64_t)e->nblk * ((e->B + pg * 2 - 1) / (pg * 2)) >= 2048)
+           (int64_t)e->blk_n * ((e->B + pg * 2 - 1) / (pg * 2)) >= 2048)
         pg *= 2;
     e->PG = pg;
     HIPCHK(e, hipMalloc(&e->lists, sizeof(uint64_t) * (size_t)e->B * e->nblk * ks::kTopL));
     HIPCHK(e, hipMalloc(&e->cand, sizeof(uint64_t) * (size_t)e->B * ks::kTopL));
+    if (G > 1) HIPCHK(e, hipMalloc(&e->cand_all, sizeof(uint64_t) * (size_t)G * e->B * ks::kTopL));
     HIPCHK(e, hipMalloc(&e->d_mask, std::max<int64_t>(n, 1)));
     HIPCHK(e, hipMalloc(&e->d_score, sizeof(int64_t) * std::max<int64_t>(n, 1)));
     HIPCHK(e, hipMalloc(&e->d_usage, sizeof(unsigned long long) * 3 * std::max<int64_t>(n, 1)));
@@ -489,7 +547,28 @@ ks_status ks_step(ks_engine* e, int64_t ticks, ks_bind* out, int64_t cap, int64_
                 e1 = e->prof_ev[3 * launches + 1];
                 e2 = e->prof_ev[3 * launches + 2];
             }
-            HIPCHK(e, ks::launch_batch(a, e->narrow, st, e0, e1, e2));
+            if (e0) HIPCHK(e, hipEventRecord(e0, st));
+            HIPCHK(e, ks::launch_scan(a, e->narrow, st));
+            const int G = e->world * e->vsh;
+            const int64_t L = ks::kTopL, BL = (int64_t)e->B * L;
+            if (G == 1) {
+                HIPCHK(e, ks::launch_merge(a, e->lists, (int64_t)e->nblk * L, e->nblk, L, e->cand, st));
+            } else {
+                for (int v = 0; v < e->vsh; v++) {
+                    const int p = e->rank * e->vsh + v;
+                    HIPCHK(e, ks::launch_merge(a, e->lists + (int64_t)e->part_lo[p] * L, (int64_t)e->nblk * L,
+                                               e->part_lo[p + 1] - e->part_lo[p], L, e->cand_all + p * BL, st));
+                }
+                if (e->comm) {
+                    const ncclResult_t nr = ncclAllGather(e->cand_all + (int64_t)e->rank * e->vsh * BL, e->cand_all,
+                                                          (size_t)e->vsh * BL, ncclUint64, e->comm, st);
+                    if (nr != ncclSuccess) return fail(e, KS_EDEVICE, "ncclAllGather: %s", ncclGetErrorString(nr));
+                }
+                HIPCHK(e, ks::launch_merge(a, e->cand_all, L, G, BL, e->cand, st));
+            }
+            if (e1) HIPCHK(e, hipEventRecord(e1, st));
+            HIPCHK(e, ks::launch_resolve(a, e->narrow, st));
+            if (e2) HIPCHK(e, hipEventRecord(e2, st));
             launches++;
         }
         HIPCHK(e, hipMemcpyAsync(e->h_ctr, e->d_ctr, 5 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
@@ -605,10 +684,10 @@ ks_status ks_last_step_stats(const ks_engine* e, ks_step_stats* out) {
     return KS_OK;
 }
 
-ks_status ks_debug_counters(ks_engine* e, int64_t* out16) {
-    if (!e || !out16) return KS_EINVAL;
+ks_status ks_debug_counters(ks_engine* e, int64_t* out32) {
+    if (!e || !out32) return KS_EINVAL;
     HIPCHK(e, hipSetDevice(e->device));
-    HIPCHK(e, hipMemcpyAsync(out16, e->d_ctr, 16 * sizeof(int64_t), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(out32, e->d_ctr, 32 * sizeof(int64_t), hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
     return KS_OK;
 }

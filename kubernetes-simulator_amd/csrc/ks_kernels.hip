@@ -32,10 +32,16 @@ constexpr int kBlockNodes = kScanWaves * kWave;
 constexpr int kL = kTopL;                // candidate list length per pod
 constexpr int kMaxPG = 32;               // pods per scan workgroup (LDS list staging)
 constexpr int kResolveThreads = 1024;    // 16 waves
-constexpr int kResolveWaves = kResolveThreads / kWave;
-constexpr int kOwnerWave0 = 3;           // waves 3..15 own the touched entries
-constexpr int kOwners = kResolveThreads - kOwnerWave0 * kWave;
-constexpr int kTMax = 768;               // touched-node table (LDS); <= kOwners
+constexpr int kOwnerWave0 = 3;           // waves 3..15 own the touched entries ...
+#ifndef KS_SPARE1
+#define KS_SPARE1 1
+#endif
+// ... except, with KS_SPARE1, waves 5, 9, 13: they share wave 1's SIMD (waves are dealt to the
+// four SIMDs round-robin) and wave 1 carries each pod's critical path (bind, then the next
+// pod's key on the bound node), so they stay idle
+constexpr int kOwnerWaves = KS_SPARE1 ? 10 : 13;
+constexpr int kOwners = kOwnerWaves * kWave;
+constexpr int kTMax = KS_SPARE1 ? 640 : 768;  // touched-node table (LDS); <= kOwners
 constexpr int kHash = 2048;              // open-addressing node -> entry map (LDS)
 constexpr int kMaxBatchR = 256;          // pods per resolve launch
 constexpr int kMaxExp = kTMax - kMaxBatchR;  // expiries pre-inserted per batch
@@ -46,6 +52,14 @@ static_assert(kTMax <= kOwners, "one touched entry per owner thread");
 enum : int64_t { kCtrStart = 0, kCtrEnd = 1, kCtrErr = 2, kCtrErrPod = 3, kCtrEarly = 4 };
 enum : uint32_t { kFlagBadKey = 1, kFlagBadSpec = 2 };
 enum : int64_t { kErrEinval = 1, kErrNotFound = 2 };
+
+// owner slot of a resolve wave, or -1
+__device__ __forceinline__ int owner_slot(int wave) {
+    if (wave < kOwnerWave0) return -1;
+    if (!KS_SPARE1) return wave - kOwnerWave0;
+    if ((wave & 3) == 1) return -1;
+    return wave - kOwnerWave0 - (wave > 5) - (wave > 9) - (wave > 13);
+}
 
 __device__ __forceinline__ int popc_below(uint64_t mask, int lane) {
     return __popcll(mask & ((1ull << lane) - 1ull));
@@ -87,7 +101,7 @@ __global__ __launch_bounds__(256) void scan_kernel(EngineArgs a) {
     const int pg0 = blockIdx.y * a.PG;
     if (pg0 >= nb) return;
     const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
-    const int blk = blockIdx.x;
+    const int blk = a.blk_lo + blockIdx.x;
     const uint32_t base = (uint32_t)blk * kBlockNodes + wave * kWave;
     const int64_t node = (int64_t)base + lane;
     const bool valid = node < a.c.n_nodes;
@@ -139,9 +153,11 @@ __global__ __launch_bounds__(256) void scan_kernel(EngineArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
-// merge: one 256-thread workgroup per pod; exact global top-L over the block lists.
+// merge: one 256-thread workgroup per pod; exact top-L over nl sorted lists (the scan's block
+// lists of one shard, or the shards' all-gathered lists).
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void merge_kernel(EngineArgs a) {
+__global__ __launch_bounds__(256) void merge_kernel(EngineArgs a, const uint64_t* src, int64_t pod_stride, int32_t nl,
+                                                     int64_t list_stride, uint64_t* out) {
     __shared__ uint64_t red[4];
     __shared__ int32_t owner[4];
     const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
@@ -153,11 +169,11 @@ __global__ __launch_bounds__(256) void merge_kernel(EngineArgs a) {
     uint64_t top[kL];  // per-thread sorted (descending) top-L over its blocks
 #pragma unroll
     for (int k = 0; k < kL; ++k) top[k] = 0;
-    const uint64_t* lists = a.lists + (int64_t)b * a.nblk * kL;
-    for (int blk = tid; blk < a.nblk; blk += 256) {
+    const uint64_t* lists = src + (int64_t)b * pod_stride;
+    for (int blk = tid; blk < nl; blk += 256) {
 #pragma unroll
         for (int k = 0; k < kL; ++k) {
-            uint64_t v = lists[(int64_t)blk * kL + k];
+            uint64_t v = lists[(int64_t)blk * list_stride + k];
             if (v <= top[kL - 1]) break;  // block lists are sorted: nothing further can enter
 #pragma unroll
             for (int s = 0; s < kL; ++s) {
@@ -186,7 +202,7 @@ __global__ __launch_bounds__(256) void merge_kernel(EngineArgs a) {
 #pragma unroll
         for (int w = 0; w < 4; ++w)
             if (red[w] > best) { best = red[w]; who = owner[w]; }
-        if (tid == 0) a.cand[(int64_t)b * kL + r] = best;
+        if (tid == 0) out[(int64_t)b * kL + r] = best;
         if (tid == who) head++;
         __syncthreads();
     }
@@ -195,12 +211,17 @@ __global__ __launch_bounds__(256) void merge_kernel(EngineArgs a) {
 // ------------------------------------------------------------------------------------------
 // resolve: one workgroup, sequential over the batch in FIFO order (one bind per tick).
 //
-// One barrier per pod.  After the barrier every wave derives pod i's winner from the
-// double-buffered partial maxima red[i&1] (identical decision in every wave, including the
-// NotFound / InvalidArgument / exhausted-list stops).  Then, until the next barrier, the waves
-// split the bind of pod i and the evaluation of pod i+1:
-//   wave 0    table insert of an untouched winner; walk pod i+1's top-L list against the
-//             table; stage the snapshot fields of its best untouched node in LDS
+// One barrier per pod.  Pod i's winner is a single LDS word best[i % 3]: every contributor of
+// pod i (list candidate, re-evaluated touched entries) folds its key in with an LDS atomic max
+// during iteration i-1, so after the barrier every wave reads the decision (and the NotFound /
+// InvalidArgument / exhausted-list stops) with one load.  Internal key (ikey):
+//     (total + 1) << 34 | (2^24 - 1 - node) << 10 | entry          (entry 1023 = untouched)
+// orders exactly like the packed key (node < 2^24, total + 1 < 2^30: ks_engine.cpp) and carries
+// the winner's table entry.  Between two barriers the waves split the bind of pod i and the
+// evaluation of pod i+1:
+//   wave 0    table insert of an untouched winner; pod i+1's best untouched list node (chosen
+//             from two prefetched candidates, see below) staged in LDS; pod i+2's list walk and
+//             HBM prefetch
 //   wave 1    CreatePod admission + bind on the winner's entry (and pod i+1's expiries that
 //             land on it); outputs; pod i+1's exact key on that entry
 //   wave 2    pod i+1's other expiries; pod i+1's exact keys on those entries
@@ -208,13 +229,18 @@ __global__ __launch_bounds__(256) void merge_kernel(EngineArgs a) {
 //             mutable fields when an entry was modified the iteration before) and computes pod
 //             i+1's exact key on it, unless wave 1 or 2 owns the entry this iteration
 // Writers (waves 1, 2) touch disjoint entries and every reader of those skips them.
+//
+// Prefetch: pod i+2's list is walked in iteration i; its first two untouched entries' records
+// are loaded into wave 0's registers (lane = slot * 10 + field).  In iteration i+1 exactly one
+// node can join the table (pod i+1's winner), so pod i+2's first untouched entry is the first
+// prefetched one unless that node just won, else the second.
+//
+// Pruning (exact): pod i+1's winner is >= its first untouched list entry >= its L-th list
+// entry (lists are sorted; a full list with every entry touched stops the batch before the
+// winner matters; wave 0 publishes a tighter bound, see prefetch_issue).  A touched entry whose
+// float upper bound (prune_tmax) is below it is not evaluated, and exact keys below it are not
+// folded into best.
 // ------------------------------------------------------------------------------------------
-struct alignas(16) RedSlot {
-    uint64_t key;
-    int32_t ent;  // touched-table entry, -1 = the list candidate
-    int32_t pad;
-};
-
 struct ResolveShared {
     int64_t ts[8][kTMax];       // touched-node state: ac am ag ap rc rm rg nr
     uint64_t tu[2][kTMax];      // taint label
@@ -224,6 +250,7 @@ struct ResolveShared {
     int32_t hval[kHash];        // entry index
     uint32_t tfilt[kFilterBits / 32];
     PodRec pod[kMaxBatchR];
+    float podf[kMaxBatchR][2];  // cpu / memory requests as float (prune_tmax)
     int32_t dur[kMaxBatchR];
     int32_t exp_slot[kMaxBatchR];  // window slot of an in-batch pod's own expiry, or -1
     uint64_t cand[kMaxBatchR][kL];
@@ -233,15 +260,35 @@ struct ResolveShared {
     int32_t ex_ok[kMaxExp];     // the expiring pod was bound Ok and has not expired yet
     int32_t ex_entry[kMaxExp];  // table entry of its node (set at the bind for in-batch pods)
     int64_t ex_req[kMaxExp][3];
-    RedSlot red[2][kResolveWaves];  // per-pod hand-offs, double-buffered by pod parity
+    uint64_t best[3];           // pod i's winner (ikey), folded during iteration i-1
     int64_t stage[2][10];       // snapshot fields of the pod's best untouched list node
     int32_t kfull[2];           // every entry of a full list touched: the batch must stop
+    uint64_t lbk[2];            // lower bound of the pod's winner key (see prefetch_issue)
     int32_t ntab[2];            // table size when the pod is evaluated
     int32_t n_t, committed, err_code, err_pod, nb;
 };
 
-// Diagnostic build only (-DKS_STAMPS): per-iteration cycle sums of waves 0-3, written to
-// ctr[8..13]; the real kernel executes no stamp.
+constexpr int kEntUntouched = 1023;
+static_assert(kTMax < kEntUntouched, "entry index fits 10 bits");
+
+__device__ __forceinline__ uint64_t ikey(uint64_t key, int ent) {
+    const uint32_t node = 0xFFFFFFFFu - (uint32_t)key;
+    return ((key >> 32) << 34) | ((uint64_t)(0xFFFFFFu - node) << 10) | (uint64_t)(uint32_t)ent;
+}
+__device__ __forceinline__ int32_t ikey_node(uint64_t b) { return (int32_t)(0xFFFFFFu - (uint32_t)((b >> 10) & 0xFFFFFFu)); }
+__device__ __forceinline__ int ikey_ent(uint64_t b) {
+    const int e = (int)(b & 1023u);
+    return e == kEntUntouched ? -1 : e;
+}
+__device__ __forceinline__ void fold_best(uint64_t* slot, uint64_t k) {
+    atomicMax((unsigned long long*)slot, (unsigned long long)k);
+}
+
+// Diagnostic build only (-DKS_STAMPS): per-iteration cycle sums and lane counts, accumulated in
+// ctr[16..31] (layout: tests/dev/diag_resolve.py); the real kernel executes no stamp.
+#ifndef KS_ABL
+#define KS_ABL 0  // diagnostic ablations (timing only, results invalid); 0 in every real build
+#endif
 #ifdef KS_STAMPS
 __device__ __forceinline__ uint64_t stamp() {
     uint64_t t;
@@ -302,34 +349,62 @@ __device__ __forceinline__ NodeV stage_node(const ResolveShared& sh, int b) {
     return v;
 }
 
+// field f (0..9, NodeV order) of node i: one load per lane, the field pointer by selects
 __device__ __forceinline__ int64_t node_field(const NodeSoA& s, int f, int64_t i) {
-    switch (f) {
-        case 0: return s.ac[i]; case 1: return s.am[i]; case 2: return s.ag[i]; case 3: return s.ap[i];
-        case 4: return s.rc[i]; case 5: return s.rm[i]; case 6: return s.rg[i]; case 7: return s.nr[i];
-        case 8: return (int64_t)s.taint[i]; default: return (int64_t)s.label[i];
-    }
+    const int64_t* p = f == 0 ? s.ac : f == 1 ? s.am : f == 2 ? s.ag : f == 3 ? s.ap : f == 4 ? s.rc
+                     : f == 5 ? s.rm : f == 6 ? s.rg : f == 7 ? s.nr : f == 8 ? (const int64_t*)s.taint
+                     : (const int64_t*)s.label;
+    return p[i];
 }
 
 __device__ __forceinline__ int32_t key_node(uint64_t key) { return (int32_t)(0xFFFFFFFFu - (uint32_t)key); }
 
-// Wave 0: first entry of pod i's list whose node is not in the touched table (-1 if none);
-// `full` = the list holds L candidates (so "none" means exhausted, not "no candidates").
-__device__ __forceinline__ int first_untouched(const ResolveShared& sh, int i, int lane, bool& full) {
+// Wave 0: first two entries of pod i's list whose node is not in the touched table (-1 if
+// none); `full` = the list holds L candidates (so "none" means exhausted, not "no candidates").
+__device__ __forceinline__ void first_untouched2(const ResolveShared& sh, int i, int lane, int& pa1, int& pa2,
+                                                 bool& full) {
     const uint64_t c = lane < kL ? sh.cand[i][lane] : 0ull;
     const bool ok = c != 0 && !is_touched(sh, key_node(c));
-    const uint64_t m = __ballot(ok);
+    uint64_t m = __ballot(ok);
     full = __popcll(__ballot(c != 0)) == kL;
-    return m ? __ffsll((unsigned long long)m) - 1 : -1;
+    pa1 = m ? __ffsll((unsigned long long)m) - 1 : -1;
+    m &= m - 1;
+    pa2 = m ? __ffsll((unsigned long long)m) - 1 : -1;
 }
 
-// wave-wide max of (key, entry) pairs: the key decides, the entry follows it
-__device__ __forceinline__ RedSlot wave_best_entry(uint64_t key, int ent) {
-    RedSlot r;
-    r.key = wave_max_u64(key);
-    const uint64_t who = __ballot(key == r.key && r.key != 0);
-    r.ent = who ? __builtin_amdgcn_readlane(ent, __ffsll((unsigned long long)who) - 1) : -1;
-    r.pad = 0;
-    return r;
+// Wave 0 prefetch state for one pod: lanes 0..19 hold field (lane % 10) of slot lane / 10
+struct Prefetch {
+    int64_t val;
+    int pa1, pa2;
+    int32_t node1;
+    bool full;
+};
+
+// Also publishes pod p's winner lower bound: the first untouched entry when pod p is decided is
+// the first or the second prefetched one (or none: then the batch stops at a full list, or the
+// list is short and the bound is 0), so the second one — or the first when the list is full and
+// has no second — is <= it.
+__device__ __forceinline__ void prefetch_issue(const EngineArgs& a, ResolveShared& sh, int p, int lane,
+                                               Prefetch& pf) {
+    first_untouched2(sh, p, lane, pf.pa1, pf.pa2, pf.full);
+    if (lane == 0)
+        sh.lbk[p & 1] = pf.pa2 >= 0 ? sh.cand[p][pf.pa2] : (pf.full && pf.pa1 >= 0 ? sh.cand[p][pf.pa1] : 0ull);
+    pf.node1 = pf.pa1 >= 0 ? key_node(sh.cand[p][pf.pa1]) : -1;
+    const int slot_pa = lane < 10 ? pf.pa1 : pf.pa2;
+    if (lane < 20 && slot_pa >= 0) pf.val = node_field(a.s, lane % 10, key_node(sh.cand[p][slot_pa]));
+}
+
+// Wave 0: pod p's best untouched list node given that `winner` just joined the table (-1:
+// none): stage its record, fold its key into best[bslot], set kfull.
+__device__ __forceinline__ void prefetch_commit(ResolveShared& sh, int p, int lane, const Prefetch& pf,
+                                                int32_t winner, int stage_buf, int bslot) {
+    const int slot = (pf.pa1 >= 0 && pf.node1 == winner) ? 1 : 0;
+    const int pa = slot ? pf.pa2 : pf.pa1;
+    if (pa >= 0 && lane < 20 && lane / 10 == slot) sh.stage[stage_buf][lane % 10] = pf.val;
+    if (lane == 0) {
+        if (pa >= 0) fold_best(&sh.best[bslot], ikey(sh.cand[p][pa], kEntUntouched));
+        sh.kfull[stage_buf] = pa < 0 && pf.full;
+    }
 }
 
 template <bool kNarrow>
@@ -352,6 +427,7 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
         }
         sh.nb = lo;
         sh.n_t = 0; sh.committed = lo; sh.err_code = 0; sh.err_pod = -1;
+        sh.best[0] = 0; sh.best[1] = 0; sh.best[2] = 0;
     }
     for (int h = tid; h < kHash; h += kResolveThreads) sh.hkey[h] = -1;
     for (int w = tid; w < kFilterBits / 32; w += kResolveThreads) sh.tfilt[w] = 0;
@@ -361,6 +437,8 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
 
     for (int i = tid; i < nb; i += kResolveThreads) {
         sh.pod[i] = a.pods[start + i];
+        sh.podf[i][0] = (float)a.pods[start + i].req[0];
+        sh.podf[i][1] = (float)a.pods[start + i].req[1];
         sh.dur[i] = a.dur[start + i];
         const int64_t pos = a.exp_pos[start + i];
         sh.exp_slot[i] = (pos >= e_base && pos - e_base < e_cnt) ? (int32_t)(pos - e_base) : -1;
@@ -419,56 +497,52 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
     __syncthreads();
 
     // owner registers (waves 3..15): entry r = tid - 192
-    const int r = tid - kOwnerWave0 * kWave;
+    const int oslot = owner_slot(wave);
+    const int r = oslot >= 0 ? oslot * kWave + lane : kTMax;
     bool loaded = false;
     NodeV own{};
     int32_t own_node = 0;
+    PruneF own_pf{};      // prune_tmax state of the entry
+    Prefetch pf{};        // wave 0
 
-    // ---- prologue: pod 0's partial maxima
+    // ---- prologue: pod 0's contributions into best[0]; pod 1's prefetch
     if (wave == 0) {
         bool full;
-        const int pa = first_untouched(sh, 0, lane, full);
+        int pa, pa2;
+        first_untouched2(sh, 0, lane, pa, pa2, full);
         if (pa >= 0 && lane < 10) sh.stage[0][lane] = node_field(a.s, lane, key_node(sh.cand[0][pa]));
         if (lane == 0) {
-            sh.red[0][0].key = pa >= 0 ? sh.cand[0][pa] : 0ull;
-            sh.red[0][0].ent = -1;
+            if (pa >= 0) fold_best(&sh.best[0], ikey(sh.cand[0][pa], kEntUntouched));
             sh.kfull[0] = pa < 0 && full;
             sh.ntab[0] = sh.n_t;
         }
-    } else if (wave < kOwnerWave0) {
-        if (lane == 0) { sh.red[0][wave].key = 0; sh.red[0][wave].ent = -1; }
-    } else {
-        uint64_t k = 0;
-        if (r < sh.n_t) {
-            own = t_node(sh, r);
-            own_node = sh.tnode[r];
-            loaded = true;
-            k = make_key(eval_t<kNarrow>(a.c, sh.pod[0], own), (uint32_t)own_node);
-        }
-        const RedSlot w = wave_best_entry(k, r);
-        if (lane == 0) sh.red[0][wave] = w;
+        if (lane == 0) sh.lbk[0] = sh.cand[0][kL - 1];
+        if (nb > 1) prefetch_issue(a, sh, 1, lane, pf);
+    } else if (oslot >= 0 && r < sh.n_t) {
+        own = t_node(sh, r);
+        own_node = sh.tnode[r];
+        own_pf = prune_prep(a.c, own);
+        loaded = true;
+        const uint64_t k = make_key(eval_t<kNarrow>(a.c, sh.pod[0], own), (uint32_t)own_node);
+        if (k != 0 && k >= sh.cand[0][kL - 1]) fold_best(&sh.best[0], ikey(k, r));
     }
     __syncthreads();
 
 #ifdef KS_STAMPS
-    uint64_t acc_work = 0, acc_wait = 0;
+    uint64_t acc_work = 0, acc_wait = 0, acc_sub[8] = {0, 0, 0, 0, 0, 0, 0, 0}, acc_cnt[4] = {0, 0, 0, 0};
 #endif
     int i = 0;
     for (; i < nb; ++i) {
         KS_STAMP(s0);
         const int64_t j = start + i;
         const int cur = i & 1, nxt = cur ^ 1;
+        const int b_cur = i % 3, b_nxt = (i + 1) % 3;
         // ---- every wave: pod i's winner and the stop decision (identical in all waves)
-        RedSlot rs;
-        rs.key = 0; rs.ent = -1;
-        if (lane < kResolveWaves) rs = sh.red[cur][lane];
-        const uint64_t v = wave_max_u64(rs.key);
-        const uint64_t wl = __ballot(rs.key == v && v != 0);
-        const int went = wl ? __builtin_amdgcn_readlane(rs.ent, __ffsll((unsigned long long)wl) - 1) : -1;
+        const uint64_t bw = sh.best[b_cur];
         const uint32_t pflags = sh.pod[i].flags;
         int stop = 0;
         if (sh.kfull[cur]) stop = 1;                                  // list exhausted: rescan
-        else if (v == 0) stop = 2;                                    // NotFound
+        else if (bw == 0) stop = 2;                                   // NotFound
         else if (pflags & (kFlagBadKey | kFlagBadSpec)) stop = 3;     // InvalidArgument
         if (stop) {
             if (tid == 0) {
@@ -477,32 +551,76 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
             }
             break;
         }
+        const int went = ikey_ent(bw);
+        const int32_t nd = ikey_node(bw);
         const int nt = sh.ntab[cur];
-        const int32_t nd = key_node(v);
         const int t = went >= 0 ? went : nt;  // an untouched winner becomes entry nt
         const bool has_next = i + 1 < nb;
         const int e0 = has_next ? sh.ex_off[i + 1] : 0, e1 = has_next ? sh.ex_off[i + 2] : 0;
+        KS_STAMP(sw);
+#ifdef KS_STAMPS
+        acc_sub[0] += sw - s0;
+#endif
 
-        if (wave == 0) {
+        if (oslot >= 0) {
+            if (has_next && oslot * kWave < nt && !(KS_ABL & 16)) {
+                if (r < nt) {
+                    if (!loaded) {
+                        own = t_node(sh, r);
+                        own_node = sh.tnode[r];
+                        own_pf = prune_prep(a.c, own);
+                        loaded = true;
+                    } else if (sh.dirty[r] == i) {
+                        own.rc = sh.ts[4][r]; own.rm = sh.ts[5][r]; own.rg = sh.ts[6][r]; own.nr = sh.ts[7][r];
+                        own_pf = prune_prep(a.c, own);
+                    }
+                }
+                const uint64_t lbk = sh.lbk[nxt];
+                bool want = r < nt && own_pf.live && r != went;
+#ifdef KS_STAMPS
+                acc_cnt[0] += __popcll(__ballot(r < nt));
+                acc_cnt[1] += __popcll(__ballot(want));
+#endif
+                if (lbk != 0 && want) {
+                    const uint32_t tm = prune_tmax(a.c, own_pf, sh.podf[i + 1][0], sh.podf[i + 1][1]);
+                    want = make_key(tm + 1u, (uint32_t)own_node) >= lbk;
+                }
+#ifdef KS_STAMPS
+                acc_cnt[2] += __popcll(__ballot(want));
+                acc_cnt[3] += __ballot(want) != 0;
+#endif
+                KS_STAMP(sa);
+                if (__ballot(want)) {
+                    for (int x = e0; x < e1; ++x)  // wave 2 owns the entries pod i+1's expiries land on
+                        want &= !(sh.ex_entry[x] == r && sh.ex_q[x] != j);
+                    KS_STAMP(sb);
+                    if (want && !(KS_ABL & 1)) {
+                        const uint64_t k = make_key(eval_t<kNarrow>(a.c, sh.pod[i + 1], own), (uint32_t)own_node);
+                        if (k != 0 && k >= lbk) fold_best(&sh.best[b_nxt], ikey(k, r));
+                    }
+                    KS_STAMP(sc);
+#ifdef KS_STAMPS
+                    if (wave == 3) { acc_sub[2] += sb - sa; acc_sub[3] += sc - sb; }
+#endif
+                }
+#ifdef KS_STAMPS
+                if (wave == 3) acc_sub[1] += sa - sw;
+#endif
+            }
+        } else if (wave == 0) {
             if (lane == 0) {
                 if (went < 0) { sh.tnode[t] = nd; h_insert(sh, nd, t); }
                 sh.ntab[nxt] = went < 0 ? nt + 1 : nt;
+                sh.best[(i + 2) % 3] = 0;  // read in iteration i-1, folded into in iteration i+1
             }
-            if (has_next) {
-                bool full;
-                const int pa = first_untouched(sh, i + 1, lane, full);
-                if (pa >= 0 && lane < 10) sh.stage[nxt][lane] = node_field(a.s, lane, key_node(sh.cand[i + 1][pa]));
-                if (lane == 0) {
-                    sh.red[nxt][0].key = pa >= 0 ? sh.cand[i + 1][pa] : 0ull;
-                    sh.red[nxt][0].ent = -1;
-                    sh.kfull[nxt] = pa < 0 && full;
-                }
-            }
+            if (has_next) prefetch_commit(sh, i + 1, lane, pf, went < 0 ? nd : -1, nxt, b_nxt);
+            if (i + 2 < nb) prefetch_issue(a, sh, i + 2, lane, pf);
         } else if (wave == 1) {
             const PodRec p = sh.pod[i];
             NodeV n = went >= 0 ? t_node(sh, t) : stage_node(sh, cur);
             const bool ok = fits(p, n);  // CreatePod admission (kubesim/node/node.go:44-47)
             if (ok && sh.dur[i] > 0) { n.rc += p.req[0]; n.rm += p.req[1]; n.rg += p.req[2]; n.nr += 1; }
+            KS_STAMP(t1a);
             for (int x = e0; x < e1; ++x) {  // pod i+1's expiries on this entry (pod i's own included)
                 const int32_t q = sh.ex_q[x];
                 const bool hit = q == j ? ok : (sh.ex_entry[x] == t && sh.ex_ok[x] != 0);
@@ -510,6 +628,7 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
                 n.rc -= sh.ex_req[x][0]; n.rm -= sh.ex_req[x][1]; n.rg -= sh.ex_req[x][2]; n.nr -= 1;
                 if (lane == 0) a.expired[q] = 1;
             }
+            KS_STAMP(t1b);
             if (lane == 0) {
                 if (went < 0) {
                     sh.ts[0][t] = n.ac; sh.ts[1][t] = n.am; sh.ts[2][t] = n.ag; sh.ts[3][t] = n.ap;
@@ -522,12 +641,17 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
                 a.b_node[j] = nd;
                 a.b_status[j] = ok ? 0 : 1;
             }
-            if (has_next) {
-                const uint32_t t1 = eval_t<kNarrow>(a.c, sh.pod[i + 1], n);
-                if (lane == 0) { sh.red[nxt][1].key = make_key(t1, (uint32_t)nd); sh.red[nxt][1].ent = t; }
+            KS_STAMP(t1c);
+            if (lane == 0 && has_next && !(KS_ABL & 2)) {
+                const uint64_t k = make_key(eval_t<kNarrow>(a.c, sh.pod[i + 1], n), (uint32_t)nd);
+                if (k != 0) fold_best(&sh.best[b_nxt], ikey(k, t));
             }
+            KS_STAMP(t1d);
+#ifdef KS_STAMPS
+            acc_sub[4] += t1a - sw; acc_sub[5] += t1b - t1a; acc_sub[6] += t1c - t1b; acc_sub[7] += t1d - t1c;
+#endif
         } else if (wave == 2) {
-            if (has_next) {
+            if (has_next && e1 > e0 && !(KS_ABL & 4)) {
                 if (lane == 0) {
                     for (int x = e0; x < e1; ++x) {
                         const int tq = sh.ex_entry[x];
@@ -539,34 +663,13 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
                     }
                 }
                 const PodRec pn = sh.pod[i + 1];
-                uint64_t best = 0;
-                int bent = -1;
                 for (int x = e0 + lane; x < e1; x += kWave) {
                     const int tq = sh.ex_entry[x];
                     if (sh.ex_q[x] == j || tq < 0 || tq == t) continue;
                     const uint64_t k = make_key(eval_t<kNarrow>(a.c, pn, t_node(sh, tq)), (uint32_t)sh.tnode[tq]);
-                    if (k > best) { best = k; bent = tq; }
+                    if (k != 0) fold_best(&sh.best[b_nxt], ikey(k, tq));
                 }
-                const RedSlot w = wave_best_entry(best, bent);
-                if (lane == 0) sh.red[nxt][2] = w;
             }
-        } else if (has_next) {
-            uint64_t k = 0;
-            if (r < nt) {
-                if (!loaded) {
-                    own = t_node(sh, r);
-                    own_node = sh.tnode[r];
-                    loaded = true;
-                } else if (sh.dirty[r] == i) {
-                    own.rc = sh.ts[4][r]; own.rm = sh.ts[5][r]; own.rg = sh.ts[6][r]; own.nr = sh.ts[7][r];
-                }
-                bool mine = r != went;  // wave 1 owns the winner's entry this iteration
-                for (int x = e0; x < e1; ++x)  // wave 2 owns the entries pod i+1's expiries land on
-                    mine &= !(sh.ex_entry[x] == r && sh.ex_q[x] != j);
-                if (mine) k = make_key(eval_t<kNarrow>(a.c, sh.pod[i + 1], own), (uint32_t)own_node);
-            }
-            const RedSlot w = wave_best_entry(k, r);
-            if (lane == 0) sh.red[nxt][wave] = w;
         }
         KS_STAMP(s1);
         __syncthreads();
@@ -578,12 +681,20 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
     }
     __syncthreads();
 #ifdef KS_STAMPS
-    if (lane == 0 && wave <= 3) {
-        const int slot = wave == 0 ? 8 : (wave == 1 ? 10 : (wave == 2 ? 13 : 11));
-        atomicAdd((unsigned long long*)&a.ctr[slot], (unsigned long long)acc_work);
-        if (wave == 0) atomicAdd((unsigned long long*)&a.ctr[9], (unsigned long long)acc_wait);
+    {
+        unsigned long long* d = (unsigned long long*)a.ctr + 16;
+        if (lane == 0 && wave <= 3) atomicAdd(&d[wave == 3 ? 15 : (wave == 0 ? 0 : wave + 1)], acc_work);
+        if (lane == 0 && wave == 0) atomicAdd(&d[1], acc_wait);
+        if (tid == 0) atomicAdd(&d[4], (unsigned long long)i);
+        if (lane == 0 && wave == 3)
+            for (int k = 0; k < 4; ++k) atomicAdd(&d[5 + k], acc_sub[k]);       // top, load, excl, eval
+        if (lane == 0 && wave == 1)
+            for (int k = 0; k < 4; ++k) atomicAdd(&d[11 + k], acc_sub[4 + k]);  // fetch+fit, expiries, writes, eval
+        if (lane == 0 && oslot >= 0) {
+            atomicAdd(&d[9], acc_cnt[2]);   // lanes passing prune_tmax
+            atomicAdd(&d[10], acc_cnt[3]);  // owner waves evaluating
+        }
     }
-    if (tid == 0) atomicAdd((unsigned long long*)&a.ctr[12], (unsigned long long)i);
 #endif
 
     // ---- write back the mutable fields of every touched node
@@ -686,23 +797,25 @@ int max_batch_pods() { return kMaxBatchR; }
 int max_pods_per_scan_wg() { return kMaxPG; }
 int block_nodes() { return kBlockNodes; }
 
-template <bool kNarrow>
-static void launch_batch_t(const EngineArgs& a, hipStream_t st, hipEvent_t e_scan0, hipEvent_t e_scan1,
-                           hipEvent_t e_res1) {
+hipError_t launch_scan(const EngineArgs& a, bool narrow, hipStream_t st) {
     hipLaunchKernelGGL(expire_head_kernel, dim3(1), dim3(256), 0, st, a);
-    if (e_scan0) (void)hipEventRecord(e_scan0, st);
-    dim3 g(a.nblk, (a.B + a.PG - 1) / a.PG);
-    hipLaunchKernelGGL(scan_kernel<kNarrow>, g, dim3(kBlockNodes), 0, st, a);
-    hipLaunchKernelGGL(merge_kernel, dim3(a.B), dim3(256), 0, st, a);
-    if (e_scan1) (void)hipEventRecord(e_scan1, st);
-    hipLaunchKernelGGL(resolve_kernel<kNarrow>, dim3(1), dim3(kResolveThreads), 0, st, a);
-    if (e_res1) (void)hipEventRecord(e_res1, st);
+    if (a.blk_n > 0) {
+        const dim3 g(a.blk_n, (a.B + a.PG - 1) / a.PG);
+        if (narrow) hipLaunchKernelGGL(scan_kernel<true>, g, dim3(kBlockNodes), 0, st, a);
+        else hipLaunchKernelGGL(scan_kernel<false>, g, dim3(kBlockNodes), 0, st, a);
+    }
+    return hipGetLastError();
 }
 
-hipError_t launch_batch(const EngineArgs& a, bool narrow, hipStream_t st, hipEvent_t e_scan0, hipEvent_t e_scan1,
-                        hipEvent_t e_res1) {
-    if (narrow) launch_batch_t<true>(a, st, e_scan0, e_scan1, e_res1);
-    else launch_batch_t<false>(a, st, e_scan0, e_scan1, e_res1);
+hipError_t launch_merge(const EngineArgs& a, const uint64_t* lists, int64_t pod_stride, int32_t nl,
+                        int64_t list_stride, uint64_t* out, hipStream_t st) {
+    hipLaunchKernelGGL(merge_kernel, dim3(a.B), dim3(256), 0, st, a, lists, pod_stride, nl, list_stride, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_resolve(const EngineArgs& a, bool narrow, hipStream_t st) {
+    if (narrow) hipLaunchKernelGGL(resolve_kernel<true>, dim3(1), dim3(kResolveThreads), 0, st, a);
+    else hipLaunchKernelGGL(resolve_kernel<false>, dim3(1), dim3(kResolveThreads), 0, st, a);
     return hipGetLastError();
 }
 

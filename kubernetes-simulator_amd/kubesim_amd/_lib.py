@@ -26,7 +26,9 @@ STATUS_NAMES = {KS_OK: "OK", KS_EINVAL: "InvalidArgument", KS_ENOTFOUND: "NotFou
 # every symbol include/ks_engine.h declares
 EXPORTED_SYMBOLS = ("ks_create", "ks_destroy", "ks_load_nodes", "ks_submit_pods", "ks_step",
                     "ks_filter", "ks_score", "ks_usage", "ks_current_tick", "ks_queued_pods",
-                    "ks_last_error", "ks_last_step_stats", "ks_set_profiling", "ks_debug_counters")
+                    "ks_last_error", "ks_last_step_stats", "ks_set_profiling", "ks_debug_counters",
+                    "ks_comm_unique_id", "ks_shard")
+KS_COMM_ID_BYTES = 128
 
 
 class KsScorer(C.Structure):
@@ -85,5 +87,9 @@ def load():
     L.ks_debug_counters.restype = C.c_int
     L.ks_set_profiling.argtypes = [p, C.c_int]
     L.ks_set_profiling.restype = None
+    L.ks_comm_unique_id.argtypes = [p]
+    L.ks_comm_unique_id.restype = C.c_int
+    L.ks_shard.argtypes = [p, C.c_int32, C.c_int32, p, C.c_int32]
+    L.ks_shard.restype = C.c_int
     _lib = L
     return L

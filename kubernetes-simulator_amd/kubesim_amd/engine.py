@@ -84,6 +84,18 @@ class Engine:
         if rc != _lib.KS_OK:
             raise KsError(rc, self._L.ks_last_error(self.h).decode(), binds)
 
+    # -- node sharding ------------------------------------------------------
+    def shard(self, world: int, rank: int, comm_id: bytes | None = None, vshards: int = 1):
+        """Scan only this rank's node range; candidates are all-gathered per batch over RCCL
+        (comm_id from :func:`comm_unique_id` on rank 0, broadcast by the caller).  Before
+        ``load_nodes``.  ``vshards`` > 1 splits the range further (one-GPU testing)."""
+        buf = None
+        if comm_id is not None:
+            if len(comm_id) != _lib.KS_COMM_ID_BYTES:
+                raise ValueError("comm_id must be KS_COMM_ID_BYTES long")
+            buf = (C.c_uint8 * _lib.KS_COMM_ID_BYTES).from_buffer_copy(comm_id)
+        self._check(self._L.ks_shard(self.h, world, rank, buf, vshards))
+
     # -- cluster / queue ---------------------------------------------------------------------
     def load_nodes(self, alloc, taint, label):
         alloc = _c(alloc, np.int64).reshape(-1, 4)
@@ -144,7 +156,7 @@ class Engine:
                     pods=s.pods)
 
     def debug_counters(self):
-        out = np.zeros(16, np.int64)
+        out = np.zeros(32, np.int64)
         self._check(self._L.ks_debug_counters(self.h, _p(out)))
         return out
 
@@ -157,3 +169,13 @@ def engine_for_trace(trace, enc, **cfg):
     eng = Engine(tick_seconds=trace["tick_seconds"], **cfg)
     eng.load_nodes(enc["alloc"], enc["taint"], enc["label"])
     return eng
+
+
+def comm_unique_id() -> bytes:
+    """A fresh RCCL communicator id for :meth:`Engine.shard` (create on rank 0 only)."""
+    L = _lib.load()
+    buf = (C.c_uint8 * _lib.KS_COMM_ID_BYTES)()
+    rc = L.ks_comm_unique_id(buf)
+    if rc != 0:
+        raise KsError(rc, "ks_comm_unique_id failed")
+    return bytes(buf)

@@ -18,9 +18,12 @@ c0 = eng.debug_counters().copy()
 t = time.perf_counter(); eng.step(32768); dt = time.perf_counter() - t
 c1 = eng.debug_counters()
 d = c1 - c0
-pods = d[12]
+D = d[16:]
+pods = D[4]
 print(f"B={B} pods={pods} wall {dt*1e3:.1f} ms  -> {32768/dt:.0f} pods/s")
-for k, name in enumerate(["wave0 work", "wave0 wait", "wave1 work", "wave3 work"]):
-    print(f"  {name:11s} {d[8+k]/max(pods,1):9.0f} cycles/pod")
-for k, name in ((7, "w3 winner"), (13, "w3 excl+ld"), (14, "w3 eval"), (15, "w3 reduce")):
-    print(f"  {name:11s} {d[k]/max(pods,1):9.0f} cycles/pod")
+for k, name in ((0, "wave0 work"), (1, "wave0 wait"), (2, "wave1 work"), (3, "wave2 work"), (15, "wave3 work"),
+                (5, "w3 top"), (6, "w3 load"), (7, "w3 excl"), (8, "w3 eval"),
+                (11, "w1 fetch+fit"), (12, "w1 expiries"), (13, "w1 writes"), (14, "w1 eval")):
+    print(f"  {name:12s} {D[k]/max(pods,1):9.0f} cycles/pod")
+for k, name in ((9, "pass prune"), (10, "eval waves")):
+    print(f"  {name:12s} {D[k]/max(pods,1):9.2f} per pod")

@@ -17,11 +17,14 @@ MODES = {
 }
 
 
-def make_engine(trace, enc, mode, batch_pods=0, engine_flags=0):
+def make_engine(trace, enc, mode, batch_pods=0, engine_flags=0, shard=None):
+    """shard = (world, rank, comm_id, vshards) for a node-sharded engine (Engine.shard)."""
     from kubesim_amd.engine import Engine
     fm, fl, sc = MODES[mode] if isinstance(mode, str) else mode
     eng = Engine(tick_seconds=trace["tick_seconds"], filter_mode=fm, filters=fl, scorers=sc,
                  batch_pods=batch_pods, engine_flags=engine_flags)
+    if shard is not None:
+        eng.shard(*shard)
     eng.load_nodes(enc["alloc"], enc["taint"], enc["label"])
     return eng
 

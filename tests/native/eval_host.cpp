@@ -20,3 +20,52 @@ extern "C" int ks_host_lr(int64_t A, int64_t u) { return ks::lr_one(A, u); }
 extern "C" int ks_host_ba(int64_t Ac, int64_t Am, int64_t uc, int64_t um) { return ks::ba_score(Ac, Am, uc, um); }
 extern "C" int ks_host_lr_n(int32_t A, int32_t u) { return ks::lr_one_n(A, u); }
 extern "C" int ks_host_ba_n(int32_t Ac, int32_t Am, int32_t uc, int32_t um) { return ks::ba_score_n(Ac, Am, uc, um); }
+
+// batched forms for the CPU tests (tests/test_evaluator_host.py)
+extern "C" void ks_host_lr_n_batch(int64_t n, const int32_t* A, const int32_t* u, int32_t* out) {
+    for (int64_t i = 0; i < n; i++) out[i] = ks::lr_one_n(A[i], u[i]);
+}
+extern "C" void ks_host_ba_n_batch(int64_t n, const int32_t* Ac, const int32_t* Am, const int32_t* uc,
+                                   const int32_t* um, int32_t* out) {
+    for (int64_t i = 0; i < n; i++) out[i] = ks::ba_score_n(Ac[i], Am[i], uc[i], um[i]);
+}
+extern "C" void ks_host_ba_batch(int64_t n, const int64_t* Ac, const int64_t* Am, const int64_t* uc,
+                                 const int64_t* um, int32_t* out) {
+    for (int64_t i = 0; i < n; i++) out[i] = ks::ba_score(Ac[i], Am[i], uc[i], um[i]);
+}
+// per case: exact eval_total1 (wide and narrow) of pod req[i] on node i, and prune_tmax
+extern "C" void ks_host_prune_batch(const ks::Cfg* c, int64_t n, const int64_t* alloc /*[n][4]*/,
+                                    const int64_t* run /*[n][3]*/, const int64_t* req /*[n][3]*/,
+                                    uint32_t* total1, uint32_t* total1_n, uint32_t* tmax) {
+    for (int64_t i = 0; i < n; i++) {
+        ks::NodeV v{};
+        v.ac = alloc[i * 4 + 0]; v.am = alloc[i * 4 + 1]; v.ag = alloc[i * 4 + 2]; v.ap = alloc[i * 4 + 3];
+        v.rc = run[i * 3 + 0]; v.rm = run[i * 3 + 1]; v.rg = run[i * 3 + 2]; v.nr = 0;
+        ks::PodRec p{};
+        p.req[0] = req[i * 3 + 0]; p.req[1] = req[i * 3 + 1]; p.req[2] = req[i * 3 + 2];
+        p.keymask = 0xFF;
+        total1[i] = ks::eval_total1(*c, p, v);
+        total1_n[i] = ks::eval_total1_narrow(*c, p, v);
+        tmax[i] = ks::prune_tmax(*c, ks::prune_prep(*c, v), (float)p.req[0], (float)p.req[1]);
+    }
+}
+// guarded float evaluator: total1 through eval_g and the fraction of lanes that needed the exact path
+extern "C" double ks_host_fast_batch(const ks::Cfg* c, int64_t n, const int64_t* alloc, const int64_t* run,
+                                     const int64_t* req, int narrow, uint32_t* total1_g) {
+    int64_t needs = 0;
+    for (int64_t i = 0; i < n; i++) {
+        ks::NodeV v{};
+        v.ac = alloc[i * 4 + 0]; v.am = alloc[i * 4 + 1]; v.ag = alloc[i * 4 + 2]; v.ap = alloc[i * 4 + 3];
+        v.rc = run[i * 3 + 0]; v.rm = run[i * 3 + 1]; v.rg = run[i * 3 + 2]; v.nr = 0;
+        ks::PodRec p{};
+        p.req[0] = req[i * 3 + 0]; p.req[1] = req[i * 3 + 1]; p.req[2] = req[i * 3 + 2];
+        p.keymask = 0x7;
+        const float ic = ks::node_rcp(v.ac), im = ks::node_rcp(v.am);
+        bool need = false;
+        if (narrow) (void)ks::eval_fast<true>(*c, p, v, ic, im, need);
+        else (void)ks::eval_fast<false>(*c, p, v, ic, im, need);
+        needs += need;
+        total1_g[i] = narrow ? ks::eval_g<true>(*c, p, v, ic, im) : ks::eval_g<false>(*c, p, v, ic, im);
+    }
+    return n ? (double)needs / n : 0.0;
+}

@@ -166,3 +166,50 @@ def test_memory_unit_rescale_mid_run():
         assert_same_binds(eb, ob)
         assert erc == orc
         np.testing.assert_array_equal(eng.usage(), ora.usage())
+
+
+# ---- node sharding: per-shard top-L lists merged after an exchange ----------
+@pytest.mark.parametrize("vshards", [2, 3, 8])
+def test_virtual_shards_match_oracle(vshards):
+    """One rank, several node shards: the per-shard scan + merge + shard merge path."""
+    tr = small_trace(21, n_nodes=1500, n_pods=3000, taints=True, selectors=True)
+    enc = encoded(tr)
+    mode = "feeds_all_lrba"
+    eng = make_engine(tr, enc, mode, 256, shard=(1, 0, None, vshards))
+    eng.submit(enc["pods"])
+    ora = make_oracle(tr, mode)
+    ora.submit(tr)
+    for chunk in (700, 2300):
+        eb, erc = engine_run(eng, chunk, chunk)
+        ob, orc = oracle_run(ora, chunk)
+        assert_same_binds(eb, ob)
+        assert erc == orc
+        np.testing.assert_array_equal(eng.usage(), ora.usage())
+
+
+def test_rccl_exchange_single_rank():
+    """The RCCL all-gather path with a one-rank communicator (two virtual shards)."""
+    from kubesim_amd.engine import comm_unique_id
+    tr = small_trace(22, n_nodes=700, n_pods=1500)
+    enc = encoded(tr)
+    mode = "literal_lrba_filters_ignored"
+    eng = make_engine(tr, enc, mode, 128, shard=(1, 0, comm_unique_id(), 2))
+    eng.submit(enc["pods"])
+    ora = make_oracle(tr, mode)
+    ora.submit(tr)
+    eb, erc = engine_run(eng, 1500, 1500)
+    ob, orc = oracle_run(ora, 1500)
+    assert_same_binds(eb, ob)
+    assert erc == orc
+
+
+def test_shard_geometry_rejected():
+    from kubesim_amd.engine import Engine, KsError
+    eng = Engine()
+    with pytest.raises(KsError):
+        eng.shard(2, 0, None)  # world > 1 needs a communicator
+    with pytest.raises(KsError):
+        eng.shard(1, 1, None)
+    eng.load_nodes(np.array([[1000, 1000, -1, 10]]), np.zeros(1, np.uint64), np.zeros(1, np.uint64))
+    with pytest.raises(KsError):
+        eng.shard(1, 0, None, 2)  # after load_nodes

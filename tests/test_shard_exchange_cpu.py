@@ -1,0 +1,90 @@
+"""Node sharding exchange on CPU with gloo, world_size 2.
+
+Each rank evaluates pods against its node shard only (the oracle's Filter+Score,
+oracle/ks_oracle.c ko_eval), keeps the exact per-pod top-L packed keys, the lists are
+all-gathered, and the merge must equal the global top-L — whose head is the oracle's bind.
+This is the algorithm the device runs (ks_engine.cpp ks_step: per-shard merge, RCCL
+all-gather, merge); the GPU suite checks the device path itself (tests/test_engine_gpu.py).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from harness import make_oracle, small_trace
+from kubesim_amd import shard
+
+MODE = "feeds_all_lrba"
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(rank, world, port, n_nodes, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tr = small_trace(31, n_nodes=n_nodes, n_pods=400, selectors=False)
+        ora = make_oracle(tr, MODE)
+        ora.submit(tr)
+        b, rc = ora.step(150)  # a non-trivial cluster state: pods running, some expired
+        assert rc == 0, rc
+        lo, hi = shard.rank_nodes(n_nodes, world, rank)
+        pods = list(range(150, 182))  # the next pods in FIFO order
+        mine = np.zeros((len(pods), shard.TOP_L), np.uint64)
+        full = []
+        for i, p in enumerate(pods):
+            feas, score = ora.eval(p)
+            keys = shard.packed_keys(score, (feas != 0) & (score >= 0))
+            full.append(shard.top_l(keys))
+            if hi > lo:
+                mine[i] = shard.top_l(shard.packed_keys(score[lo:hi], (feas[lo:hi] != 0) & (score[lo:hi] >= 0), lo))
+        t = torch.from_numpy(mine.view(np.int64).copy())
+        parts = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        merged = shard.merge_lists(np.stack([x.numpy().view(np.uint64) for x in parts]))
+        ok = np.array_equal(merged, np.stack(full))
+        # the head of the merged list is the oracle's next bind
+        nb, rc = ora.step(1)
+        head_node = 0xFFFFFFFF - int(merged[0, 0] & np.uint64(0xFFFFFFFF))
+        q.put((rank, bool(ok), rc, int(nb["node"][0]) if len(nb["node"]) else -1, head_node, lo, hi))
+    except BaseException as e:  # report instead of leaving the parent waiting
+        q.put((rank, False, repr(e), -1, -2, -1, -1))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_nodes", [300, 1024, 1500])
+def test_shard_exchange_gloo_world2(n_nodes):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, n_nodes, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ranges = [(r[5], r[6]) for r in res]
+    assert ranges[0][0] == 0 and ranges[-1][1] == n_nodes and ranges[0][1] == ranges[1][0]
+    for rank, ok, rc, bind_node, head_node, lo, hi in res:
+        assert ok, f"rank {rank}: merged shard lists differ from the global top-L"
+        assert rc == 0 and bind_node == head_node
+
+
+def test_part_blocks_match_engine_geometry():
+    # ks_load_nodes: n_pad = max(64, ceil64(n)); nblk = ceil(n_pad / 256); part p = p * nblk / G
+    pb = shard.part_blocks(50_000, 8, 1)
+    assert pb[0] == 0 and pb[-1] == (50_048 + 255) // 256 and np.all(np.diff(pb) >= 24)
+    assert shard.rank_nodes(1000, 4, 3) == (768, 1000)
+    assert shard.rank_nodes(100, 4, 0) == (0, 0)  # one block: parts 0..2 empty
