@@ -87,9 +87,10 @@ typedef struct {
     int32_t reserved[7];
 } ks_config;
 
-/* engine_flags: FORCE_WIDE keeps the 64/128-bit evaluator even when every scaled capacity fits
- * the 32-bit one (both are exact; this exists to test them against each other). */
-enum { KS_ENGINE_FORCE_WIDE = 1 };
+/* engine_flags: the engine picks the narrowest exact evaluator the scaled capacities allow
+ * (tiny int32 / narrow 32x32->64 / wide 64/128-bit).  FORCE_WIDE keeps the wide one, NO_TINY
+ * skips the tiny one; all are exact, the flags exist to test them against each other. */
+enum { KS_ENGINE_FORCE_WIDE = 1, KS_ENGINE_NO_TINY = 2 };
 
 typedef struct {
     int64_t pod;    /* FIFO index (submission order) */

@@ -46,6 +46,7 @@ struct alignas(16) PodRec {
 static_assert(sizeof(PodRec) == 48, "PodRec layout");
 
 // Node state: 80 B per node, stored struct-of-arrays in HBM.
+// One allocation, field k at ac + k * stride (ks_load_nodes), so a field index is an offset.
 struct NodeSoA {
     int64_t* ac;   // alloc cpu (milli; -1 absent)
     int64_t* am;   // alloc memory
@@ -229,9 +230,70 @@ __host__ __device__ __forceinline__ uint32_t eval_total1_narrow(const Cfg& c, co
     return (uint32_t)total + 1u;
 }
 
-template <bool kNarrow>
+// ---------------------------------------------------------------------------------------------
+// Tiny evaluator: every scaled capacity below 2^26 and Ac * Am below 2^26 (C2 / C3 after the gcd
+// scaling: cpu <= 1280 units, memory <= 2048).  Requests are clamped to 2^27 (any request above
+// every capacity behaves the same), so every product and sum — 10 (A - u), q A, Ac Am,
+// uc Am, 10 (D - X), q D — fits int32; each floor is a float estimate (error < 1e-5) corrected
+// exactly by one int32 compare on each side.  No 64-bit multiply and no double on the path.
+// ---------------------------------------------------------------------------------------------
+constexpr int64_t kTinyCap = 1LL << 26;
+constexpr int64_t kTinyReq = 1LL << 27;
+
+__host__ __device__ __forceinline__ int32_t clamp_tiny(int64_t q) { return (int32_t)(q < kTinyReq ? q : kTinyReq); }
+
+// floor(y / A) for 0 <= y <= 10 A, A < 2^26, given iA ~ 1/A
+__host__ __device__ __forceinline__ int32_t div10_tiny(int32_t y, int32_t A, float iA) {
+    int32_t q = (int32_t)((float)y * iA);
+    q = q < 0 ? 0 : (q > 10 ? 10 : q);
+    const int32_t t = q * A;
+    q += (y >= t + A) ? 1 : 0;
+    q -= (y < t) ? 1 : 0;
+    return q;
+}
+
+__host__ __device__ __forceinline__ uint32_t eval_total1_tiny(const Cfg& c, const PodRec& p, const NodeV& n) {
+    // Branch-free: every floor is computed on safe inputs and selected, so the LR / LR / BA
+    // chains interleave even when a single lane evaluates (the resolver's bind wave).
+    const int32_t ac = (int32_t)n.ac, am = (int32_t)n.am, ag = (int32_t)n.ag;
+    const int32_t rc = (int32_t)n.rc, rm = (int32_t)n.rm, rg = (int32_t)n.rg;
+    const int32_t qc = clamp_tiny(p.req[0]), qm = clamp_tiny(p.req[1]), qg = clamp_tiny(p.req[2]);
+    const int32_t uc = rc + qc, um = rm + qm;
+    const bool fit_on = c.filter_feeds && (c.filters & kFilterFit);
+    const bool taint_on = c.filter_feeds && (c.filters & kFilterTaint);
+    const bool sel_on = c.filter_feeds && (c.filters & kFilterSelector);
+    bool ok = c.has_scorers != 0;
+    ok &= !fit_on || ((n.nr < n.ap) & (!(p.keymask & 1) || uc <= ac) & (!(p.keymask & 2) || um <= am) &
+                      (!(p.keymask & 4) || rg + qg <= ag));
+    ok &= !taint_on || (n.taint & ~p.tol) == 0;
+    ok &= !sel_on || (n.label & p.sel) == p.sel;
+    const bool lc_on = ac > 0 && uc <= ac, lm_on = am > 0 && um <= am;
+    const int32_t acs = ac > 0 ? ac : 1, ams = am > 0 ? am : 1;
+    const float iac = rcp_est((float)acs), iam = rcp_est((float)ams);  // node-invariant: hoisted
+    const int32_t lc = div10_tiny(lc_on ? 10 * (ac - uc) : 0, acs, iac);
+    const int32_t lm = div10_tiny(lm_on ? 10 * (am - um) : 0, ams, iam);
+    const bool ba_on = ac > 0 && am > 0 && uc < ac && um < am;
+    const int32_t ucs = ba_on ? uc : 0, ums = ba_on ? um : 0;
+    const int32_t D = acs * ams, a = ucs * ams, b = ums * acs;
+    const int32_t X = a > b ? a - b : b - a;
+    const int32_t N = 10 * (D - X);
+    int32_t q = (int32_t)(10.f - 10.f * fabsf((float)ucs * iac - (float)ums * iam));
+    q = q < 0 ? 0 : (q > 10 ? 10 : q);
+    const int32_t t = q * D;
+    q += (N >= t + D) ? 1 : 0;
+    q -= (N < t) ? 1 : 0;
+    const int32_t total = c.const_total + c.w_lr * (((lc_on ? lc : 0) + (lm_on ? lm : 0)) >> 1) +
+                          c.w_ba * (ba_on ? q : 0);
+    return ok ? (uint32_t)total + 1u : 0u;
+}
+
+// Evaluator variants: 0 wide (64/128-bit), 1 narrow (capacities < 2^29), 2 tiny (see above).
+enum : int { kEvalWide = 0, kEvalNarrow = 1, kEvalTiny = 2 };
+
+template <int kMode>
 __host__ __device__ __forceinline__ uint32_t eval_t(const Cfg& c, const PodRec& p, const NodeV& n) {
-    if constexpr (kNarrow) return eval_total1_narrow(c, p, n);
+    if constexpr (kMode == kEvalTiny) return eval_total1_tiny(c, p, n);
+    else if constexpr (kMode == kEvalNarrow) return eval_total1_narrow(c, p, n);
     else return eval_total1(c, p, n);
 }
 
@@ -257,12 +319,12 @@ __host__ __device__ __forceinline__ int32_t floor_guarded(float y, float guard, 
     return q;
 }
 
-template <bool kNarrow>
+template <int kMode>
 __host__ __device__ __forceinline__ uint32_t eval_fast(const Cfg& c, const PodRec& p, const NodeV& n, float ic,
                                                        float im, bool& need) {
     if (!c.has_scorers) return 0;
     int64_t uc, um;
-    if constexpr (kNarrow) {
+    if constexpr (kMode != kEvalWide) {
         const int32_t qc = clamp_req(p.req[0]), qm = clamp_req(p.req[1]);
         const int32_t ucn = (int32_t)n.rc + qc, umn = (int32_t)n.rm + qm;
         if (c.filter_feeds) {
@@ -305,11 +367,11 @@ __host__ __device__ __forceinline__ uint32_t eval_fast(const Cfg& c, const PodRe
 }
 
 // eval_t through the guarded float path (exact: falls back per lane)
-template <bool kNarrow>
+template <int kMode>
 __host__ __device__ __forceinline__ uint32_t eval_g(const Cfg& c, const PodRec& p, const NodeV& n, float ic, float im) {
     bool need = false;
-    uint32_t t = eval_fast<kNarrow>(c, p, n, ic, im, need);
-    if (need) t = eval_t<kNarrow>(c, p, n);
+    uint32_t t = eval_fast<kMode>(c, p, n, ic, im, need);
+    if (need) t = eval_t<kMode>(c, p, n);
     return t;
 }
 
@@ -410,14 +472,14 @@ int max_batch_pods();
 int max_pods_per_scan_wg();
 int block_nodes();
 // expire_head + scan of blocks [blk_lo, blk_lo + blk_n)
-hipError_t launch_scan(const EngineArgs& a, bool narrow, hipStream_t st);
+hipError_t launch_scan(const EngineArgs& a, int mode, hipStream_t st);
 // per pod b < batch size: exact top-L over nl sorted lists lists[b*pod_stride + k*list_stride]
 hipError_t launch_merge(const EngineArgs& a, const uint64_t* lists, int64_t pod_stride, int32_t nl,
                         int64_t list_stride, uint64_t* out, hipStream_t st);
-hipError_t launch_resolve(const EngineArgs& a, bool narrow, hipStream_t st);
+hipError_t launch_resolve(const EngineArgs& a, int mode, hipStream_t st);
 hipError_t launch_rescale(const NodeSoA& s, int64_t n_pad, PodRec* pods, int64_t P, const int64_t f[3], hipStream_t st);
 hipError_t launch_eval_pod(const Cfg& c, const NodeSoA& s, const PodRec* pod, uint32_t filters, uint8_t* mask,
-                           int64_t* score, bool narrow, hipStream_t st);
+                           int64_t* score, int mode, hipStream_t st);
 hipError_t launch_flush(const NodeSoA& s, const PodRec* pods, const int64_t* fin, int64_t t, int64_t n_done,
                         const int32_t* b_node, const int32_t* b_status, uint8_t* expired, hipStream_t st);
 hipError_t launch_usage(int64_t q_lo, int64_t q_hi, int64_t t, int32_t tick_s, const int32_t* b_node,

@@ -12,7 +12,9 @@
 //    g_k = gcd of every capacity and request of k seen so far (exact: every fit / LeastRequested
 //    / BalancedAllocation result is unit-free).  A pod whose request g_k does not divide shrinks
 //    the unit (rescale_kernel multiplies the device state by g_k / g_k').  When every scaled
-//    capacity is < 2^29 the kernels use the narrow (32-bit) evaluator, else the 64/128-bit one.
+//    capacity is < 2^29 the kernels use the narrow (32-bit) evaluator, when moreover every scaled
+//    capacity and the largest cpu x memory product are < 2^26 the tiny (int32-only) one, else
+//    the 64/128-bit one.
 //  * batching: launches (expire_head, scan, merge, resolve) until the device counter says
 //    every pod due in [tick+1, tick+ticks] is bound, then copies the binds back.
 //  * node sharding (ks_shard): every rank holds the whole node state and runs
@@ -116,8 +118,8 @@ struct ks_engine {
     int64_t last_arrival = 0;
     int64_t scale[3] = {1, 1, 1};   // device unit of cpu / memory / gpu, in milli-units
     int64_t max_alloc[3] = {0, 0, 0};  // largest capacity per resource, milli-units
-    bool narrow = false;
-    bool force_wide = false;
+    int mode = ks::kEvalWide;  // evaluator variant (ks_device.h)
+    uint32_t flags = 0;        // KS_ENGINE_*
     std::vector<int64_t> h_exp_pos;  // global exp_pod index holding pod q's own expiry, or -1
 
     // progress
@@ -190,10 +192,14 @@ ks::EngineArgs make_args(ks_engine* e) {
     return a;
 }
 
-void update_narrow(ks_engine* e) {
-    bool ok = !e->force_wide;
-    for (int k = 0; k < 3; k++) ok &= e->max_alloc[k] / e->scale[k] < ks::kNarrowCap;
-    e->narrow = ok;
+void update_mode(ks_engine* e) {
+    int64_t m[3];
+    for (int k = 0; k < 3; k++) m[k] = e->max_alloc[k] / e->scale[k];
+    const bool narrow = m[0] < ks::kNarrowCap && m[1] < ks::kNarrowCap && m[2] < ks::kNarrowCap;
+    const bool tiny = m[0] < ks::kTinyCap && m[1] < ks::kTinyCap && m[2] < ks::kTinyCap && m[0] * m[1] < ks::kTinyCap;
+    e->mode = (e->flags & KS_ENGINE_FORCE_WIDE) ? ks::kEvalWide
+            : (tiny && !(e->flags & KS_ENGINE_NO_TINY)) ? ks::kEvalTiny
+            : narrow ? ks::kEvalNarrow : ks::kEvalWide;
 }
 
 }  // namespace
@@ -210,7 +216,7 @@ ks_status ks_create(const ks_config* cfg, ks_engine** out) {
     if (cfg->filters & ~7u) return KS_EINVAL;
     if (cfg->n_scorers < 0 || cfg->n_scorers > 8) return KS_EINVAL;
     if (cfg->batch_pods < 0 || cfg->batch_pods > kMaxBatch) return KS_EINVAL;
-    if (cfg->engine_flags & ~(uint32_t)KS_ENGINE_FORCE_WIDE) return KS_EINVAL;
+    if (cfg->engine_flags & ~(uint32_t)(KS_ENGINE_FORCE_WIDE | KS_ENGINE_NO_TINY)) return KS_EINVAL;
     int64_t const_total = 0, w_lr = 0, w_ba = 0;
     for (int i = 0; i < cfg->n_scorers; i++) {
         const ks_scorer& sc = cfg->scorers[i];
@@ -231,7 +237,7 @@ ks_status ks_create(const ks_config* cfg, ks_engine** out) {
     e->cfg = *cfg;
     e->device = cfg->device;
     e->B = cfg->batch_pods ? cfg->batch_pods : kDefaultBatch;
-    e->force_wide = (cfg->engine_flags & KS_ENGINE_FORCE_WIDE) != 0;
+    e->flags = cfg->engine_flags;
     e->dc.filter_feeds = cfg->filter_mode == KS_FILTER_FEEDS_SCORE;
     e->dc.filters = cfg->filters;
     e->dc.has_scorers = cfg->n_scorers > 0;
@@ -336,7 +342,7 @@ ks_status ks_load_nodes(ks_engine* e, int64_t n, const int64_t* alloc, const uin
         e->scale[k] = g > 0 ? g : 1;
         e->max_alloc[k] = mx;
     }
-    update_narrow(e);
+    update_mode(e);
     std::vector<int64_t> h(10 * np, 0);
     for (int64_t i = 0; i < np; i++) {
         const bool real = i < n;
@@ -420,7 +426,7 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
             HIPCHK(e, hipSetDevice(e->device));
             HIPCHK(e, ks::launch_rescale(e->s, e->n_pad, e->pods.p, e->P, f, e->st));
             HIPCHK(e, hipStreamSynchronize(e->st));
-            update_narrow(e);
+            update_mode(e);
         }
     }
     std::vector<ks::PodRec> recs(m);
@@ -548,7 +554,7 @@ ks_status ks_step(ks_engine* e, int64_t ticks, ks_bind* out, int64_t cap, int64_
                 e2 = e->prof_ev[3 * launches + 2];
             }
             if (e0) HIPCHK(e, hipEventRecord(e0, st));
-            HIPCHK(e, ks::launch_scan(a, e->narrow, st));
+            HIPCHK(e, ks::launch_scan(a, e->mode, st));
             const int G = e->world * e->vsh;
             const int64_t L = ks::kTopL, BL = (int64_t)e->B * L;
             if (G == 1) {
@@ -567,7 +573,7 @@ ks_status ks_step(ks_engine* e, int64_t ticks, ks_bind* out, int64_t cap, int64_
                 HIPCHK(e, ks::launch_merge(a, e->cand_all, L, G, BL, e->cand, st));
             }
             if (e1) HIPCHK(e, hipEventRecord(e1, st));
-            HIPCHK(e, ks::launch_resolve(a, e->narrow, st));
+            HIPCHK(e, ks::launch_resolve(a, e->mode, st));
             if (e2) HIPCHK(e, hipEventRecord(e2, st));
             launches++;
         }
@@ -637,7 +643,7 @@ static ks_status eval_pod(ks_engine* e, int64_t pod) {
     ks_status r = flush_expiries(e);
     if (r != KS_OK) return r;
     if (e->n == 0) return KS_OK;
-    HIPCHK(e, ks::launch_eval_pod(e->dc, e->s, e->pods.p + pod, e->cfg.filters, e->d_mask, e->d_score, e->narrow, e->st));
+    HIPCHK(e, ks::launch_eval_pod(e->dc, e->s, e->pods.p + pod, e->cfg.filters, e->d_mask, e->d_score, e->mode, e->st));
     return KS_OK;
 }
 

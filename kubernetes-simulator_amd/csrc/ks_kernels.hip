@@ -18,8 +18,9 @@
 //                list scores below every list entry.  winner = max(those).  If all L entries
 //                are touched the batch commits early and the next batch rescans.
 //
-// Every kernel that evaluates exists twice: kNarrow = true is the 32-bit evaluator, used when
-// every scaled capacity fits (ks_device.h); kNarrow = false the general 64/128-bit one.
+// Every kernel that evaluates exists three times, one per evaluator (ks_device.h): kEvalTiny
+// (int32 math; capacities and Ac*Am < 2^26), kEvalNarrow (capacities < 2^29), kEvalWide
+// (64/128-bit, any capacity < 2^59).  The host picks the narrowest that holds.
 //
 // Packed key: (total + 1) << 32 | (0xFFFFFFFF - node); 0 = no candidate (NotFound).  Max key =
 // highest total, ties to the lowest node index.
@@ -32,16 +33,11 @@ constexpr int kBlockNodes = kScanWaves * kWave;
 constexpr int kL = kTopL;                // candidate list length per pod
 constexpr int kMaxPG = 32;               // pods per scan workgroup (LDS list staging)
 constexpr int kResolveThreads = 1024;    // 16 waves
-constexpr int kOwnerWave0 = 3;           // waves 3..15 own the touched entries ...
-#ifndef KS_SPARE1
-#define KS_SPARE1 1
-#endif
-// ... except, with KS_SPARE1, waves 5, 9, 13: they share wave 1's SIMD (waves are dealt to the
-// four SIMDs round-robin) and wave 1 carries each pod's critical path (bind, then the next
-// pod's key on the bound node), so they stay idle
-constexpr int kOwnerWaves = KS_SPARE1 ? 10 : 13;
+constexpr int kOwnerWave0 = 3;           // waves 3..15 own the touched entries, except
+constexpr int kWriterWave = 5;           // the bind's bookkeeping writer (off the critical path)
+constexpr int kOwnerWaves = kResolveThreads / kWave - kOwnerWave0 - 1;
 constexpr int kOwners = kOwnerWaves * kWave;
-constexpr int kTMax = KS_SPARE1 ? 640 : 768;  // touched-node table (LDS); <= kOwners
+constexpr int kTMax = 768;               // touched-node table (LDS); <= kOwners
 constexpr int kHash = 2048;              // open-addressing node -> entry map (LDS)
 constexpr int kMaxBatchR = 256;          // pods per resolve launch
 constexpr int kMaxExp = kTMax - kMaxBatchR;  // expiries pre-inserted per batch
@@ -55,10 +51,8 @@ enum : int64_t { kErrEinval = 1, kErrNotFound = 2 };
 
 // owner slot of a resolve wave, or -1
 __device__ __forceinline__ int owner_slot(int wave) {
-    if (wave < kOwnerWave0) return -1;
-    if (!KS_SPARE1) return wave - kOwnerWave0;
-    if ((wave & 3) == 1) return -1;
-    return wave - kOwnerWave0 - (wave > 5) - (wave > 9) - (wave > 13);
+    if (wave < kOwnerWave0 || wave == kWriterWave) return -1;
+    return wave - kOwnerWave0 - (wave > kWriterWave);
 }
 
 __device__ __forceinline__ int popc_below(uint64_t mask, int lane) {
@@ -92,7 +86,7 @@ __global__ __launch_bounds__(256) void expire_head_kernel(EngineArgs a) {
 // (lowest lanes first), repeat below it — a 32-bit wave max + ballot per class.  The four
 // wave lists are then merged by rank (each list is sorted) into the block's top-L.
 // ------------------------------------------------------------------------------------------
-template <bool kNarrow>
+template <int kMode>
 __global__ __launch_bounds__(256) void scan_kernel(EngineArgs a) {
     __shared__ uint64_t wl[kMaxPG][kScanWaves][kL];  // per-pod, per-wave top-L lists
     const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
@@ -110,7 +104,7 @@ __global__ __launch_bounds__(256) void scan_kernel(EngineArgs a) {
     const int np = (int)min<int64_t>(a.PG, nb - pg0);
     for (int b = 0; b < np; ++b) {
         const PodRec p = a.pods[start + pg0 + b];
-        uint32_t rem = valid ? eval_t<kNarrow>(a.c, p, n) : 0u;
+        uint32_t rem = valid ? eval_t<kMode>(a.c, p, n) : 0u;
         int cnt = 0;
         for (int r = 0; r < kL && cnt < kL; ++r) {
             const uint32_t m = wave_max_u32(rem);
@@ -211,7 +205,7 @@ __global__ __launch_bounds__(256) void merge_kernel(EngineArgs a, const uint64_t
 // ------------------------------------------------------------------------------------------
 // resolve: one workgroup, sequential over the batch in FIFO order (one bind per tick).
 //
-// One barrier per pod.  Pod i's winner is a single LDS word best[i % 3]: every contributor of
+// One barrier per pod.  Pod i's winner is a single LDS word ctl[i % 3].best: every contributor of
 // pod i (list candidate, re-evaluated touched entries) folds its key in with an LDS atomic max
 // during iteration i-1, so after the barrier every wave reads the decision (and the NotFound /
 // InvalidArgument / exhausted-list stops) with one load.  Internal key (ikey):
@@ -241,6 +235,23 @@ __global__ __launch_bounds__(256) void merge_kernel(EngineArgs a, const uint64_t
 // float upper bound (prune_tmax) is below it is not evaluated, and exact keys below it are not
 // folded into best.
 // ------------------------------------------------------------------------------------------
+// Per-pod control read by every wave right after the barrier: one 16/32-byte LDS load each,
+// issued together (a chain of dependent reads here costs ~150 cycles per link).
+struct alignas(16) Ctl {
+    uint64_t best;   // pod's winner (ikey), folded during the previous iteration
+    uint64_t lbk;    // lower bound of the pod's winner key (prefetch_issue)
+    int32_t kfull;   // every entry of a full list touched: the batch must stop
+    int32_t ntab;    // table size when the pod is evaluated
+    int32_t pad[2];
+};
+struct alignas(16) PodCtl {
+    uint32_t flags;
+    int32_t ex_lo, ex_hi;  // window range of the expiries due before the pod binds
+    int32_t dur;           // ticks the pod runs if bound Ok
+    int32_t exp_slot;      // window slot of this pod's own expiry, or -1
+    int32_t pad[3];
+};
+
 struct ResolveShared {
     int64_t ts[8][kTMax];       // touched-node state: ac am ag ap rc rm rg nr
     uint64_t tu[2][kTMax];      // taint label
@@ -249,22 +260,17 @@ struct ResolveShared {
     int32_t hkey[kHash];        // node id or -1
     int32_t hval[kHash];        // entry index
     uint32_t tfilt[kFilterBits / 32];
-    PodRec pod[kMaxBatchR];
+    PodRec pod[kMaxBatchR + 1];  // +1: pod i + 1 is read unconditionally
     float podf[kMaxBatchR][2];  // cpu / memory requests as float (prune_tmax)
-    int32_t dur[kMaxBatchR];
-    int32_t exp_slot[kMaxBatchR];  // window slot of an in-batch pod's own expiry, or -1
+    PodCtl pctl[kMaxBatchR + 1];
     uint64_t cand[kMaxBatchR][kL];
-    int32_t ex_off[kMaxBatchR + 1];
     int32_t ex_q[kMaxExp];
     int32_t ex_node[kMaxExp];
     int32_t ex_ok[kMaxExp];     // the expiring pod was bound Ok and has not expired yet
     int32_t ex_entry[kMaxExp];  // table entry of its node (set at the bind for in-batch pods)
     int64_t ex_req[kMaxExp][3];
-    uint64_t best[3];           // pod i's winner (ikey), folded during iteration i-1
+    Ctl ctl[3];                 // pod i's decision state, slot i % 3
     int64_t stage[2][10];       // snapshot fields of the pod's best untouched list node
-    int32_t kfull[2];           // every entry of a full list touched: the batch must stop
-    uint64_t lbk[2];            // lower bound of the pod's winner key (see prefetch_issue)
-    int32_t ntab[2];            // table size when the pod is evaluated
     int32_t n_t, committed, err_code, err_pod, nb;
 };
 
@@ -326,11 +332,23 @@ __device__ __forceinline__ void h_insert(ResolveShared& sh, int32_t node, int32_
     sh.tfilt[f >> 5] |= 1u << (f & 31);
 }
 
-// touched? — one LDS read unless the filter bit is shared with another node
-__device__ __forceinline__ bool is_touched(const ResolveShared& sh, int32_t node) {
+// touched? — one LDS read; the filter is exact (node & 0xFFFF is injective) when the cluster has
+// at most kFilterBits nodes, otherwise a set bit is confirmed in the hash
+__device__ __forceinline__ bool is_touched(const ResolveShared& sh, int32_t node, bool exact) {
     const uint32_t f = (uint32_t)node & (kFilterBits - 1);
     if (!((sh.tfilt[f >> 5] >> (f & 31)) & 1u)) return false;
-    return h_find(sh, node) >= 0;
+    return exact || h_find(sh, node) >= 0;
+}
+
+// table insert of an in-loop winner: with an exact filter only the filter bit (the hash is
+// consulted only by the batch-start pre-insert and by inexact filters)
+__device__ __forceinline__ void t_insert(ResolveShared& sh, int32_t node, int32_t idx, bool exact) {
+    if (exact) {
+        const uint32_t f = (uint32_t)node & (kFilterBits - 1);
+        atomicOr(&sh.tfilt[f >> 5], 1u << (f & 31));
+    } else {
+        h_insert(sh, node, idx);
+    }
 }
 
 __device__ __forceinline__ NodeV t_node(const ResolveShared& sh, int e) {
@@ -349,70 +367,113 @@ __device__ __forceinline__ NodeV stage_node(const ResolveShared& sh, int b) {
     return v;
 }
 
-// field f (0..9, NodeV order) of node i: one load per lane, the field pointer by selects
+// field f (0..9, NodeV order) of node i: the SoA is one allocation with a fixed field stride
 __device__ __forceinline__ int64_t node_field(const NodeSoA& s, int f, int64_t i) {
-    const int64_t* p = f == 0 ? s.ac : f == 1 ? s.am : f == 2 ? s.ag : f == 3 ? s.ap : f == 4 ? s.rc
-                     : f == 5 ? s.rm : f == 6 ? s.rg : f == 7 ? s.nr : f == 8 ? (const int64_t*)s.taint
-                     : (const int64_t*)s.label;
-    return p[i];
+    return s.ac[(int64_t)f * (s.am - s.ac) + i];
 }
 
 __device__ __forceinline__ int32_t key_node(uint64_t key) { return (int32_t)(0xFFFFFFFFu - (uint32_t)key); }
 
-// Wave 0: first two entries of pod i's list whose node is not in the touched table (-1 if
-// none); `full` = the list holds L candidates (so "none" means exhausted, not "no candidates").
-__device__ __forceinline__ void first_untouched2(const ResolveShared& sh, int i, int lane, int& pa1, int& pa2,
-                                                 bool& full) {
-    const uint64_t c = lane < kL ? sh.cand[i][lane] : 0ull;
-    const bool ok = c != 0 && !is_touched(sh, key_node(c));
-    uint64_t m = __ballot(ok);
-    full = __popcll(__ballot(c != 0)) == kL;
-    pa1 = m ? __ffsll((unsigned long long)m) - 1 : -1;
-    m &= m - 1;
-    pa2 = m ? __ffsll((unsigned long long)m) - 1 : -1;
+// A pod record read from LDS as three 16-byte loads issued together, pinned in registers by an
+// empty asm use (otherwise the compiler sinks each field's load into the config branch that
+// uses it, turning one LDS round trip into several dependent ones).
+__device__ __forceinline__ PodRec pod_regs(const PodRec* src) {
+    const uint4* w = reinterpret_cast<const uint4*>(src);
+    const uint4 w0 = w[0], w1 = w[1], w2 = w[2];
+    asm volatile("" ::"v"(w0.x), "v"(w0.y), "v"(w0.z), "v"(w0.w), "v"(w1.x), "v"(w1.y), "v"(w1.z), "v"(w1.w),
+                 "v"(w2.x), "v"(w2.y), "v"(w2.z), "v"(w2.w));
+    PodRec p;
+    static_assert(sizeof(PodRec) == 3 * sizeof(uint4), "PodRec is three 16-byte words");
+    __builtin_memcpy(&p, &w0, 16);
+    __builtin_memcpy(reinterpret_cast<char*>(&p) + 16, &w1, 16);
+    __builtin_memcpy(reinterpret_cast<char*>(&p) + 32, &w2, 16);
+    return p;
 }
 
-// Wave 0 prefetch state for one pod: lanes 0..19 hold field (lane % 10) of slot lane / 10
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Wave 0 prefetch state for one pod: its first two list entries whose node is untouched
+// (key1, key2; 0 = none), whether the list holds L candidates (so "none" means exhausted, not
+// "no candidates"), and their records: lanes 0..19 hold field (lane % 10) of entry lane / 10.
 struct Prefetch {
     int64_t val;
-    int pa1, pa2;
-    int32_t node1;
+    uint64_t key1, key2;
     bool full;
 };
 
-// Also publishes pod p's winner lower bound: the first untouched entry when pod p is decided is
-// the first or the second prefetched one (or none: then the batch stops at a full list, or the
-// list is short and the bound is 0), so the second one — or the first when the list is full and
-// has no second — is <= it.
-__device__ __forceinline__ void prefetch_issue(const EngineArgs& a, ResolveShared& sh, int p, int lane,
+// Walk pod p's list against the table and issue the record loads.  Also publishes pod p's
+// winner lower bound: the first untouched entry when pod p is decided is key1 or key2 (or none:
+// then the batch stops at a full list, or the list is short and the bound is 0), so key2 — or
+// key1 when the list is full and has no second — is <= it.
+__device__ __forceinline__ void prefetch_issue(const EngineArgs& a, ResolveShared& sh, int p, int lane, bool exact,
                                                Prefetch& pf) {
-    first_untouched2(sh, p, lane, pf.pa1, pf.pa2, pf.full);
-    if (lane == 0)
-        sh.lbk[p & 1] = pf.pa2 >= 0 ? sh.cand[p][pf.pa2] : (pf.full && pf.pa1 >= 0 ? sh.cand[p][pf.pa1] : 0ull);
-    pf.node1 = pf.pa1 >= 0 ? key_node(sh.cand[p][pf.pa1]) : -1;
-    const int slot_pa = lane < 10 ? pf.pa1 : pf.pa2;
-    if (lane < 20 && slot_pa >= 0) pf.val = node_field(a.s, lane % 10, key_node(sh.cand[p][slot_pa]));
+    const uint64_t c = lane < kL ? sh.cand[p][lane] : 0ull;
+    const bool ok = c != 0 && !is_touched(sh, key_node(c), exact);
+    uint64_t m = __ballot(ok);
+    pf.full = __popcll(__ballot(c != 0)) == kL;
+    const int pa1 = m ? __ffsll((unsigned long long)m) - 1 : -1;
+    m &= m - 1;
+    const int pa2 = m ? __ffsll((unsigned long long)m) - 1 : -1;
+    pf.key1 = pa1 >= 0 ? readlane64(c, pa1) : 0ull;
+    pf.key2 = pa2 >= 0 ? readlane64(c, pa2) : 0ull;
+    if (lane == 0) sh.ctl[p % 3].lbk = pf.key2 ? pf.key2 : (pf.full ? pf.key1 : 0ull);
+    const uint64_t ks = lane < 10 ? pf.key1 : pf.key2;
+    if (lane < 20 && ks != 0) pf.val = node_field(a.s, lane % 10, key_node(ks));
 }
 
 // Wave 0: pod p's best untouched list node given that `winner` just joined the table (-1:
-// none): stage its record, fold its key into best[bslot], set kfull.
-__device__ __forceinline__ void prefetch_commit(ResolveShared& sh, int p, int lane, const Prefetch& pf,
-                                                int32_t winner, int stage_buf, int bslot) {
-    const int slot = (pf.pa1 >= 0 && pf.node1 == winner) ? 1 : 0;
-    const int pa = slot ? pf.pa2 : pf.pa1;
-    if (pa >= 0 && lane < 20 && lane / 10 == slot) sh.stage[stage_buf][lane % 10] = pf.val;
+// none): stage its record, fold its key into ctl[bslot].best, set kfull.
+__device__ __forceinline__ void prefetch_commit(ResolveShared& sh, int lane, const Prefetch& pf, int32_t winner,
+                                                int stage_buf, int bslot) {
+    const int slot = (pf.key1 != 0 && key_node(pf.key1) == winner) ? 1 : 0;
+    const uint64_t key = slot ? pf.key2 : pf.key1;
+    if (key != 0 && lane < 20 && lane / 10 == slot) sh.stage[stage_buf][lane % 10] = pf.val;
     if (lane == 0) {
-        if (pa >= 0) fold_best(&sh.best[bslot], ikey(sh.cand[p][pa], kEntUntouched));
-        sh.kfull[stage_buf] = pa < 0 && pf.full;
+        if (key != 0) fold_best(&sh.ctl[bslot].best, ikey(key, kEntUntouched));
+        sh.ctl[bslot].kfull = key == 0 && pf.full;
     }
 }
 
-template <bool kNarrow>
+// The expiries due before pod j + 1 binds (window range [e0, e1)) that land on entry t — pod
+// j's own included when it was bound Ok and runs one tick — subtracted from n.  Lane-parallel:
+// one LDS round for the whole range; the (usually zero or one) hits are folded via a ballot.
+// Marks them expired when `expired` is given (the writer wave).
+__device__ __forceinline__ void expire_on(const ResolveShared& sh, int e0, int e1, int t, int64_t j, bool ok,
+                                          int lane, NodeV& n, uint8_t* expired) {
+    for (int x0 = e0; x0 < e1; x0 += kWave) {
+        const int x = x0 + lane;
+        bool hit = false;
+        int32_t q = 0;
+        int64_t r0 = 0, r1 = 0, r2 = 0;
+        if (x < e1) {
+            q = sh.ex_q[x];
+            hit = q == j ? ok : (sh.ex_entry[x] == t && sh.ex_ok[x] != 0);
+            r0 = sh.ex_req[x][0]; r1 = sh.ex_req[x][1]; r2 = sh.ex_req[x][2];
+        }
+        if (hit && expired) expired[q] = 1;
+        uint64_t m = __ballot(hit);
+        while (m) {
+            const int l = __ffsll((unsigned long long)m) - 1;
+            m &= m - 1;
+            n.rc -= (int64_t)readlane64((uint64_t)r0, l);
+            n.rm -= (int64_t)readlane64((uint64_t)r1, l);
+            n.rg -= (int64_t)readlane64((uint64_t)r2, l);
+            n.nr -= 1;
+        }
+    }
+}
+
+template <int kMode>
 __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) {
     __shared__ ResolveShared sh;
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid >> 6;
     const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
     if (a.ctr[kCtrErr] != 0) return;
+    const bool exact = a.c.n_nodes <= kFilterBits;  // touched filter needs no hash confirmation
     int nb = (int)min<int64_t>(min<int64_t>(a.B, kMaxBatchR), end - start);
     if (nb <= 0) return;
 
@@ -427,7 +488,7 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
         }
         sh.nb = lo;
         sh.n_t = 0; sh.committed = lo; sh.err_code = 0; sh.err_pod = -1;
-        sh.best[0] = 0; sh.best[1] = 0; sh.best[2] = 0;
+        for (int b = 0; b < 3; ++b) sh.ctl[b] = Ctl{0, 0, 0, 0, {0, 0}};
     }
     for (int h = tid; h < kHash; h += kResolveThreads) sh.hkey[h] = -1;
     for (int w = tid; w < kFilterBits / 32; w += kResolveThreads) sh.tfilt[w] = 0;
@@ -439,13 +500,18 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
         sh.pod[i] = a.pods[start + i];
         sh.podf[i][0] = (float)a.pods[start + i].req[0];
         sh.podf[i][1] = (float)a.pods[start + i].req[1];
-        sh.dur[i] = a.dur[start + i];
         const int64_t pos = a.exp_pos[start + i];
-        sh.exp_slot[i] = (pos >= e_base && pos - e_base < e_cnt) ? (int32_t)(pos - e_base) : -1;
+        PodCtl pc;
+        pc.flags = a.pods[start + i].flags;
+        pc.ex_lo = i <= 1 ? 0 : (int32_t)(a.exp_off[start + i] - e_base);
+        pc.ex_hi = i + 1 <= 1 ? 0 : (int32_t)(a.exp_off[start + i + 1] - e_base);
+        pc.dur = a.dur[start + i];
+        pc.exp_slot = (pos >= e_base && pos - e_base < e_cnt) ? (int32_t)(pos - e_base) : -1;
+        pc.pad[0] = pc.pad[1] = pc.pad[2] = 0;
+        sh.pctl[i] = pc;
     }
     for (int i = tid; i < nb * kL; i += kResolveThreads) sh.cand[i / kL][i % kL] = a.cand[i];
-    for (int i = tid; i <= nb; i += kResolveThreads)
-        sh.ex_off[i] = i <= 1 ? 0 : (int32_t)(a.exp_off[start + i] - e_base);
+    if (tid == 0) sh.pctl[nb] = PodCtl{0, 0, 0, 0, -1, {0, 0, 0}};
     for (int e = tid; e < e_cnt; e += kResolveThreads) {
         const int32_t q = a.exp_pod[e_base + e];
         const PodRec& pq = a.pods[q];
@@ -505,26 +571,20 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
     PruneF own_pf{};      // prune_tmax state of the entry
     Prefetch pf{};        // wave 0
 
-    // ---- prologue: pod 0's contributions into best[0]; pod 1's prefetch
+    // ---- prologue: pod 0's contributions into ctl[0].best; pod 1's prefetch
     if (wave == 0) {
-        bool full;
-        int pa, pa2;
-        first_untouched2(sh, 0, lane, pa, pa2, full);
-        if (pa >= 0 && lane < 10) sh.stage[0][lane] = node_field(a.s, lane, key_node(sh.cand[0][pa]));
-        if (lane == 0) {
-            if (pa >= 0) fold_best(&sh.best[0], ikey(sh.cand[0][pa], kEntUntouched));
-            sh.kfull[0] = pa < 0 && full;
-            sh.ntab[0] = sh.n_t;
-        }
-        if (lane == 0) sh.lbk[0] = sh.cand[0][kL - 1];
-        if (nb > 1) prefetch_issue(a, sh, 1, lane, pf);
+        Prefetch p0;
+        prefetch_issue(a, sh, 0, lane, exact, p0);
+        prefetch_commit(sh, lane, p0, -1, 0, 0);
+        if (lane == 0) sh.ctl[0].ntab = sh.n_t;
+        if (nb > 1) prefetch_issue(a, sh, 1, lane, exact, pf);
     } else if (oslot >= 0 && r < sh.n_t) {
         own = t_node(sh, r);
         own_node = sh.tnode[r];
         own_pf = prune_prep(a.c, own);
         loaded = true;
-        const uint64_t k = make_key(eval_t<kNarrow>(a.c, sh.pod[0], own), (uint32_t)own_node);
-        if (k != 0 && k >= sh.cand[0][kL - 1]) fold_best(&sh.best[0], ikey(k, r));
+        const uint64_t k = make_key(eval_t<kMode>(a.c, sh.pod[0], own), (uint32_t)own_node);
+        if (k != 0 && k >= sh.cand[0][kL - 1]) fold_best(&sh.ctl[0].best, ikey(k, r));
     }
     __syncthreads();
 
@@ -538,12 +598,14 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
         const int cur = i & 1, nxt = cur ^ 1;
         const int b_cur = i % 3, b_nxt = (i + 1) % 3;
         // ---- every wave: pod i's winner and the stop decision (identical in all waves)
-        const uint64_t bw = sh.best[b_cur];
-        const uint32_t pflags = sh.pod[i].flags;
+        const Ctl cc = sh.ctl[b_cur];
+        const PodCtl pci = sh.pctl[i], pcn = sh.pctl[i + 1];
+        const uint64_t lbk = sh.ctl[b_nxt].lbk;
+        const uint64_t bw = cc.best;
         int stop = 0;
-        if (sh.kfull[cur]) stop = 1;                                  // list exhausted: rescan
+        if (cc.kfull) stop = 1;                                       // list exhausted: rescan
         else if (bw == 0) stop = 2;                                   // NotFound
-        else if (pflags & (kFlagBadKey | kFlagBadSpec)) stop = 3;     // InvalidArgument
+        else if (pci.flags & (kFlagBadKey | kFlagBadSpec)) stop = 3;  // InvalidArgument
         if (stop) {
             if (tid == 0) {
                 sh.committed = i;
@@ -553,10 +615,10 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
         }
         const int went = ikey_ent(bw);
         const int32_t nd = ikey_node(bw);
-        const int nt = sh.ntab[cur];
+        const int nt = cc.ntab;
         const int t = went >= 0 ? went : nt;  // an untouched winner becomes entry nt
         const bool has_next = i + 1 < nb;
-        const int e0 = has_next ? sh.ex_off[i + 1] : 0, e1 = has_next ? sh.ex_off[i + 2] : 0;
+        const int e0 = has_next ? pcn.ex_lo : 0, e1 = has_next ? pcn.ex_hi : 0;
         KS_STAMP(sw);
 #ifdef KS_STAMPS
         acc_sub[0] += sw - s0;
@@ -564,25 +626,28 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
 
         if (oslot >= 0) {
             if (has_next && oslot * kWave < nt && !(KS_ABL & 16)) {
+                // one round of independent LDS reads, then the (rare) reload
+                const int32_t dr = sh.dirty[r < kTMax ? r : 0];
+                const float qfc = sh.podf[i + 1][0], qfm = sh.podf[i + 1][1];
+                const PodRec pn = pod_regs(&sh.pod[i + 1]);
                 if (r < nt) {
                     if (!loaded) {
                         own = t_node(sh, r);
                         own_node = sh.tnode[r];
                         own_pf = prune_prep(a.c, own);
                         loaded = true;
-                    } else if (sh.dirty[r] == i) {
+                    } else if (dr == i) {
                         own.rc = sh.ts[4][r]; own.rm = sh.ts[5][r]; own.rg = sh.ts[6][r]; own.nr = sh.ts[7][r];
                         own_pf = prune_prep(a.c, own);
                     }
                 }
-                const uint64_t lbk = sh.lbk[nxt];
                 bool want = r < nt && own_pf.live && r != went;
 #ifdef KS_STAMPS
                 acc_cnt[0] += __popcll(__ballot(r < nt));
                 acc_cnt[1] += __popcll(__ballot(want));
 #endif
                 if (lbk != 0 && want) {
-                    const uint32_t tm = prune_tmax(a.c, own_pf, sh.podf[i + 1][0], sh.podf[i + 1][1]);
+                    const uint32_t tm = prune_tmax(a.c, own_pf, qfc, qfm);
                     want = make_key(tm + 1u, (uint32_t)own_node) >= lbk;
                 }
 #ifdef KS_STAMPS
@@ -595,8 +660,8 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
                         want &= !(sh.ex_entry[x] == r && sh.ex_q[x] != j);
                     KS_STAMP(sb);
                     if (want && !(KS_ABL & 1)) {
-                        const uint64_t k = make_key(eval_t<kNarrow>(a.c, sh.pod[i + 1], own), (uint32_t)own_node);
-                        if (k != 0 && k >= lbk) fold_best(&sh.best[b_nxt], ikey(k, r));
+                        const uint64_t k = make_key(eval_t<kMode>(a.c, pn, own), (uint32_t)own_node);
+                        if (k != 0 && k >= lbk) fold_best(&sh.ctl[b_nxt].best, ikey(k, r));
                     }
                     KS_STAMP(sc);
 #ifdef KS_STAMPS
@@ -609,65 +674,80 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
             }
         } else if (wave == 0) {
             if (lane == 0) {
-                if (went < 0) { sh.tnode[t] = nd; h_insert(sh, nd, t); }
-                sh.ntab[nxt] = went < 0 ? nt + 1 : nt;
-                sh.best[(i + 2) % 3] = 0;  // read in iteration i-1, folded into in iteration i+1
+                if (went < 0) { sh.tnode[t] = nd; t_insert(sh, nd, t, exact); }
+                sh.ctl[b_nxt].ntab = went < 0 ? nt + 1 : nt;
+                sh.ctl[(i + 2) % 3].best = 0;  // read in iteration i-1, folded into in iteration i+1
             }
-            if (has_next) prefetch_commit(sh, i + 1, lane, pf, went < 0 ? nd : -1, nxt, b_nxt);
-            if (i + 2 < nb) prefetch_issue(a, sh, i + 2, lane, pf);
-        } else if (wave == 1) {
-            const PodRec p = sh.pod[i];
+            KS_STAMP(t0a);
+            if (has_next) prefetch_commit(sh, lane, pf, went < 0 ? nd : -1, nxt, b_nxt);
+            KS_STAMP(t0b);
+            if (i + 2 < nb) prefetch_issue(a, sh, i + 2, lane, exact, pf);
+            KS_STAMP(t0c);
+#ifdef KS_STAMPS
+            acc_cnt[0] += t0a - sw; acc_cnt[1] += t0b - t0a; acc_cnt[2] += t0c - t0b;
+#endif
+        } else if (wave == 1 || wave == kWriterWave) {
+            // the bind of pod i on entry t: wave 1 computes pod i+1's key on the new state (the
+            // critical path), the writer wave stores the state and the outputs
+            const PodRec pnext = pod_regs(&sh.pod[i + 1]);  // i + 1 <= nb: a readable slot
+            const PodRec p = pod_regs(&sh.pod[i]);
             NodeV n = went >= 0 ? t_node(sh, t) : stage_node(sh, cur);
             const bool ok = fits(p, n);  // CreatePod admission (kubesim/node/node.go:44-47)
-            if (ok && sh.dur[i] > 0) { n.rc += p.req[0]; n.rm += p.req[1]; n.rg += p.req[2]; n.nr += 1; }
+            if (ok && pci.dur > 0) { n.rc += p.req[0]; n.rm += p.req[1]; n.rg += p.req[2]; n.nr += 1; }
             KS_STAMP(t1a);
-            for (int x = e0; x < e1; ++x) {  // pod i+1's expiries on this entry (pod i's own included)
-                const int32_t q = sh.ex_q[x];
-                const bool hit = q == j ? ok : (sh.ex_entry[x] == t && sh.ex_ok[x] != 0);
-                if (!hit) continue;
-                n.rc -= sh.ex_req[x][0]; n.rm -= sh.ex_req[x][1]; n.rg -= sh.ex_req[x][2]; n.nr -= 1;
-                if (lane == 0) a.expired[q] = 1;
-            }
+            expire_on(sh, e0, e1, t, j, ok, lane, n, wave == 1 ? nullptr : a.expired);
             KS_STAMP(t1b);
-            if (lane == 0) {
+            if (wave == 1) {
+                if (lane == 0 && has_next && !(KS_ABL & 2)) {
+                    const uint64_t k = make_key(eval_t<kMode>(a.c, pnext, n), (uint32_t)nd);
+                    if (k != 0) fold_best(&sh.ctl[b_nxt].best, ikey(k, t));
+                }
+                KS_STAMP(t1d);
+#ifdef KS_STAMPS
+                acc_sub[4] += t1a - sw; acc_sub[5] += t1b - t1a; acc_sub[7] += t1d - t1b;
+#endif
+            } else if (lane == 0) {
                 if (went < 0) {
                     sh.ts[0][t] = n.ac; sh.ts[1][t] = n.am; sh.ts[2][t] = n.ag; sh.ts[3][t] = n.ap;
                     sh.tu[0][t] = n.taint; sh.tu[1][t] = n.label;
                 }
                 sh.ts[4][t] = n.rc; sh.ts[5][t] = n.rm; sh.ts[6][t] = n.rg; sh.ts[7][t] = n.nr;
                 sh.dirty[t] = i + 1;
-                const int slot = sh.exp_slot[i];
+                const int slot = pci.exp_slot;
                 if (slot >= 0) { sh.ex_entry[slot] = t; sh.ex_ok[slot] = ok ? 1 : 0; }
                 a.b_node[j] = nd;
                 a.b_status[j] = ok ? 0 : 1;
             }
-            KS_STAMP(t1c);
-            if (lane == 0 && has_next && !(KS_ABL & 2)) {
-                const uint64_t k = make_key(eval_t<kNarrow>(a.c, sh.pod[i + 1], n), (uint32_t)nd);
-                if (k != 0) fold_best(&sh.best[b_nxt], ikey(k, t));
-            }
-            KS_STAMP(t1d);
-#ifdef KS_STAMPS
-            acc_sub[4] += t1a - sw; acc_sub[5] += t1b - t1a; acc_sub[6] += t1c - t1b; acc_sub[7] += t1d - t1c;
-#endif
         } else if (wave == 2) {
             if (has_next && e1 > e0 && !(KS_ABL & 4)) {
-                if (lane == 0) {
-                    for (int x = e0; x < e1; ++x) {
+                // pod i+1's other expiries, lane-parallel: LDS atomics apply them (several may hit
+                // one entry), then each lane evaluates its expiry's entry on the final state
+                // (LDS operations of one wave complete in order)
+                const PodRec pn = pod_regs(&sh.pod[i + 1]);
+                for (int x0 = e0; x0 < e1; x0 += kWave) {  // apply every expiry first ...
+                    const int x = x0 + lane;
+                    if (x < e1) {
+                        const int32_t q = sh.ex_q[x];
                         const int tq = sh.ex_entry[x];
-                        if (sh.ex_q[x] == j || tq < 0 || tq == t || !sh.ex_ok[x]) continue;
-                        sh.ts[4][tq] -= sh.ex_req[x][0]; sh.ts[5][tq] -= sh.ex_req[x][1];
-                        sh.ts[6][tq] -= sh.ex_req[x][2]; sh.ts[7][tq] -= 1;
-                        sh.dirty[tq] = i + 1;
-                        a.expired[sh.ex_q[x]] = 1;
+                        if (q != j && tq >= 0 && tq != t && sh.ex_ok[x]) {
+                            atomicAdd((unsigned long long*)&sh.ts[4][tq], (unsigned long long)-sh.ex_req[x][0]);
+                            atomicAdd((unsigned long long*)&sh.ts[5][tq], (unsigned long long)-sh.ex_req[x][1]);
+                            atomicAdd((unsigned long long*)&sh.ts[6][tq], (unsigned long long)-sh.ex_req[x][2]);
+                            atomicAdd((unsigned long long*)&sh.ts[7][tq], (unsigned long long)-1ll);
+                            sh.dirty[tq] = i + 1;
+                            a.expired[q] = 1;
+                        }
                     }
                 }
-                const PodRec pn = sh.pod[i + 1];
-                for (int x = e0 + lane; x < e1; x += kWave) {
-                    const int tq = sh.ex_entry[x];
-                    if (sh.ex_q[x] == j || tq < 0 || tq == t) continue;
-                    const uint64_t k = make_key(eval_t<kNarrow>(a.c, pn, t_node(sh, tq)), (uint32_t)sh.tnode[tq]);
-                    if (k != 0) fold_best(&sh.best[b_nxt], ikey(k, tq));
+                for (int x0 = e0; x0 < e1; x0 += kWave) {  // ... then evaluate their entries
+                    const int x = x0 + lane;
+                    if (x < e1) {
+                        const int tq = sh.ex_entry[x];
+                        if (sh.ex_q[x] != j && tq >= 0 && tq != t) {
+                            const uint64_t k = make_key(eval_t<kMode>(a.c, pn, t_node(sh, tq)), (uint32_t)sh.tnode[tq]);
+                            if (k != 0) fold_best(&sh.ctl[b_nxt].best, ikey(k, tq));
+                        }
+                    }
                 }
             }
         }
@@ -690,6 +770,10 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
             for (int k = 0; k < 4; ++k) atomicAdd(&d[5 + k], acc_sub[k]);       // top, load, excl, eval
         if (lane == 0 && wave == 1)
             for (int k = 0; k < 4; ++k) atomicAdd(&d[11 + k], acc_sub[4 + k]);  // fetch+fit, expiries, writes, eval
+        if (lane == 0 && wave == 3) atomicAdd(&d[3 + 0], 0ull);
+        if (tid == 0) atomicAdd(&d[4 + 0], 0ull);
+        if (lane == 0 && wave == 0)
+            for (int k = 0; k < 3; ++k) atomicAdd((unsigned long long*)a.ctr + 5 + k, acc_cnt[k]);  // w0 insert/commit/issue
         if (lane == 0 && oslot >= 0) {
             atomicAdd(&d[9], acc_cnt[2]);   // lanes passing prune_tmax
             atomicAdd(&d[10], acc_cnt[3]);  // owner waves evaluating
@@ -698,7 +782,7 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
 #endif
 
     // ---- write back the mutable fields of every touched node
-    const int n_final = sh.ntab[sh.committed & 1];
+    const int n_final = sh.ctl[sh.committed % 3].ntab;
     for (int e = tid; e < n_final; e += kResolveThreads) {
         const int64_t ndx = sh.tnode[e];
         a.s.rc[ndx] = sh.ts[4][e];
@@ -716,7 +800,7 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
 // ------------------------------------------------------------------------------------------
 // Filter mask / score of one pod against every node (api.Filter / api.Scorer shims).
 // ------------------------------------------------------------------------------------------
-template <bool kNarrow>
+template <int kMode>
 __global__ __launch_bounds__(256) void eval_pod_kernel(Cfg c, NodeSoA s, const PodRec* pod, uint32_t filters,
                                                         uint8_t* mask, int64_t* score) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -728,7 +812,7 @@ __global__ __launch_bounds__(256) void eval_pod_kernel(Cfg c, NodeSoA s, const P
     if (filters & kFilterTaint) ok &= (n.taint & ~p.tol) == 0;
     if (filters & kFilterSelector) ok &= (n.label & p.sel) == p.sel;
     mask[i] = ok ? 1 : 0;
-    const uint32_t t1 = eval_t<kNarrow>(c, p, n);
+    const uint32_t t1 = eval_t<kMode>(c, p, n);
     score[i] = t1 ? (int64_t)t1 - 1 : -1;
 }
 
@@ -797,12 +881,15 @@ int max_batch_pods() { return kMaxBatchR; }
 int max_pods_per_scan_wg() { return kMaxPG; }
 int block_nodes() { return kBlockNodes; }
 
-hipError_t launch_scan(const EngineArgs& a, bool narrow, hipStream_t st) {
+hipError_t launch_scan(const EngineArgs& a, int mode, hipStream_t st) {
     hipLaunchKernelGGL(expire_head_kernel, dim3(1), dim3(256), 0, st, a);
     if (a.blk_n > 0) {
         const dim3 g(a.blk_n, (a.B + a.PG - 1) / a.PG);
-        if (narrow) hipLaunchKernelGGL(scan_kernel<true>, g, dim3(kBlockNodes), 0, st, a);
-        else hipLaunchKernelGGL(scan_kernel<false>, g, dim3(kBlockNodes), 0, st, a);
+        switch (mode) {
+            case kEvalTiny: hipLaunchKernelGGL(scan_kernel<kEvalTiny>, g, dim3(kBlockNodes), 0, st, a); break;
+            case kEvalNarrow: hipLaunchKernelGGL(scan_kernel<kEvalNarrow>, g, dim3(kBlockNodes), 0, st, a); break;
+            default: hipLaunchKernelGGL(scan_kernel<kEvalWide>, g, dim3(kBlockNodes), 0, st, a); break;
+        }
     }
     return hipGetLastError();
 }
@@ -813,9 +900,12 @@ hipError_t launch_merge(const EngineArgs& a, const uint64_t* lists, int64_t pod_
     return hipGetLastError();
 }
 
-hipError_t launch_resolve(const EngineArgs& a, bool narrow, hipStream_t st) {
-    if (narrow) hipLaunchKernelGGL(resolve_kernel<true>, dim3(1), dim3(kResolveThreads), 0, st, a);
-    else hipLaunchKernelGGL(resolve_kernel<false>, dim3(1), dim3(kResolveThreads), 0, st, a);
+hipError_t launch_resolve(const EngineArgs& a, int mode, hipStream_t st) {
+    switch (mode) {
+        case kEvalTiny: hipLaunchKernelGGL(resolve_kernel<kEvalTiny>, dim3(1), dim3(kResolveThreads), 0, st, a); break;
+        case kEvalNarrow: hipLaunchKernelGGL(resolve_kernel<kEvalNarrow>, dim3(1), dim3(kResolveThreads), 0, st, a); break;
+        default: hipLaunchKernelGGL(resolve_kernel<kEvalWide>, dim3(1), dim3(kResolveThreads), 0, st, a); break;
+    }
     return hipGetLastError();
 }
 
@@ -825,10 +915,13 @@ hipError_t launch_rescale(const NodeSoA& s, int64_t n_pad, PodRec* pods, int64_t
 }
 
 hipError_t launch_eval_pod(const Cfg& c, const NodeSoA& s, const PodRec* pod, uint32_t filters, uint8_t* mask,
-                           int64_t* score, bool narrow, hipStream_t st) {
+                           int64_t* score, int mode, hipStream_t st) {
     const dim3 g((c.n_nodes + 255) / 256);
-    if (narrow) hipLaunchKernelGGL(eval_pod_kernel<true>, g, dim3(256), 0, st, c, s, pod, filters, mask, score);
-    else hipLaunchKernelGGL(eval_pod_kernel<false>, g, dim3(256), 0, st, c, s, pod, filters, mask, score);
+    switch (mode) {
+        case kEvalTiny: hipLaunchKernelGGL(eval_pod_kernel<kEvalTiny>, g, dim3(256), 0, st, c, s, pod, filters, mask, score); break;
+        case kEvalNarrow: hipLaunchKernelGGL(eval_pod_kernel<kEvalNarrow>, g, dim3(256), 0, st, c, s, pod, filters, mask, score); break;
+        default: hipLaunchKernelGGL(eval_pod_kernel<kEvalWide>, g, dim3(256), 0, st, c, s, pod, filters, mask, score); break;
+    }
     return hipGetLastError();
 }
 

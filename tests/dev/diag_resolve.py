@@ -25,5 +25,7 @@ for k, name in ((0, "wave0 work"), (1, "wave0 wait"), (2, "wave1 work"), (3, "wa
                 (5, "w3 top"), (6, "w3 load"), (7, "w3 excl"), (8, "w3 eval"),
                 (11, "w1 fetch+fit"), (12, "w1 expiries"), (13, "w1 writes"), (14, "w1 eval")):
     print(f"  {name:12s} {D[k]/max(pods,1):9.0f} cycles/pod")
+for k, name in ((5, "w0 insert"), (6, "w0 commit"), (7, "w0 issue")):
+    print(f"  {name:12s} {d[k]/max(pods,1):9.0f} cycles/pod")
 for k, name in ((9, "pass prune"), (10, "eval waves")):
     print(f"  {name:12s} {D[k]/max(pods,1):9.2f} per pod")

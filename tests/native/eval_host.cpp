@@ -36,7 +36,7 @@ extern "C" void ks_host_ba_batch(int64_t n, const int64_t* Ac, const int64_t* Am
 // per case: exact eval_total1 (wide and narrow) of pod req[i] on node i, and prune_tmax
 extern "C" void ks_host_prune_batch(const ks::Cfg* c, int64_t n, const int64_t* alloc /*[n][4]*/,
                                     const int64_t* run /*[n][3]*/, const int64_t* req /*[n][3]*/,
-                                    uint32_t* total1, uint32_t* total1_n, uint32_t* tmax) {
+                                    uint32_t* total1, uint32_t* total1_n, uint32_t* tmax, uint32_t* total1_t) {
     for (int64_t i = 0; i < n; i++) {
         ks::NodeV v{};
         v.ac = alloc[i * 4 + 0]; v.am = alloc[i * 4 + 1]; v.ag = alloc[i * 4 + 2]; v.ap = alloc[i * 4 + 3];
@@ -46,6 +46,7 @@ extern "C" void ks_host_prune_batch(const ks::Cfg* c, int64_t n, const int64_t* 
         p.keymask = 0xFF;
         total1[i] = ks::eval_total1(*c, p, v);
         total1_n[i] = ks::eval_total1_narrow(*c, p, v);
+        total1_t[i] = ks::eval_total1_tiny(*c, p, v);
         tmax[i] = ks::prune_tmax(*c, ks::prune_prep(*c, v), (float)p.req[0], (float)p.req[1]);
     }
 }
@@ -62,10 +63,10 @@ extern "C" double ks_host_fast_batch(const ks::Cfg* c, int64_t n, const int64_t*
         p.keymask = 0x7;
         const float ic = ks::node_rcp(v.ac), im = ks::node_rcp(v.am);
         bool need = false;
-        if (narrow) (void)ks::eval_fast<true>(*c, p, v, ic, im, need);
-        else (void)ks::eval_fast<false>(*c, p, v, ic, im, need);
+        if (narrow) (void)ks::eval_fast<ks::kEvalNarrow>(*c, p, v, ic, im, need);
+        else (void)ks::eval_fast<ks::kEvalWide>(*c, p, v, ic, im, need);
         needs += need;
-        total1_g[i] = narrow ? ks::eval_g<true>(*c, p, v, ic, im) : ks::eval_g<false>(*c, p, v, ic, im);
+        total1_g[i] = narrow ? ks::eval_g<ks::kEvalNarrow>(*c, p, v, ic, im) : ks::eval_g<ks::kEvalWide>(*c, p, v, ic, im);
     }
     return n ? (double)needs / n : 0.0;
 }

@@ -53,13 +53,22 @@ def test_c1_kat():
         np.testing.assert_array_equal(eng.usage(), np.array(kat["usage"][t - 1], dtype=np.int64))
 
 
-@pytest.mark.parametrize("wide", [0, 1])
+@pytest.mark.parametrize("wide", [0, 1, 2])
 @pytest.mark.parametrize("mode", sorted(MODES))
 @pytest.mark.parametrize("seed", [1, 2])
 def test_lockstep_small(mode, seed, wide):
-    """Both evaluator variants (narrow 32-bit / forced 64-bit) against the oracle."""
+    """Every evaluator variant against the oracle: 0 = engine's choice (tiny int32 for these
+    capacities), 1 = forced 64/128-bit, 2 = no tiny (narrow 32x32->64)."""
     tr = small_trace(seed, n_nodes=400, n_pods=300, arrival="stream")
     _lockstep(tr, mode, 400, engine_flags=wide)
+
+
+def test_narrow_capacities_use_narrow_evaluator():
+    """cpu x memory beyond the tiny range (2^26 scaled units) but within the narrow one."""
+    tr = small_trace(43, n_nodes=300, n_pods=600, taints=False, selectors=False, tolerations=False)
+    nd = tr["nodes"]
+    nd["alloc"][::2, 0] = 120_001 + 3 * np.arange(len(nd["alloc"][::2]))  # cpu unit 1m: ~2^17 x 2^11
+    _lockstep(tr, "feeds_all_lrba", 600, batch_pods=128, chunk=150)
 
 
 def test_wide_capacities_use_general_evaluator():

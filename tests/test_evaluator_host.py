@@ -40,7 +40,7 @@ def lib():
     L.ks_host_lr_n_batch.argtypes = [C.c_int64] + [p()] * 3
     L.ks_host_ba_n_batch.argtypes = [C.c_int64] + [p()] * 5
     L.ks_host_ba_batch.argtypes = [C.c_int64] + [p()] * 5
-    L.ks_host_prune_batch.argtypes = [C.POINTER(Cfg), C.c_int64] + [p()] * 6
+    L.ks_host_prune_batch.argtypes = [C.POINTER(Cfg), C.c_int64] + [p()] * 7
     L.ks_host_fast_batch.argtypes = [C.POINTER(Cfg), C.c_int64, p(), p(), p(), C.c_int, p()]
     L.ks_host_fast_batch.restype = C.c_double
     return L
@@ -145,7 +145,8 @@ def test_prune_bound_sound(lib, feeds, const, w_lr, w_ba, cap_bits):
     c = Cfg(n_nodes=n, nwb=0, filter_feeds=feeds, filters=1 if feeds else 0, has_scorers=1, w_lr=w_lr,
             w_ba=w_ba, const_total=const, tick_seconds=1)
     t1 = np.zeros(n, np.uint32); t1n = np.zeros(n, np.uint32); tm = np.zeros(n, np.uint32)
-    lib.ks_host_prune_batch(C.byref(c), n, _p(alloc), _p(run), _p(req), _p(t1), _p(t1n), _p(tm))
+    t1t = np.zeros(n, np.uint32)
+    lib.ks_host_prune_batch(C.byref(c), n, _p(alloc), _p(run), _p(req), _p(t1), _p(t1n), _p(tm), _p(t1t))
     np.testing.assert_array_equal(t1n, t1)  # narrow == wide below 2^29
     live = t1 > 0
     assert live.sum() > n // 3
@@ -176,9 +177,31 @@ def test_guarded_float_eval_exact(lib, feeds, const, w_lr, w_ba, cap_bits):
     c = Cfg(n_nodes=n, nwb=0, filter_feeds=feeds, filters=1 if feeds else 0, has_scorers=1, w_lr=w_lr,
             w_ba=w_ba, const_total=const, tick_seconds=1)
     t1 = np.zeros(n, np.uint32); t1n = np.zeros(n, np.uint32); tm = np.zeros(n, np.uint32)
-    lib.ks_host_prune_batch(C.byref(c), n, _p(alloc), _p(run), _p(req), _p(t1), _p(t1n), _p(tm))
+    t1t = np.zeros(n, np.uint32)
+    lib.ks_host_prune_batch(C.byref(c), n, _p(alloc), _p(run), _p(req), _p(t1), _p(t1n), _p(tm), _p(t1t))
     narrow = cap_bits < 29
     g = np.zeros(n, np.uint32)
     frac = lib.ks_host_fast_batch(C.byref(c), n, _p(alloc), _p(run), _p(req), 1 if narrow else 0, _p(g))
     np.testing.assert_array_equal(g, t1n if narrow else t1)
     assert frac < 0.3  # the boundary-heavy mix above; random states need the fallback far less
+
+
+@pytest.mark.parametrize("feeds,const,w_lr,w_ba", [(1, 0, 1, 1), (0, 0, 1, 1), (1, 5, 2, 0), (0, 3, 0, 3)])
+@pytest.mark.parametrize("cap_bits", [6, 11, 13])
+def test_tiny_eval_exact(lib, feeds, const, w_lr, w_ba, cap_bits):
+    """eval_total1_tiny == the wide evaluator while capacities and Ac*Am stay below 2^26,
+    including C3-like small-denominator states (exact integer LR / BA values)."""
+    rng = np.random.default_rng(1000 + cap_bits * 7 + w_lr * 3 + w_ba + const + feeds)
+    n = 80_000
+    alloc, run, req = _nodes(rng, n, cap_bits)
+    # C3-like: multiples of small units, requests up to the capacity and beyond (clamp path)
+    run[:, :2] = (run[:, :2] // 8) * 8
+    req[rng.random(n) < 0.05, 0] = 1 << 40
+    req[rng.random(n) < 0.05, 1] = (1 << 27) + 5
+    assert (np.maximum(alloc[:, 0], 0) * np.maximum(alloc[:, 1], 0) < (1 << 26)).all()
+    c = Cfg(n_nodes=n, nwb=0, filter_feeds=feeds, filters=1 if feeds else 0, has_scorers=1, w_lr=w_lr,
+            w_ba=w_ba, const_total=const, tick_seconds=1)
+    t1 = np.zeros(n, np.uint32); t1n = np.zeros(n, np.uint32); tm = np.zeros(n, np.uint32)
+    t1t = np.zeros(n, np.uint32)
+    lib.ks_host_prune_batch(C.byref(c), n, _p(alloc), _p(run), _p(req), _p(t1), _p(t1n), _p(tm), _p(t1t))
+    np.testing.assert_array_equal(t1t, t1)
