@@ -390,6 +390,22 @@ __device__ __forceinline__ PodRec pod_regs(const PodRec* src) {
     return p;
 }
 
+// two records, all six loads issued before the single pin
+__device__ __forceinline__ void pod_regs2(const PodRec* s0, const PodRec* s1, PodRec& p0, PodRec& p1) {
+    const uint4* a = reinterpret_cast<const uint4*>(s0);
+    const uint4* b = reinterpret_cast<const uint4*>(s1);
+    const uint4 a0 = a[0], a1 = a[1], a2 = a[2], b0 = b[0], b1 = b[1], b2 = b[2];
+    asm volatile("" ::"v"(a0.x), "v"(a0.y), "v"(a0.z), "v"(a0.w), "v"(a1.x), "v"(a1.y), "v"(a1.z), "v"(a1.w),
+                 "v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w), "v"(b0.x), "v"(b0.y), "v"(b0.z), "v"(b0.w),
+                 "v"(b1.x), "v"(b1.y), "v"(b1.z), "v"(b1.w), "v"(b2.x), "v"(b2.y), "v"(b2.z), "v"(b2.w));
+    __builtin_memcpy(&p0, &a0, 16);
+    __builtin_memcpy(reinterpret_cast<char*>(&p0) + 16, &a1, 16);
+    __builtin_memcpy(reinterpret_cast<char*>(&p0) + 32, &a2, 16);
+    __builtin_memcpy(&p1, &b0, 16);
+    __builtin_memcpy(reinterpret_cast<char*>(&p1) + 16, &b1, 16);
+    __builtin_memcpy(reinterpret_cast<char*>(&p1) + 32, &b2, 16);
+}
+
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
@@ -689,8 +705,8 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
         } else if (wave == 1 || wave == kWriterWave) {
             // the bind of pod i on entry t: wave 1 computes pod i+1's key on the new state (the
             // critical path), the writer wave stores the state and the outputs
-            const PodRec pnext = pod_regs(&sh.pod[i + 1]);  // i + 1 <= nb: a readable slot
-            const PodRec p = pod_regs(&sh.pod[i]);
+            PodRec p, pnext;  // pod i + 1 <= nb: a readable slot
+            pod_regs2(&sh.pod[i], &sh.pod[i + 1], p, pnext);
             NodeV n = went >= 0 ? t_node(sh, t) : stage_node(sh, cur);
             const bool ok = fits(p, n);  // CreatePod admission (kubesim/node/node.go:44-47)
             if (ok && pci.dur > 0) { n.rc += p.req[0]; n.rm += p.req[1]; n.rg += p.req[2]; n.nr += 1; }
@@ -729,10 +745,12 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
                     if (x < e1) {
                         const int32_t q = sh.ex_q[x];
                         const int tq = sh.ex_entry[x];
-                        if (q != j && tq >= 0 && tq != t && sh.ex_ok[x]) {
-                            atomicAdd((unsigned long long*)&sh.ts[4][tq], (unsigned long long)-sh.ex_req[x][0]);
-                            atomicAdd((unsigned long long*)&sh.ts[5][tq], (unsigned long long)-sh.ex_req[x][1]);
-                            atomicAdd((unsigned long long*)&sh.ts[6][tq], (unsigned long long)-sh.ex_req[x][2]);
+                        const int okx = sh.ex_ok[x];
+                        const int64_t r0 = sh.ex_req[x][0], r1 = sh.ex_req[x][1], r2 = sh.ex_req[x][2];
+                        if (q != j && tq >= 0 && tq != t && okx) {
+                            atomicAdd((unsigned long long*)&sh.ts[4][tq], (unsigned long long)-r0);
+                            atomicAdd((unsigned long long*)&sh.ts[5][tq], (unsigned long long)-r1);
+                            atomicAdd((unsigned long long*)&sh.ts[6][tq], (unsigned long long)-r2);
                             atomicAdd((unsigned long long*)&sh.ts[7][tq], (unsigned long long)-1ll);
                             sh.dirty[tq] = i + 1;
                             a.expired[q] = 1;
