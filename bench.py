@@ -157,6 +157,7 @@ def main():
         pods_per_launch = st["pods"] / launches
         scan_avg_ms = st["scan_ms"] / launches
         res_avg_ms = st["resolve_ms"] / launches
+        other_avg_ms = st["other_ms"] / launches
         # algorithmic bytes of one scan launch: 80 B per (pod, node) eval
         scan_alg_bytes = BYTES_PER_EVAL * pods_per_launch * nodes
         achieved = scan_alg_bytes / (scan_avg_ms * 1e-3) / 1e9 if scan_avg_ms > 0 else None
@@ -191,6 +192,7 @@ def main():
                                  "the measured HBM bytes per launch"},
             "kernels": {"launches_per_step": launches, "pods_per_launch": pods_per_launch,
                         "scan_avg_ms": scan_avg_ms, "resolve_avg_ms": res_avg_ms,
+                        "other_avg_ms": other_avg_ms,
                         "profiled_step_ms": st["step_ms"]},
             "cpu_baseline": cpu,
             "host": {"cpu": platform.processor() or platform.machine(), "nproc": os.cpu_count()},

@@ -148,14 +148,17 @@ int64_t ks_current_tick(const ks_engine* eng);
 int64_t ks_queued_pods(const ks_engine* eng);
 const char* ks_last_error(const ks_engine* eng);
 
-/* Timing of the last ks_step on the engine's stream (HIP events): total device ms and the
- * summed scan / resolve kernel ms, number of scan+resolve launches. */
+/* Timing of the last ks_step on the engine's stream (HIP events, recorded only while
+ * ks_set_profiling is on): total device ms; the summed ms of the scan kernel alone, of the
+ * resolve kernel alone and of everything else (expire_head, merge, RCCL exchange); the number of
+ * batches (one launch of each kernel per batch) and of pods bound. */
 typedef struct {
     double step_ms;
     double scan_ms;
     double resolve_ms;
     int64_t launches;
     int64_t pods;
+    double other_ms;
 } ks_step_stats;
 ks_status ks_last_step_stats(const ks_engine* eng, ks_step_stats* out);
 /* Device counters (diagnostics): [0] next pod, [1] step end, [2] error, [3] error pod,

@@ -471,7 +471,9 @@ struct EngineArgs {
 int max_batch_pods();
 int max_pods_per_scan_wg();
 int block_nodes();
-// expire_head + scan of blocks [blk_lo, blk_lo + blk_n)
+// expiries due before the batch's first pod
+hipError_t launch_expire_head(const EngineArgs& a, hipStream_t st);
+// scan of blocks [blk_lo, blk_lo + blk_n)
 hipError_t launch_scan(const EngineArgs& a, int mode, hipStream_t st);
 // per pod b < batch size: exact top-L over nl sorted lists lists[b*pod_stride + k*list_stride]
 hipError_t launch_merge(const EngineArgs& a, const uint64_t* lists, int64_t pod_stride, int32_t nl,

@@ -48,6 +48,7 @@ constexpr int64_t kMaxNodes = 1LL << 24;  // node ids fit the packed key; lists 
 constexpr int64_t kMaxValue = 1LL << 59;
 constexpr int kMaxBatch = 256;
 constexpr int kDefaultBatch = 256;
+constexpr int kProfEv = 5;  // per launch: expire_head | scan | merge (+exchange) | resolve
 constexpr int64_t kNever = std::numeric_limits<int64_t>::max();
 
 // Growable device array (stream-ordered copies on growth).
@@ -542,19 +543,22 @@ ks_status ks_step(ks_engine* e, int64_t ticks, ks_bind* out, int64_t cap, int64_
     while (true) {
         const int64_t nbat = (p_hi - start + e->B - 1) / e->B;
         for (int64_t b = 0; b < nbat; b++) {
-            hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
+            // profiling: events around the scan kernel alone and the resolve kernel alone (on
+            // the engine's stream), so their averages agree with rocprofv3's kernel trace
+            hipEvent_t ev[kProfEv] = {};
             if (e->profiling) {
-                while ((int64_t)e->prof_ev.size() < 3 * (launches + 1)) {
-                    hipEvent_t ev;
-                    HIPCHK(e, hipEventCreate(&ev));
-                    e->prof_ev.push_back(ev);
+                while ((int64_t)e->prof_ev.size() < kProfEv * (launches + 1)) {
+                    hipEvent_t x;
+                    HIPCHK(e, hipEventCreate(&x));
+                    e->prof_ev.push_back(x);
                 }
-                e0 = e->prof_ev[3 * launches];
-                e1 = e->prof_ev[3 * launches + 1];
-                e2 = e->prof_ev[3 * launches + 2];
+                for (int k = 0; k < kProfEv; k++) ev[k] = e->prof_ev[kProfEv * launches + k];
             }
-            if (e0) HIPCHK(e, hipEventRecord(e0, st));
+            if (ev[0]) HIPCHK(e, hipEventRecord(ev[0], st));
+            HIPCHK(e, ks::launch_expire_head(a, st));
+            if (ev[1]) HIPCHK(e, hipEventRecord(ev[1], st));
             HIPCHK(e, ks::launch_scan(a, e->mode, st));
+            if (ev[2]) HIPCHK(e, hipEventRecord(ev[2], st));
             const int G = e->world * e->vsh;
             const int64_t L = ks::kTopL, BL = (int64_t)e->B * L;
             if (G == 1) {
@@ -572,9 +576,9 @@ ks_status ks_step(ks_engine* e, int64_t ticks, ks_bind* out, int64_t cap, int64_
                 }
                 HIPCHK(e, ks::launch_merge(a, e->cand_all, L, G, BL, e->cand, st));
             }
-            if (e1) HIPCHK(e, hipEventRecord(e1, st));
+            if (ev[3]) HIPCHK(e, hipEventRecord(ev[3], st));
             HIPCHK(e, ks::launch_resolve(a, e->mode, st));
-            if (e2) HIPCHK(e, hipEventRecord(e2, st));
+            if (ev[4]) HIPCHK(e, hipEventRecord(ev[4], st));
             launches++;
         }
         HIPCHK(e, hipMemcpyAsync(e->h_ctr, e->d_ctr, 5 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
@@ -593,18 +597,21 @@ ks_status ks_step(ks_engine* e, int64_t ticks, ks_bind* out, int64_t cap, int64_
     HIPCHK(e, hipStreamSynchronize(st));
     float ms = 0;
     (void)hipEventElapsedTime(&ms, e->ev[0], e->ev[1]);
+    double other_ms = 0;
     if (e->profiling) {
         for (int64_t l = 0; l < launches; l++) {
-            float a1 = 0, a2 = 0;
-            (void)hipEventElapsedTime(&a1, e->prof_ev[3 * l], e->prof_ev[3 * l + 1]);
-            (void)hipEventElapsedTime(&a2, e->prof_ev[3 * l + 1], e->prof_ev[3 * l + 2]);
-            scan_ms += a1;
-            res_ms += a2;
+            float t[kProfEv - 1] = {};
+            for (int k = 0; k + 1 < kProfEv; k++)
+                (void)hipEventElapsedTime(&t[k], e->prof_ev[kProfEv * l + k], e->prof_ev[kProfEv * l + k + 1]);
+            other_ms += t[0] + t[2];
+            scan_ms += t[1];
+            res_ms += t[3];
         }
     }
     e->stats.step_ms = ms;
     e->stats.scan_ms = scan_ms;
     e->stats.resolve_ms = res_ms;
+    e->stats.other_ms = other_ms;
     e->stats.launches = launches;
     e->stats.pods = nb;
     for (int64_t i = 0; i < nb && i < cap; i++) {

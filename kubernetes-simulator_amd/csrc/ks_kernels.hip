@@ -271,7 +271,7 @@ struct ResolveShared {
     int64_t ex_req[kMaxExp][3];
     Ctl ctl[3];                 // pod i's decision state, slot i % 3
     int64_t stage[2][10];       // snapshot fields of the pod's best untouched list node
-    int32_t n_t, committed, err_code, err_pod, nb;
+    int32_t n_t, committed, err_code, err_pod, nb, e_cnt;
 };
 
 constexpr int kEntUntouched = 1023;
@@ -492,25 +492,26 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
     const bool exact = a.c.n_nodes <= kFilterBits;  // touched filter needs no hash confirmation
     int nb = (int)min<int64_t>(min<int64_t>(a.B, kMaxBatchR), end - start);
     if (nb <= 0) return;
+    KS_STAMP(g0);
 
     // window: expiries of pods start+1 .. start+nb-1 (pod start's were applied by expire_head);
     // shrink the batch so that they fit the pre-insert budget
+    // largest nb' <= nb whose window fits: exp_off is non-decreasing, so the count of fitting
+    // prefixes is nb' (one HBM round trip for all candidates instead of a serial bisection)
     const int64_t e_base = a.exp_off[start + 1];
+    const int64_t off_mid = tid < nb ? a.exp_off[start + tid + 1] : 0;
+    const bool fits_win = tid < nb && off_mid - e_base <= kMaxExp;
     if (tid == 0) {
-        int lo = 1, hi = nb;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) / 2;
-            if (a.exp_off[start + mid] - e_base <= kMaxExp) lo = mid; else hi = mid - 1;
-        }
-        sh.nb = lo;
-        sh.n_t = 0; sh.committed = lo; sh.err_code = 0; sh.err_pod = -1;
+        sh.n_t = 0; sh.err_code = 0; sh.err_pod = -1;
         for (int b = 0; b < 3; ++b) sh.ctl[b] = Ctl{0, 0, 0, 0, {0, 0}};
     }
     for (int h = tid; h < kHash; h += kResolveThreads) sh.hkey[h] = -1;
     for (int w = tid; w < kFilterBits / 32; w += kResolveThreads) sh.tfilt[w] = 0;
+    nb = __syncthreads_count(fits_win);
+    if (tid == nb - 1) { sh.nb = nb; sh.committed = nb; sh.e_cnt = nb > 1 ? (int32_t)(off_mid - e_base) : 0; }
     __syncthreads();
-    nb = sh.nb;
-    const int64_t e_cnt = nb > 1 ? a.exp_off[start + nb] - e_base : 0;
+    const int64_t e_cnt = sh.e_cnt;
+    KS_STAMP(g1);
 
     for (int i = tid; i < nb; i += kResolveThreads) {
         sh.pod[i] = a.pods[start + i];
@@ -543,32 +544,38 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
         }
     }
     __syncthreads();
+    KS_STAMP(g2);
     // pre-insert every node an expiry of this batch lands on (q bound before the batch): the
-    // per-pod expiry step then never waits on HBM
-    if (wave == 0) {
-        for (int e0 = 0; e0 < e_cnt; e0 += kWave) {
-            const int e = e0 + lane;
-            const bool want = e < e_cnt && sh.ex_ok[e];
-            const int32_t mine = want ? sh.ex_node[e] : 0;
-            uint64_t m = __ballot(want);
-            while (m) {
-                const int l = __ffsll((unsigned long long)m) - 1;
-                m &= m - 1;
-                const int32_t nd = __shfl(mine, l, kWave);
-                if (lane == 0) {
-                    int idx = h_find(sh, nd);
-                    if (idx < 0) {
-                        idx = sh.n_t;
-                        sh.tnode[idx] = nd;
-                        h_insert(sh, nd, idx);
-                        sh.n_t = idx + 1;
-                    }
-                    sh.ex_entry[e0 + l] = idx;
-                }
-            }
+    // per-pod expiry step then never waits on HBM.  One thread per expiry (e_cnt <= kMaxExp <
+    // kResolveThreads): claim the node's hash slot with a CAS (duplicates find it), number the
+    // claimed slots, then read the entry back.  Entry numbering order is immaterial: an entry
+    // index only names a node, it never takes part in a comparison between distinct nodes.
+    static_assert(kMaxExp <= kResolveThreads, "one thread per pre-inserted expiry");
+    const bool pre_want = tid < e_cnt && sh.ex_ok[tid];
+    int pre_slot = -1;
+    bool pre_claim = false;
+    if (pre_want) {
+        const int32_t nd = sh.ex_node[tid];
+        uint32_t hs = hslot(nd);
+        for (;;) {  // the table holds <= kMaxExp < kHash nodes: terminates
+            const int32_t prev = atomicCAS(&sh.hkey[hs], -1, nd);
+            if (prev == -1 || prev == nd) { pre_slot = (int)hs; pre_claim = prev == -1; break; }
+            hs = (hs + 1) & (kHash - 1);
         }
     }
     __syncthreads();
+    if (pre_claim) {
+        const int32_t nd = sh.ex_node[tid];
+        const int idx = atomicAdd(&sh.n_t, 1);
+        sh.hval[pre_slot] = idx;
+        sh.tnode[idx] = nd;
+        const uint32_t f = (uint32_t)nd & (kFilterBits - 1);
+        atomicOr(&sh.tfilt[f >> 5], 1u << (f & 31));
+    }
+    __syncthreads();
+    if (pre_want) sh.ex_entry[tid] = sh.hval[pre_slot];
+    __syncthreads();
+    KS_STAMP(g3);
     for (int e = tid; e < kTMax; e += kResolveThreads) sh.dirty[e] = -1;
     for (int e = tid; e < sh.n_t; e += kResolveThreads) {
         const NodeV v = load_node(a.s, sh.tnode[e]);
@@ -577,6 +584,7 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
         sh.tu[0][e] = v.taint; sh.tu[1][e] = v.label;
     }
     __syncthreads();
+    KS_STAMP(g4);
 
     // owner registers (waves 3..15): entry r = tid - 192
     const int oslot = owner_slot(wave);
@@ -603,6 +611,7 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
         if (k != 0 && k >= sh.cand[0][kL - 1]) fold_best(&sh.ctl[0].best, ikey(k, r));
     }
     __syncthreads();
+    KS_STAMP(g5);
 
 #ifdef KS_STAMPS
     uint64_t acc_work = 0, acc_wait = 0, acc_sub[8] = {0, 0, 0, 0, 0, 0, 0, 0}, acc_cnt[4] = {0, 0, 0, 0};
@@ -800,6 +809,7 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
 #endif
 
     // ---- write back the mutable fields of every touched node
+    KS_STAMP(g6);
     const int n_final = sh.ctl[sh.committed % 3].ntab;
     for (int e = tid; e < n_final; e += kResolveThreads) {
         const int64_t ndx = sh.tnode[e];
@@ -813,6 +823,21 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
         if (sh.committed < a.B && sh.err_code == 0 && start + sh.committed < end) a.ctr[kCtrEarly] += 1;
         if (sh.err_code) { a.ctr[kCtrErr] = sh.err_code; a.ctr[kCtrErrPod] = sh.err_pod; }
     }
+#ifdef KS_STAMPS
+    __syncthreads();
+    KS_STAMP(g7);
+    if (tid == 0) {  // setup / writeback phases, ctr[8..14]
+        unsigned long long* d = (unsigned long long*)a.ctr;
+        atomicAdd(&d[8], g1 - g0);   // init + expiry-window search
+        atomicAdd(&d[9], g2 - g1);   // pod / list / expiry loads
+        atomicAdd(&d[10], g3 - g2);  // expiry-node pre-insert
+        atomicAdd(&d[11], g4 - g3);  // table record loads
+        atomicAdd(&d[12], g5 - g4);  // prologue (pod 0)
+        atomicAdd(&d[13], g7 - g6);  // writeback
+        atomicAdd(&d[14], 1ull);     // launches
+        atomicAdd(&d[15], (unsigned long long)e_cnt);  // expiries in windows
+    }
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -899,8 +924,12 @@ int max_batch_pods() { return kMaxBatchR; }
 int max_pods_per_scan_wg() { return kMaxPG; }
 int block_nodes() { return kBlockNodes; }
 
-hipError_t launch_scan(const EngineArgs& a, int mode, hipStream_t st) {
+hipError_t launch_expire_head(const EngineArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(expire_head_kernel, dim3(1), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan(const EngineArgs& a, int mode, hipStream_t st) {
     if (a.blk_n > 0) {
         const dim3 g(a.blk_n, (a.B + a.PG - 1) / a.PG);
         switch (mode) {

@@ -48,7 +48,7 @@ class KsBind(C.Structure):
 
 class KsStepStats(C.Structure):
     _fields_ = [("step_ms", C.c_double), ("scan_ms", C.c_double), ("resolve_ms", C.c_double),
-                ("launches", C.c_int64), ("pods", C.c_int64)]
+                ("launches", C.c_int64), ("pods", C.c_int64), ("other_ms", C.c_double)]
 
 
 _lib = None

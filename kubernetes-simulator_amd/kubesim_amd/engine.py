@@ -153,7 +153,7 @@ class Engine:
         s = KsStepStats()
         self._L.ks_last_step_stats(self.h, C.byref(s))
         return dict(step_ms=s.step_ms, scan_ms=s.scan_ms, resolve_ms=s.resolve_ms, launches=s.launches,
-                    pods=s.pods)
+                    pods=s.pods, other_ms=s.other_ms)
 
     def debug_counters(self):
         out = np.zeros(32, np.int64)

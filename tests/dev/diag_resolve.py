@@ -15,7 +15,9 @@ eng.load_nodes(enc["alloc"], enc["taint"], enc["label"])
 eng.submit(enc["pods"])
 eng.step(65536)
 c0 = eng.debug_counters().copy()
+eng.set_profiling(True)
 t = time.perf_counter(); eng.step(32768); dt = time.perf_counter() - t
+st = eng.last_step_stats()
 c1 = eng.debug_counters()
 d = c1 - c0
 D = d[16:]
@@ -29,3 +31,11 @@ for k, name in ((5, "w0 insert"), (6, "w0 commit"), (7, "w0 issue")):
     print(f"  {name:12s} {d[k]/max(pods,1):9.0f} cycles/pod")
 for k, name in ((9, "pass prune"), (10, "eval waves")):
     print(f"  {name:12s} {D[k]/max(pods,1):9.2f} per pod")
+L = max(d[14], 1)
+print(f"  launches {d[14]}  pods/launch {pods / L:.1f}  expiries/launch {d[15] / L:.1f}")
+for k, name in ((8, "init+search"), (9, "loads"), (10, "pre-insert"), (11, "table loads"), (12, "prologue"), (13, "writeback")):
+    print(f"  {name:12s} {d[k] / L:9.0f} cycles/launch")
+print(f"  resolve {st['resolve_ms'] / L * 1e3:.1f} us/launch, scan {st['scan_ms'] / L * 1e3:.1f}, other {st['other_ms'] / L * 1e3:.1f}")
+loop = (D[0] + D[1]) / L
+setup = sum(d[k] for k in (8, 9, 10, 11, 12, 13)) / L
+print(f"  stamp clock ~ {(loop + setup) / (st['resolve_ms'] / L * 1e3) / 1e3:.2f} GHz (loop+setup cycles / resolve time)")
