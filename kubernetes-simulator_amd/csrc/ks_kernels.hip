@@ -34,7 +34,13 @@ constexpr int kL = kTopL;                // candidate list length per pod
 constexpr int kMaxPG = 32;               // pods per scan workgroup (LDS list staging)
 constexpr int kResolveThreads = 1024;    // 16 waves
 constexpr int kOwnerWave0 = 3;           // waves 3..15 own the touched entries, except
-constexpr int kWriterWave = 5;           // the bind's bookkeeping writer (off the critical path)
+#ifndef KS_WRITER_WAVE
+#define KS_WRITER_WAVE 5
+#endif
+#ifndef KS_PRIO
+#define KS_PRIO 0
+#endif
+constexpr int kWriterWave = KS_WRITER_WAVE;  // the bind's bookkeeping writer (off the critical path)
 constexpr int kOwnerWaves = kResolveThreads / kWave - kOwnerWave0 - 1;
 constexpr int kOwners = kOwnerWaves * kWave;
 constexpr int kTMax = 768;               // touched-node table (LDS); <= kOwners
@@ -615,6 +621,12 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) 
 
 #ifdef KS_STAMPS
     uint64_t acc_work = 0, acc_wait = 0, acc_sub[8] = {0, 0, 0, 0, 0, 0, 0, 0}, acc_cnt[4] = {0, 0, 0, 0};
+#endif
+#if KS_PRIO
+    // static issue priority for the waves on the per-pod critical path (the bind wave first,
+    // then the list walker and the expiry wave) over the owner waves sharing their SIMDs
+    if (wave == 1) __builtin_amdgcn_s_setprio(2);
+    else if (wave == 0 || wave == 2) __builtin_amdgcn_s_setprio(1);
 #endif
     int i = 0;
     for (; i < nb; ++i) {
