@@ -82,7 +82,15 @@ def main():
     ap.add_argument("--cpu-sample-pods", type=int, default=4000)
     ap.add_argument("--cpu-budget-s", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--config", choices=("c3", "c4"), default="c3",
+                    help="c3 (default): the metric's 50k-node workload; c4: BASELINE configs[3], "
+                         "independent what-if scenarios batched in one launch per kernel")
+    ap.add_argument("--scenarios", type=int, default=1024, help="c4: scenarios (split across ranks)")
+    ap.add_argument("--scenario-nodes", type=int, default=2000)
+    ap.add_argument("--scenario-pods", type=int, default=10_000)
     args = ap.parse_args()
+    if args.config == "c4":
+        return main_c4(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -199,6 +207,89 @@ def main():
         }
         print(json.dumps(line), flush=True)
     eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def main_c4(args):
+    """BASELINE.json configs[3]: `scenarios` independent clusters (2k nodes, 10k-pod traces each,
+    seed 0x5EED0004 ^ s) stepped together through ks_group_step; ranks take disjoint scenario
+    ranges (weak scaling, no collective).  A step = `pods-per-step` ticks of every scenario."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    from kubesim_amd import encode, tracegen
+    from kubesim_amd.engine import Group
+    per = args.scenarios // world
+    lo = rank * per
+    S_pps = min(args.pods_per_step, args.scenario_pods // max(args.steps + args.warmup, 1))
+    t0 = time.perf_counter()
+    g = Group(per, device=local)
+    scorers = ((1, 1, 0), (2, 1, 0))
+    for s in range(lo, lo + per):
+        tr = tracegen.c4_scenario(s, n_nodes=args.scenario_nodes, n_pods=args.scenario_pods)
+        enc = encode.encode_trace(tr)
+        e = g.add(tick_seconds=tr["tick_seconds"], filter_mode=1, filters=7, scorers=scorers)
+        e.load_nodes(enc["alloc"], enc["taint"], enc["label"])
+        e.submit(enc["pods"])
+    log(f"[rank {rank}] {per} scenarios ready in {time.perf_counter() - t0:.1f}s; {S_pps} ticks per step")
+    for _ in range(args.warmup):
+        g.step(S_pps)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        try:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.synchronize(local)
+        except ImportError:
+            pass
+
+    barrier()
+    t_start = time.perf_counter()
+    binds, dev_ms, launches, aborted = 0, 0.0, 0, 0
+    for _ in range(args.steps):
+        res, st, stats = g.step(S_pps)
+        binds += sum(len(b) for b in res)
+        dev_ms += stats["step_ms"]
+        launches += stats["launches"]
+        aborted += sum(1 for x in st if x != 0)
+    t_el = time.perf_counter() - t_start
+    barrier()
+    total = binds
+    if dist is not None:
+        import torch
+        t = torch.tensor([t_el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_el = float(t.item())
+        c = torch.tensor([binds], dtype=torch.float64)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        total = int(c.item())
+    if rank == 0:
+        evals = total * args.scenario_nodes
+        line = {
+            "metric": "pod-node Filter+Score evals/sec and pods bound/sec (C4 what-if scenarios)",
+            "value": evals / t_el, "unit": "evals/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": t_el * 1e3 / args.steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+            "data": "synthetic (tracegen C4, seed 0x5EED0004 ^ scenario)",
+            "config": {"workload": "C4: independent what-if scenarios, Filter(fit+taint+selector) -> "
+                                   "Score(LR+BA) -> argmax -> bind per scenario, one launch per kernel",
+                       "scenarios": per * world, "nodes_per_scenario": args.scenario_nodes,
+                       "pods_per_scenario": args.scenario_pods, "ticks_per_step": S_pps,
+                       "parallelism": f"scenarios/{world}"},
+            "pods_per_s": total / t_el,
+            "kernels": {"batch_rounds_per_step": launches / args.steps,
+                        "device_ms_per_step": dev_ms / args.steps},
+            "aborted_scenarios": aborted,
+        }
+        print(json.dumps(line), flush=True)
+    g.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -104,6 +104,22 @@ typedef struct ks_engine ks_engine;
 ks_status ks_create(const ks_config* cfg, ks_engine** out);
 void ks_destroy(ks_engine* eng);
 
+/* Scenario groups (BASELINE.json configs[3]: independent what-if clusters × pod traces).  A
+ * group owns a stream and up to max_scenarios engines created with ks_group_add (same device and
+ * batch size; ks_load_nodes / ks_submit_pods / ks_usage / ks_filter / ks_score / ks_step work on
+ * them as on any engine).  ks_group_step advances every member by `ticks` ticks with one launch
+ * per kernel for all of them (scenario = a grid dimension, one resolve workgroup each) — the
+ * reference would run one KubeSim.Run per scenario (kubesim/kubesim.go:90-123).  Per member i:
+ * binds into out[i * cap ...] (out may be NULL), their count in n_out[i] and the member's status
+ * in status_out[i] (an aborting error stops only that scenario).  Members are destroyed with the
+ * group (ks_destroy on a member is a no-op).  stats (may be NULL): device ms of the whole step,
+ * batch rounds, pods bound. */
+typedef struct ks_group ks_group;
+ks_status ks_group_create(int32_t device, int32_t max_scenarios, ks_group** out);
+void ks_group_destroy(ks_group* g);
+ks_status ks_group_add(ks_group* g, const ks_config* cfg, ks_engine** out);
+int32_t ks_group_size(const ks_group* g);
+
 /* Node sharding across ranks (the reference's argmax over all nodes,
  * kubesim/kubesim.go:208-222, becomes an exact merge of per-shard candidate lists).  One
  * process per GPU; every rank loads the whole cluster and submits the same pods, scans only its
@@ -161,6 +177,8 @@ typedef struct {
     double other_ms;
 } ks_step_stats;
 ks_status ks_last_step_stats(const ks_engine* eng, ks_step_stats* out);
+ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, int64_t* n_out,
+                        int32_t* status_out, ks_step_stats* stats);
 /* Device counters (diagnostics): [0] next pod, [1] step end, [2] error, [3] error pod,
  * [4] batches that committed early (top-L list exhausted), [16..31] resolver phase cycle
  * sums in a -DKS_STAMPS diagnostic build (tests/dev/diag_resolve.py). */

@@ -467,18 +467,28 @@ struct EngineArgs {
     int32_t blk_n;
 };
 
-// Launchers and limits (defined in ks_kernels.hip).
+// Launchers and limits (defined in ks_kernels.hip).  The batch launchers take a device array of
+// S engines' arguments (S = 1 for ks_step, the group's scenarios for ks_group_step).
 int max_batch_pods();
 int max_pods_per_scan_wg();
 int block_nodes();
-// expiries due before the batch's first pod
-hipError_t launch_expire_head(const EngineArgs& a, hipStream_t st);
-// scan of blocks [blk_lo, blk_lo + blk_n)
-hipError_t launch_scan(const EngineArgs& a, int mode, hipStream_t st);
-// per pod b < batch size: exact top-L over nl sorted lists lists[b*pod_stride + k*list_stride]
-hipError_t launch_merge(const EngineArgs& a, const uint64_t* lists, int64_t pod_stride, int32_t nl,
+// expiries due before each scenario's batch head
+hipError_t launch_expire_head(const EngineArgs* d, int S, hipStream_t st);
+// scan of each scenario's blocks [blk_lo, blk_lo + blk_n); grid x = the largest blk_n
+hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int mode, hipStream_t st);
+// per scenario and pod b < batch size: exact top-L over nl sorted lists
+// lists[b*pod_stride + k*list_stride] into out (lists == nullptr: the scenario's own block lists
+// into its candidate lists)
+hipError_t launch_merge(const EngineArgs* d, int S, int B, const uint64_t* lists, int64_t pod_stride, int32_t nl,
                         int64_t list_stride, uint64_t* out, hipStream_t st);
-hipError_t launch_resolve(const EngineArgs& a, int mode, hipStream_t st);
+hipError_t launch_resolve(const EngineArgs* d, int S, int mode, hipStream_t st);
+struct BindSeg {
+    const int32_t* node;
+    const int32_t* status;
+    int64_t lo, n, off;  // copy [lo, lo + n) to [off, off + n)
+};
+hipError_t launch_gather_binds(const BindSeg* segs, int S, int64_t max_n, int32_t* node, int32_t* status,
+                               hipStream_t st);
 hipError_t launch_rescale(const NodeSoA& s, int64_t n_pad, PodRec* pods, int64_t P, const int64_t f[3], hipStream_t st);
 hipError_t launch_eval_pod(const Cfg& c, const NodeSoA& s, const PodRec* pod, uint32_t filters, uint8_t* mask,
                            int64_t* score, int mode, hipStream_t st);

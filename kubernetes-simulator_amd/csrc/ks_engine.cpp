@@ -141,6 +141,10 @@ struct ks_engine {
     uint64_t* cand_all = nullptr;  // [world * vsh][B][L]
     int64_t* d_ctr = nullptr;
     int64_t* h_ctr = nullptr;  // pinned
+    ks::EngineArgs* d_args = nullptr;  // the kernels' argument record (device)
+    ks::EngineArgs* h_args = nullptr;  // its pinned host staging
+    // group membership (ks_group_add): stream, counters and argument slots belong to the group
+    ks_group* group = nullptr;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     std::vector<hipEvent_t> prof_ev;
     ks_step_stats stats{};
@@ -152,6 +156,8 @@ struct ks_engine {
 };
 
 namespace {
+
+void engine_free(ks_engine* e);  // ks_destroy's body; a group frees its members with it
 
 ks_status fail(ks_engine* e, ks_status code, const char* fmt, ...) {
     char buf[512];
@@ -207,7 +213,12 @@ void update_mode(ks_engine* e) {
 
 extern "C" {
 
-ks_status ks_create(const ks_config* cfg, ks_engine** out) {
+}  // extern "C"
+
+namespace {
+
+// Validation and host-side construction shared by ks_create and ks_group_add (no HIP calls).
+ks_status engine_init(const ks_config* cfg, ks_engine** out) {
     if (!cfg || !out) return KS_EINVAL;
     *out = nullptr;
     if (cfg->abi_version != KS_ABI_VERSION) return KS_EINVAL;
@@ -246,22 +257,40 @@ ks_status ks_create(const ks_config* cfg, ks_engine** out) {
     e->dc.w_ba = (int32_t)w_ba;
     e->dc.const_total = (int32_t)const_total;
     e->dc.tick_seconds = cfg->tick_seconds;
+    *out = e;
+    return KS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+ks_status ks_create(const ks_config* cfg, ks_engine** out) {
+    ks_engine* e = nullptr;
+    const ks_status v = engine_init(cfg, &e);
+    if (v != KS_OK) return v;
     hipError_t r = hipSetDevice(e->device);
     if (r == hipSuccess) r = hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking);
     if (r == hipSuccess) r = hipMalloc(&e->d_ctr, 32 * sizeof(int64_t));
     if (r == hipSuccess) r = hipHostMalloc(&e->h_ctr, 32 * sizeof(int64_t), hipHostMallocDefault);
+    if (r == hipSuccess) r = hipMalloc(&e->d_args, sizeof(ks::EngineArgs));
+    if (r == hipSuccess) r = hipHostMalloc(&e->h_args, sizeof(ks::EngineArgs), hipHostMallocDefault);
     for (int i = 0; i < 4 && r == hipSuccess; i++) r = hipEventCreate(&e->ev[i]);
     if (r == hipSuccess) r = hipMemsetAsync(e->d_ctr, 0, 32 * sizeof(int64_t), e->st);
     if (r == hipSuccess) r = hipStreamSynchronize(e->st);
     if (r != hipSuccess) {
-        delete e;
+        engine_free(e);
         return KS_EDEVICE;
     }
     *out = e;
     return KS_OK;
 }
 
-void ks_destroy(ks_engine* e) {
+}  // extern "C"
+
+namespace {
+
+void engine_free(ks_engine* e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
     if (e->st) (void)hipStreamSynchronize(e->st);
@@ -273,15 +302,28 @@ void ks_destroy(ks_engine* e) {
     if (e->cand) (void)hipFree(e->cand);
     if (e->cand_all) (void)hipFree(e->cand_all);
     if (e->comm) (void)ncclCommDestroy(e->comm);
-    if (e->d_ctr) (void)hipFree(e->d_ctr);
-    if (e->h_ctr) (void)hipHostFree(e->h_ctr);
+    if (!e->group) {
+        if (e->d_ctr) (void)hipFree(e->d_ctr);
+        if (e->h_ctr) (void)hipHostFree(e->h_ctr);
+        if (e->d_args) (void)hipFree(e->d_args);
+        if (e->h_args) (void)hipHostFree(e->h_args);
+    }
     if (e->d_mask) (void)hipFree(e->d_mask);
     if (e->d_score) (void)hipFree(e->d_score);
     if (e->d_usage) (void)hipFree(e->d_usage);
     for (auto ev : e->ev) if (ev) (void)hipEventDestroy(ev);
     for (auto ev : e->prof_ev) (void)hipEventDestroy(ev);
-    if (e->st) (void)hipStreamDestroy(e->st);
+    if (e->st && !e->group) (void)hipStreamDestroy(e->st);
     delete e;
+}
+
+}  // namespace
+
+extern "C" {
+
+// a group's members are destroyed with their group (ks_group_destroy)
+void ks_destroy(ks_engine* e) {
+    if (e && !e->group) engine_free(e);
 }
 
 ks_status ks_comm_unique_id(uint8_t* id_out) {
@@ -513,6 +555,63 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
     return KS_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// ks_step, first half: the pods whose bind tick falls in (tick, tick + ticks] and the device
+// counters for them.  Returns false when there is nothing to schedule (the tick just advances).
+bool step_prepare(ks_engine* e, int64_t ticks, int64_t* p_hi_out) {
+    const int64_t t_end = e->tick + ticks;
+    const int64_t p_hi = std::upper_bound(e->h_bind_tick.begin() + e->done, e->h_bind_tick.end(), t_end) -
+                         e->h_bind_tick.begin();
+    *p_hi_out = p_hi;
+    e->stats = ks_step_stats{};
+    e->h_ctr[0] = e->done;
+    e->h_ctr[1] = std::max(p_hi, e->done);
+    e->h_ctr[2] = 0;
+    e->h_ctr[3] = -1;
+    e->h_ctr[4] = 0;
+    *e->h_args = make_args(e);
+    if (p_hi <= e->done) {
+        e->tick = t_end;
+        return false;
+    }
+    return true;
+}
+
+// ks_step, second half: the binds [done, new_done) (node / status copied back by the caller),
+// errors as Run would return them (kubesim.go:114-120, 217-220).
+ks_status step_finish(ks_engine* e, int64_t t_end, int64_t new_done, const int32_t* node, const int32_t* status,
+                      ks_bind* out, int64_t cap, int64_t* n_out) {
+    const int64_t nb = new_done - e->done;
+    for (int64_t i = 0; i < nb && i < cap; i++) {
+        out[i].pod = e->done + i;
+        out[i].node = node[i];
+        out[i].status = status[i];
+        out[i].tick = e->h_bind_tick[e->done + i];
+    }
+    *n_out = nb;
+    e->done = new_done;
+    if (e->h_ctr[2] != 0) {
+        const int64_t pod = e->h_ctr[3];
+        e->err = (int)e->h_ctr[2];
+        e->tick = e->h_bind_tick[pod];
+        e->done = pod + 1;  // popped from the queue, not bound
+        if (e->err == KS_ENOTFOUND)
+            fail(e, KS_ENOTFOUND, "node \"\" not found (pod %lld, tick %lld)", (long long)pod, (long long)e->tick);
+        else
+            fail(e, KS_EINVAL, "pod %lld: invalid pod key or simSpec (tick %lld)", (long long)pod, (long long)e->tick);
+        return (ks_status)e->err;
+    }
+    e->tick = t_end;
+    return KS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 ks_status ks_step(ks_engine* e, int64_t ticks, ks_bind* out, int64_t cap, int64_t* n_out) {
     if (!e || !n_out || ticks < 0) return KS_EINVAL;
     *n_out = 0;
@@ -520,23 +619,13 @@ ks_status ks_step(ks_engine* e, int64_t ticks, ks_bind* out, int64_t cap, int64_
     if (!e->nodes_loaded) return fail(e, KS_EINVAL, "no nodes loaded");
     HIPCHK(e, hipSetDevice(e->device));
     const int64_t t_end = e->tick + ticks;
-    // pods whose bind tick falls in (tick, t_end]
-    const int64_t p_hi = std::upper_bound(e->h_bind_tick.begin() + e->done, e->h_bind_tick.end(), t_end) -
-                         e->h_bind_tick.begin();
-    e->stats = ks_step_stats{};
-    if (p_hi <= e->done) {
-        e->tick = t_end;
-        return KS_OK;
-    }
+    int64_t p_hi = 0;
+    if (!step_prepare(e, ticks, &p_hi)) return KS_OK;
     hipStream_t st = e->st;
-    e->h_ctr[0] = e->done;
-    e->h_ctr[1] = p_hi;
-    e->h_ctr[2] = 0;
-    e->h_ctr[3] = -1;
-    e->h_ctr[4] = 0;
     HIPCHK(e, hipMemcpyAsync(e->d_ctr, e->h_ctr, 5 * sizeof(int64_t), hipMemcpyHostToDevice, st));
+    HIPCHK(e, hipMemcpyAsync(e->d_args, e->h_args, sizeof(ks::EngineArgs), hipMemcpyHostToDevice, st));
     HIPCHK(e, hipEventRecord(e->ev[0], st));
-    const ks::EngineArgs a = make_args(e);
+    const ks::EngineArgs* d = e->d_args;
     int64_t start = e->done;
     int64_t launches = 0;
     double scan_ms = 0, res_ms = 0;
@@ -555,18 +644,18 @@ ks_status ks_step(ks_engine* e, int64_t ticks, ks_bind* out, int64_t cap, int64_
                 for (int k = 0; k < kProfEv; k++) ev[k] = e->prof_ev[kProfEv * launches + k];
             }
             if (ev[0]) HIPCHK(e, hipEventRecord(ev[0], st));
-            HIPCHK(e, ks::launch_expire_head(a, st));
+            HIPCHK(e, ks::launch_expire_head(d, 1, st));
             if (ev[1]) HIPCHK(e, hipEventRecord(ev[1], st));
-            HIPCHK(e, ks::launch_scan(a, e->mode, st));
+            HIPCHK(e, ks::launch_scan(d, 1, e->blk_n, e->B, e->PG, e->mode, st));
             if (ev[2]) HIPCHK(e, hipEventRecord(ev[2], st));
             const int G = e->world * e->vsh;
             const int64_t L = ks::kTopL, BL = (int64_t)e->B * L;
             if (G == 1) {
-                HIPCHK(e, ks::launch_merge(a, e->lists, (int64_t)e->nblk * L, e->nblk, L, e->cand, st));
+                HIPCHK(e, ks::launch_merge(d, 1, e->B, nullptr, 0, 0, 0, nullptr, st));
             } else {
                 for (int v = 0; v < e->vsh; v++) {
                     const int p = e->rank * e->vsh + v;
-                    HIPCHK(e, ks::launch_merge(a, e->lists + (int64_t)e->part_lo[p] * L, (int64_t)e->nblk * L,
+                    HIPCHK(e, ks::launch_merge(d, 1, e->B, e->lists + (int64_t)e->part_lo[p] * L, (int64_t)e->nblk * L,
                                                e->part_lo[p + 1] - e->part_lo[p], L, e->cand_all + p * BL, st));
                 }
                 if (e->comm) {
@@ -574,10 +663,10 @@ ks_status ks_step(ks_engine* e, int64_t ticks, ks_bind* out, int64_t cap, int64_
                                                           (size_t)e->vsh * BL, ncclUint64, e->comm, st);
                     if (nr != ncclSuccess) return fail(e, KS_EDEVICE, "ncclAllGather: %s", ncclGetErrorString(nr));
                 }
-                HIPCHK(e, ks::launch_merge(a, e->cand_all, L, G, BL, e->cand, st));
+                HIPCHK(e, ks::launch_merge(d, 1, e->B, e->cand_all, L, G, BL, e->cand, st));
             }
             if (ev[3]) HIPCHK(e, hipEventRecord(ev[3], st));
-            HIPCHK(e, ks::launch_resolve(a, e->mode, st));
+            HIPCHK(e, ks::launch_resolve(d, 1, e->mode, st));
             if (ev[4]) HIPCHK(e, hipEventRecord(ev[4], st));
             launches++;
         }
@@ -614,26 +703,211 @@ ks_status ks_step(ks_engine* e, int64_t ticks, ks_bind* out, int64_t cap, int64_
     e->stats.other_ms = other_ms;
     e->stats.launches = launches;
     e->stats.pods = nb;
-    for (int64_t i = 0; i < nb && i < cap; i++) {
-        out[i].pod = e->done + i;
-        out[i].node = node[i];
-        out[i].status = status[i];
-        out[i].tick = e->h_bind_tick[e->done + i];
+    return step_finish(e, t_end, new_done, node.data(), status.data(), out, cap, n_out);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Scenario groups (BASELINE.json configs[3]): independent what-if clusters stepped together, one
+// launch per kernel for all of them (scenario = a grid dimension; one resolve workgroup each).
+// ---------------------------------------------------------------------------------------------
+struct ks_group {
+    int device = 0;
+    int cap = 0;
+    hipStream_t st = nullptr;
+    std::vector<ks_engine*> engs;
+    int64_t* d_ctr = nullptr;           // [cap][32]
+    int64_t* h_ctr = nullptr;           // pinned
+    ks::EngineArgs* d_args = nullptr;   // [cap]
+    ks::EngineArgs* h_args = nullptr;   // pinned
+    ks::BindSeg* d_seg = nullptr;       // [cap]
+    ks::BindSeg* h_seg = nullptr;       // pinned
+    int32_t* d_out = nullptr;           // packed binds: node, then status
+    int64_t out_cap = 0;
+    std::vector<int32_t> h_out;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    std::string errmsg;
+};
+
+ks_status ks_group_create(int32_t device, int32_t max_scenarios, ks_group** out) {
+    if (!out || max_scenarios < 1 || max_scenarios > 65535) return KS_EINVAL;
+    *out = nullptr;
+    ks_group* g = new ks_group();
+    g->device = device;
+    g->cap = max_scenarios;
+    hipError_t r = hipSetDevice(device);
+    if (r == hipSuccess) r = hipStreamCreateWithFlags(&g->st, hipStreamNonBlocking);
+    if (r == hipSuccess) r = hipMalloc(&g->d_ctr, sizeof(int64_t) * 32 * max_scenarios);
+    if (r == hipSuccess) r = hipHostMalloc(&g->h_ctr, sizeof(int64_t) * 32 * max_scenarios, hipHostMallocDefault);
+    if (r == hipSuccess) r = hipMalloc(&g->d_args, sizeof(ks::EngineArgs) * max_scenarios);
+    if (r == hipSuccess) r = hipHostMalloc(&g->h_args, sizeof(ks::EngineArgs) * max_scenarios, hipHostMallocDefault);
+    if (r == hipSuccess) r = hipMalloc(&g->d_seg, sizeof(ks::BindSeg) * max_scenarios);
+    if (r == hipSuccess) r = hipHostMalloc(&g->h_seg, sizeof(ks::BindSeg) * max_scenarios, hipHostMallocDefault);
+    for (int i = 0; i < 2 && r == hipSuccess; i++) r = hipEventCreate(&g->ev[i]);
+    if (r == hipSuccess) r = hipMemsetAsync(g->d_ctr, 0, sizeof(int64_t) * 32 * max_scenarios, g->st);
+    if (r == hipSuccess) r = hipStreamSynchronize(g->st);
+    if (r != hipSuccess) {
+        ks_group_destroy(g);
+        return KS_EDEVICE;
     }
-    *n_out = nb;
-    e->done = new_done;
-    if (e->h_ctr[2] != 0) {
-        const int64_t pod = e->h_ctr[3];
-        e->err = (int)e->h_ctr[2];
-        e->tick = e->h_bind_tick[pod];
-        e->done = pod + 1;  // popped from the queue, not bound
-        if (e->err == KS_ENOTFOUND)
-            fail(e, KS_ENOTFOUND, "node \"\" not found (pod %lld, tick %lld)", (long long)pod, (long long)e->tick);
-        else
-            fail(e, KS_EINVAL, "pod %lld: invalid pod key or simSpec (tick %lld)", (long long)pod, (long long)e->tick);
-        return (ks_status)e->err;
+    *out = g;
+    return KS_OK;
+}
+
+void ks_group_destroy(ks_group* g) {
+    if (!g) return;
+    (void)hipSetDevice(g->device);
+    if (g->st) (void)hipStreamSynchronize(g->st);
+    for (ks_engine* e : g->engs) engine_free(e);
+    if (g->d_ctr) (void)hipFree(g->d_ctr);
+    if (g->h_ctr) (void)hipHostFree(g->h_ctr);
+    if (g->d_args) (void)hipFree(g->d_args);
+    if (g->h_args) (void)hipHostFree(g->h_args);
+    if (g->d_seg) (void)hipFree(g->d_seg);
+    if (g->h_seg) (void)hipHostFree(g->h_seg);
+    if (g->d_out) (void)hipFree(g->d_out);
+    for (auto ev : g->ev) if (ev) (void)hipEventDestroy(ev);
+    if (g->st) (void)hipStreamDestroy(g->st);
+    delete g;
+}
+
+ks_status ks_group_add(ks_group* g, const ks_config* cfg, ks_engine** out) {
+    if (!g || !cfg || !out) return KS_EINVAL;
+    *out = nullptr;
+    if ((int)g->engs.size() >= g->cap) return KS_EINVAL;
+    if (cfg->device != g->device) return KS_EINVAL;
+    ks_engine* e = nullptr;
+    const ks_status v = engine_init(cfg, &e);
+    if (v != KS_OK) return v;
+    if (!g->engs.empty() && e->B != g->engs[0]->B) {
+        delete e;
+        return KS_EINVAL;  // one batch size per group (one grid)
     }
-    e->tick = t_end;
+    const int idx = (int)g->engs.size();
+    e->group = g;
+    e->st = g->st;
+    e->d_ctr = g->d_ctr + 32 * idx;
+    e->h_ctr = g->h_ctr + 32 * idx;
+    e->d_args = g->d_args + idx;
+    e->h_args = g->h_args + idx;
+    hipError_t r = hipSetDevice(g->device);
+    for (int i = 0; i < 4 && r == hipSuccess; i++) r = hipEventCreate(&e->ev[i]);
+    if (r != hipSuccess) {
+        engine_free(e);
+        return KS_EDEVICE;
+    }
+    g->engs.push_back(e);
+    *out = e;
+    return KS_OK;
+}
+
+int32_t ks_group_size(const ks_group* g) { return g ? (int32_t)g->engs.size() : -1; }
+
+ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, int64_t* n_out, int32_t* status_out,
+                        ks_step_stats* stats) {
+    if (!g || !n_out || !status_out || ticks < 0 || cap < 0) return KS_EINVAL;
+    const int S = (int)g->engs.size();
+    if (S == 0) return KS_OK;
+    if (hipSetDevice(g->device) != hipSuccess) return KS_EDEVICE;
+    std::vector<int64_t> p_hi(S, 0), t_end(S, 0);
+    std::vector<char> live(S, 0);
+    int mode = ks::kEvalTiny, blk_n = 0, B = g->engs[0]->B;
+    int64_t blocks = 0;
+    for (int i = 0; i < S; i++) {
+        ks_engine* e = g->engs[i];
+        n_out[i] = 0;
+        status_out[i] = KS_OK;
+        if (e->err || !e->nodes_loaded || e->world * e->vsh != 1) {
+            status_out[i] = e->err ? e->err : KS_EINVAL;
+            if (!e->err) fail(e, KS_EINVAL, "group step needs loaded, unsharded nodes");
+            e->h_ctr[0] = e->h_ctr[1] = e->done;
+            e->h_ctr[2] = 0;
+            *e->h_args = e->nodes_loaded ? make_args(e) : ks::EngineArgs{};
+            e->h_args->ctr = e->d_ctr;
+            e->h_args->blk_n = 0;
+            continue;
+        }
+        t_end[i] = e->tick + ticks;
+        live[i] = step_prepare(e, ticks, &p_hi[i]);
+        // the widest evaluator any scenario needs (each is exact on every narrower domain)
+        mode = std::min(mode, e->mode);
+        blk_n = std::max(blk_n, e->blk_n);
+        blocks += e->blk_n;
+    }
+    // pods per scan workgroup for the whole group: the most node-record reuse that still leaves
+    // >= ~2048 workgroups per scan
+    int pg = 1;
+    while (pg < ks::max_pods_per_scan_wg() && pg < B && blocks * ((B + pg * 2 - 1) / (pg * 2)) >= 2048) pg *= 2;
+    for (int i = 0; i < S; i++) g->h_args[i].PG = pg;
+    hipStream_t st = g->st;
+    auto dev = [&](hipError_t r) { return r == hipSuccess; };
+    if (!dev(hipMemcpyAsync(g->d_ctr, g->h_ctr, sizeof(int64_t) * 32 * S, hipMemcpyHostToDevice, st)) ||
+        !dev(hipMemcpyAsync(g->d_args, g->h_args, sizeof(ks::EngineArgs) * S, hipMemcpyHostToDevice, st)) ||
+        !dev(hipEventRecord(g->ev[0], st)))
+        return KS_EDEVICE;
+    std::vector<int64_t> start(S);
+    for (int i = 0; i < S; i++) start[i] = g->engs[i]->done;
+    int64_t launches = 0;
+    while (true) {
+        int64_t nbat = 0;
+        for (int i = 0; i < S; i++)
+            if (live[i]) nbat = std::max(nbat, (p_hi[i] - start[i] + B - 1) / B);
+        if (nbat == 0) break;
+        for (int64_t b = 0; b < nbat; b++) {
+            if (!dev(ks::launch_expire_head(g->d_args, S, st)) ||
+                !dev(ks::launch_scan(g->d_args, S, blk_n, B, pg, mode, st)) ||
+                !dev(ks::launch_merge(g->d_args, S, B, nullptr, 0, 0, 0, nullptr, st)) ||
+                !dev(ks::launch_resolve(g->d_args, S, mode, st)))
+                return KS_EDEVICE;
+            launches++;
+        }
+        if (!dev(hipMemcpyAsync(g->h_ctr, g->d_ctr, sizeof(int64_t) * 32 * S, hipMemcpyDeviceToHost, st)) ||
+            !dev(hipStreamSynchronize(st)))
+            return KS_EDEVICE;
+        for (int i = 0; i < S; i++) {
+            if (!live[i]) continue;
+            ks_engine* e = g->engs[i];
+            start[i] = e->h_ctr[0];
+            if (e->h_ctr[2] != 0 || start[i] >= p_hi[i]) live[i] = 0;
+        }
+    }
+    // binds back: one gather into a packed buffer, one copy
+    int64_t total = 0, max_n = 0;
+    for (int i = 0; i < S; i++) {
+        ks_engine* e = g->engs[i];
+        const int64_t nb = status_out[i] == KS_OK && t_end[i] ? start[i] - e->done : 0;
+        g->h_seg[i] = ks::BindSeg{e->b_node.p, e->b_status.p, e->done, std::max<int64_t>(nb, 0), total};
+        total += std::max<int64_t>(nb, 0);
+        max_n = std::max(max_n, nb);
+    }
+    if (total > g->out_cap) {
+        if (g->d_out) (void)hipFree(g->d_out);
+        g->d_out = nullptr;
+        g->out_cap = std::max<int64_t>(total, 2 * g->out_cap);
+        if (!dev(hipMalloc(&g->d_out, sizeof(int32_t) * 2 * g->out_cap))) return KS_EDEVICE;
+    }
+    g->h_out.resize(2 * std::max<int64_t>(total, 1));
+    if (total) {
+        if (!dev(hipMemcpyAsync(g->d_seg, g->h_seg, sizeof(ks::BindSeg) * S, hipMemcpyHostToDevice, st)) ||
+            !dev(ks::launch_gather_binds(g->d_seg, S, max_n, g->d_out, g->d_out + total, st)) ||
+            !dev(hipMemcpyAsync(g->h_out.data(), g->d_out, sizeof(int32_t) * 2 * total, hipMemcpyDeviceToHost, st)))
+            return KS_EDEVICE;
+    }
+    if (!dev(hipEventRecord(g->ev[1], st)) || !dev(hipStreamSynchronize(st))) return KS_EDEVICE;
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, g->ev[0], g->ev[1]);
+    for (int i = 0; i < S; i++) {
+        ks_engine* e = g->engs[i];
+        if (status_out[i] != KS_OK || !t_end[i]) continue;
+        const ks::BindSeg& sg = g->h_seg[i];
+        status_out[i] = step_finish(e, t_end[i], start[i], g->h_out.data() + sg.off, g->h_out.data() + total + sg.off,
+                                    out ? out + (int64_t)i * cap : nullptr, out ? cap : 0, &n_out[i]);
+    }
+    if (stats) {
+        *stats = ks_step_stats{};
+        stats->step_ms = ms;
+        stats->launches = launches;
+        for (int i = 0; i < S; i++) stats->pods += n_out[i];
+    }
     return KS_OK;
 }
 

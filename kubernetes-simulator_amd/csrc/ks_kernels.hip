@@ -65,14 +65,21 @@ __device__ __forceinline__ int popc_below(uint64_t mask, int lane) {
     return __popcll(mask & ((1ull << lane) - 1ull));
 }
 
+// Every batch kernel takes the device array of its engines' arguments: one engine for ks_step,
+// a group's scenarios side by side for ks_group_step (BASELINE configs[3]: independent what-if
+// clusters in one launch).  The scenario index is a grid dimension, so every field read is
+// uniform (scalar loads).
+
 // ------------------------------------------------------------------------------------------
-// expire_head: expiries due before the batch's first pod, applied straight to the node SoA.
+// expire_head: grid (S).  Expiries due before the batch's first pod, applied straight to the
+// node SoA.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void expire_head_kernel(EngineArgs a) {
+__global__ __launch_bounds__(256) void expire_head_kernel(const EngineArgs* __restrict__ A) {
+    const EngineArgs a = A[blockIdx.x];
     const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
     if (a.ctr[kCtrErr] != 0 || start >= end) return;
     const int64_t e0 = a.exp_off[start], e1 = a.exp_off[start + 1];
-    for (int64_t e = e0 + blockIdx.x * blockDim.x + threadIdx.x; e < e1; e += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
         const int32_t q = a.exp_pod[e];
         if (a.b_status[q] != 0 || a.expired[q]) continue;
         const int32_t nd = a.b_node[q];
@@ -86,15 +93,17 @@ __global__ __launch_bounds__(256) void expire_head_kernel(EngineArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
-// scan: grid (nblk, ceil(B / PG)).  Each wave owns 64 nodes (lane = node); for each of the
+// scan: grid (blk_n, ceil(B / PG), S).  Each wave owns 64 nodes (lane = node); for each of the
 // workgroup's PG pods it extracts its exact top-L keys.  Scores are small integers, so the
 // top-L of a wave is usually one or two "tie classes": take the max score, every lane at it
 // (lowest lanes first), repeat below it — a 32-bit wave max + ballot per class.  The four
 // wave lists are then merged by rank (each list is sorted) into the block's top-L.
 // ------------------------------------------------------------------------------------------
 template <int kMode>
-__global__ __launch_bounds__(256) void scan_kernel(EngineArgs a) {
+__global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict__ A) {
     __shared__ uint64_t wl[kMaxPG][kScanWaves][kL];  // per-pod, per-wave top-L lists
+    const EngineArgs a = A[blockIdx.z];
+    if ((int)blockIdx.x >= a.blk_n) return;  // a group's scenarios may differ in size
     const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
     if (a.ctr[kCtrErr] != 0) return;
     const int64_t nb = min<int64_t>(a.B, end - start);
@@ -153,13 +162,23 @@ __global__ __launch_bounds__(256) void scan_kernel(EngineArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
-// merge: one 256-thread workgroup per pod; exact top-L over nl sorted lists (the scan's block
-// lists of one shard, or the shards' all-gathered lists).
+// merge: grid (B, S), one 256-thread workgroup per pod; exact top-L over nl sorted lists (the
+// scan's block lists of one shard, or the shards' all-gathered lists).  src == nullptr: the
+// scenario's own block lists into its candidate lists.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void merge_kernel(EngineArgs a, const uint64_t* src, int64_t pod_stride, int32_t nl,
-                                                     int64_t list_stride, uint64_t* out) {
+__global__ __launch_bounds__(256) void merge_kernel(const EngineArgs* __restrict__ A, const uint64_t* src,
+                                                     int64_t pod_stride, int32_t nl, int64_t list_stride,
+                                                     uint64_t* out) {
     __shared__ uint64_t red[4];
     __shared__ int32_t owner[4];
+    const EngineArgs a = A[blockIdx.y];
+    if (src == nullptr) {
+        src = a.lists;
+        pod_stride = (int64_t)a.nblk * kL;
+        nl = a.nblk;
+        list_stride = kL;
+        out = a.cand;
+    }
     const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
     if (a.ctr[kCtrErr] != 0) return;
     const int64_t nb = min<int64_t>(a.B, end - start);
@@ -490,8 +509,9 @@ __device__ __forceinline__ void expire_on(const ResolveShared& sh, int e0, int e
 }
 
 template <int kMode>
-__global__ __launch_bounds__(kResolveThreads) void resolve_kernel(EngineArgs a) {
+__global__ __launch_bounds__(kResolveThreads) void resolve_kernel(const EngineArgs* __restrict__ A) {
     __shared__ ResolveShared sh;
+    const EngineArgs a = A[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid >> 6;
     const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
     if (a.ctr[kCtrErr] != 0) return;
@@ -936,35 +956,53 @@ int max_batch_pods() { return kMaxBatchR; }
 int max_pods_per_scan_wg() { return kMaxPG; }
 int block_nodes() { return kBlockNodes; }
 
-hipError_t launch_expire_head(const EngineArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL(expire_head_kernel, dim3(1), dim3(256), 0, st, a);
+hipError_t launch_expire_head(const EngineArgs* d, int S, hipStream_t st) {
+    hipLaunchKernelGGL(expire_head_kernel, dim3(S), dim3(256), 0, st, d);
     return hipGetLastError();
 }
 
-hipError_t launch_scan(const EngineArgs& a, int mode, hipStream_t st) {
-    if (a.blk_n > 0) {
-        const dim3 g(a.blk_n, (a.B + a.PG - 1) / a.PG);
+hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int mode, hipStream_t st) {
+    if (blk_n > 0 && S > 0) {
+        const dim3 g(blk_n, (B + PG - 1) / PG, S);
         switch (mode) {
-            case kEvalTiny: hipLaunchKernelGGL(scan_kernel<kEvalTiny>, g, dim3(kBlockNodes), 0, st, a); break;
-            case kEvalNarrow: hipLaunchKernelGGL(scan_kernel<kEvalNarrow>, g, dim3(kBlockNodes), 0, st, a); break;
-            default: hipLaunchKernelGGL(scan_kernel<kEvalWide>, g, dim3(kBlockNodes), 0, st, a); break;
+            case kEvalTiny: hipLaunchKernelGGL(scan_kernel<kEvalTiny>, g, dim3(kBlockNodes), 0, st, d); break;
+            case kEvalNarrow: hipLaunchKernelGGL(scan_kernel<kEvalNarrow>, g, dim3(kBlockNodes), 0, st, d); break;
+            default: hipLaunchKernelGGL(scan_kernel<kEvalWide>, g, dim3(kBlockNodes), 0, st, d); break;
         }
     }
     return hipGetLastError();
 }
 
-hipError_t launch_merge(const EngineArgs& a, const uint64_t* lists, int64_t pod_stride, int32_t nl,
+hipError_t launch_merge(const EngineArgs* d, int S, int B, const uint64_t* lists, int64_t pod_stride, int32_t nl,
                         int64_t list_stride, uint64_t* out, hipStream_t st) {
-    hipLaunchKernelGGL(merge_kernel, dim3(a.B), dim3(256), 0, st, a, lists, pod_stride, nl, list_stride, out);
+    hipLaunchKernelGGL(merge_kernel, dim3(B, S), dim3(256), 0, st, d, lists, pod_stride, nl, list_stride, out);
     return hipGetLastError();
 }
 
-hipError_t launch_resolve(const EngineArgs& a, int mode, hipStream_t st) {
+hipError_t launch_resolve(const EngineArgs* d, int S, int mode, hipStream_t st) {
     switch (mode) {
-        case kEvalTiny: hipLaunchKernelGGL(resolve_kernel<kEvalTiny>, dim3(1), dim3(kResolveThreads), 0, st, a); break;
-        case kEvalNarrow: hipLaunchKernelGGL(resolve_kernel<kEvalNarrow>, dim3(1), dim3(kResolveThreads), 0, st, a); break;
-        default: hipLaunchKernelGGL(resolve_kernel<kEvalWide>, dim3(1), dim3(kResolveThreads), 0, st, a); break;
+        case kEvalTiny: hipLaunchKernelGGL(resolve_kernel<kEvalTiny>, dim3(S), dim3(kResolveThreads), 0, st, d); break;
+        case kEvalNarrow: hipLaunchKernelGGL(resolve_kernel<kEvalNarrow>, dim3(S), dim3(kResolveThreads), 0, st, d); break;
+        default: hipLaunchKernelGGL(resolve_kernel<kEvalWide>, dim3(S), dim3(kResolveThreads), 0, st, d); break;
     }
+    return hipGetLastError();
+}
+
+// Packed copy of each scenario's new binds (ks_group_step): one D2H copy for the whole group.
+__global__ __launch_bounds__(256) void gather_binds_kernel(const BindSeg* __restrict__ segs, int32_t* node,
+                                                            int32_t* status) {
+    const BindSeg g = segs[blockIdx.y];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < g.n; i += (int64_t)gridDim.x * blockDim.x) {
+        node[g.off + i] = g.node[g.lo + i];
+        status[g.off + i] = g.status[g.lo + i];
+    }
+}
+
+hipError_t launch_gather_binds(const BindSeg* segs, int S, int64_t max_n, int32_t* node, int32_t* status,
+                               hipStream_t st) {
+    if (S <= 0 || max_n <= 0) return hipSuccess;
+    const unsigned bx = (unsigned)std::min<int64_t>((max_n + 255) / 256, 64);
+    hipLaunchKernelGGL(gather_binds_kernel, dim3(bx, S), dim3(256), 0, st, segs, node, status);
     return hipGetLastError();
 }
 

@@ -27,7 +27,8 @@ STATUS_NAMES = {KS_OK: "OK", KS_EINVAL: "InvalidArgument", KS_ENOTFOUND: "NotFou
 EXPORTED_SYMBOLS = ("ks_create", "ks_destroy", "ks_load_nodes", "ks_submit_pods", "ks_step",
                     "ks_filter", "ks_score", "ks_usage", "ks_current_tick", "ks_queued_pods",
                     "ks_last_error", "ks_last_step_stats", "ks_set_profiling", "ks_debug_counters",
-                    "ks_comm_unique_id", "ks_shard")
+                    "ks_comm_unique_id", "ks_shard", "ks_group_create", "ks_group_destroy",
+                    "ks_group_add", "ks_group_size", "ks_group_step")
 KS_COMM_ID_BYTES = 128
 
 
@@ -91,5 +92,15 @@ def load():
     L.ks_comm_unique_id.restype = C.c_int
     L.ks_shard.argtypes = [p, C.c_int32, C.c_int32, p, C.c_int32]
     L.ks_shard.restype = C.c_int
+    L.ks_group_create.argtypes = [C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]
+    L.ks_group_create.restype = C.c_int
+    L.ks_group_destroy.argtypes = [p]
+    L.ks_group_destroy.restype = None
+    L.ks_group_add.argtypes = [p, C.POINTER(KsConfig), C.POINTER(C.c_void_p)]
+    L.ks_group_add.restype = C.c_int
+    L.ks_group_size.argtypes = [p]
+    L.ks_group_size.restype = C.c_int32
+    L.ks_group_step.argtypes = [p, C.c_int64, p, C.c_int64, p, p, C.POINTER(KsStepStats)]
+    L.ks_group_step.restype = C.c_int
     _lib = L
     return L

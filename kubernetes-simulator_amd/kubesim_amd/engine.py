@@ -43,32 +43,43 @@ def _c(a, dt):
     return np.ascontiguousarray(a, dtype=dt)
 
 
+def _config(tick_seconds, filter_mode, filters, scorers, device, batch_pods, engine_flags):
+    cfg = KsConfig()
+    cfg.abi_version = _lib.KS_ABI_VERSION
+    cfg.tick_seconds = tick_seconds
+    cfg.filter_mode = filter_mode
+    cfg.filters = filters
+    cfg.n_scorers = len(scorers)
+    for i, (k, w, v) in enumerate(scorers):
+        cfg.scorers[i].kind, cfg.scorers[i].weight, cfg.scorers[i].value = k, w, v
+    cfg.device = device
+    cfg.batch_pods = batch_pods
+    cfg.engine_flags = engine_flags
+    return cfg
+
+
 class Engine:
     def __init__(self, *, tick_seconds=10, filter_mode=_lib.KS_FILTER_REFERENCE_LITERAL, filters=0,
-                 scorers=((_lib.KS_SCORER_CONST, 1, 1),), device=0, batch_pods=0, engine_flags=0):
+                 scorers=((_lib.KS_SCORER_CONST, 1, 1),), device=0, batch_pods=0, engine_flags=0,
+                 _group=None):
         L = _lib.load()
-        cfg = KsConfig()
-        cfg.abi_version = _lib.KS_ABI_VERSION
-        cfg.tick_seconds = tick_seconds
-        cfg.filter_mode = filter_mode
-        cfg.filters = filters
-        cfg.n_scorers = len(scorers)
-        for i, (k, w, v) in enumerate(scorers):
-            cfg.scorers[i].kind, cfg.scorers[i].weight, cfg.scorers[i].value = k, w, v
-        cfg.device = device
-        cfg.batch_pods = batch_pods
-        cfg.engine_flags = engine_flags
+        self._group = _group
+        cfg = _config(tick_seconds, filter_mode, filters, scorers, device, batch_pods, engine_flags)
         h = C.c_void_p()
-        rc = L.ks_create(C.byref(cfg), C.byref(h))
+        if _group is None:
+            rc = L.ks_create(C.byref(cfg), C.byref(h))
+        else:
+            rc = L.ks_group_add(_group.h, C.byref(cfg), C.byref(h))
         if rc != _lib.KS_OK:
-            raise KsError(rc, "ks_create rejected the configuration")
+            raise KsError(rc, "ks_create / ks_group_add rejected the configuration")
         self._L = L
         self.h = h
         self.n = 0
 
     def close(self):
         if getattr(self, "h", None):
-            self._L.ks_destroy(self.h)
+            if getattr(self, "_group", None) is None:  # a group's members die with the group
+                self._L.ks_destroy(self.h)
             self.h = None
 
     def __del__(self):
@@ -179,3 +190,57 @@ def comm_unique_id() -> bytes:
     if rc != 0:
         raise KsError(rc, "ks_comm_unique_id failed")
     return bytes(buf)
+
+
+class Group:
+    """Independent what-if scenarios (BASELINE.json configs[3]) stepped together on one device:
+    one launch per kernel for all members (include/ks_engine.h, ks_group_*)."""
+
+    def __init__(self, max_scenarios: int, device: int = 0):
+        self._L = _lib.load()
+        h = C.c_void_p()
+        rc = self._L.ks_group_create(device, max_scenarios, C.byref(h))
+        if rc != _lib.KS_OK:
+            raise KsError(rc, "ks_group_create failed")
+        self.h = h
+        self.device = device
+        self.members = []
+
+    def add(self, **cfg) -> Engine:
+        """A member engine (same keyword configuration as :class:`Engine`)."""
+        cfg.setdefault("device", self.device)
+        e = Engine(_group=self, **cfg)
+        self.members.append(e)
+        return e
+
+    def step(self, ticks: int, cap: int | None = None, with_binds: bool = True):
+        """Advance every member ``ticks`` ticks.  Returns (list of bind arrays or counts,
+        list of status codes, stats dict)."""
+        S = len(self.members)
+        cap = (ticks if cap is None else cap) if with_binds else 0
+        out = (KsBind * max(S * cap, 1))() if with_binds else None
+        n = np.zeros(S, np.int64)
+        st = np.zeros(S, np.int32)
+        stats = KsStepStats()
+        rc = self._L.ks_group_step(self.h, ticks, out, cap, _p(n), _p(st), C.byref(stats))
+        if rc != _lib.KS_OK:
+            raise KsError(rc, "ks_group_step failed")
+        dt = np.dtype([("pod", "<i8"), ("node", "<i4"), ("status", "<i4"), ("tick", "<i8")])
+        res = []
+        if with_binds:
+            allb = np.frombuffer(out, dtype=dt, count=S * cap) if S * cap else np.zeros(0, dt)
+            for i in range(S):
+                res.append(allb[i * cap:i * cap + min(int(n[i]), cap)].copy())
+        else:
+            res = [int(x) for x in n]
+        return res, [int(x) for x in st], dict(step_ms=stats.step_ms, launches=stats.launches, pods=stats.pods)
+
+    def close(self):
+        if getattr(self, "h", None):
+            for e in self.members:
+                e.h = None
+            self._L.ks_group_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()

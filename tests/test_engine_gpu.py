@@ -222,3 +222,65 @@ def test_shard_geometry_rejected():
     eng.load_nodes(np.array([[1000, 1000, -1, 10]]), np.zeros(1, np.uint64), np.zeros(1, np.uint64))
     with pytest.raises(KsError):
         eng.shard(1, 0, None, 2)  # after load_nodes
+
+
+# ---- scenario groups (BASELINE.json configs[3]): what-if clusters side by side in one launch ----
+def test_group_scenarios_match_oracle():
+    """Scenarios of different sizes, traces and outcomes (one aborts with NotFound) stepped
+    together; each must equal its own oracle run, and an aborted member must not disturb the
+    others."""
+    from kubesim_amd.engine import Group
+    mode = "feeds_all_lrba"
+    fm, fl, sc = MODES[mode]
+    specs = [(0, 300, 900), (1, 700, 1200), (2, 64, 800), (3, 1500, 600), (4, 200, 1000)]
+    g = Group(len(specs))
+    runs = []
+    for s, n, p in specs:
+        tr = tracegen.c4_scenario(s, n_nodes=n, n_pods=p)
+        enc = encoded(tr)
+        e = g.add(tick_seconds=tr["tick_seconds"], filter_mode=fm, filters=fl, scorers=sc, batch_pods=256)
+        e.load_nodes(enc["alloc"], enc["taint"], enc["label"])
+        e.submit(enc["pods"])
+        o = make_oracle(tr, mode)
+        o.submit(tr)
+        runs.append((e, o))
+    aborted = 0
+    for chunk in (250, 1000):
+        binds, st, stats = g.step(chunk)
+        for (e, o), eb, rc in zip(runs, binds, st):
+            ob, orc = oracle_run(o, chunk)
+            assert_same_binds(eb, ob)
+            assert rc == orc
+            aborted += rc != 0
+            if rc == 0:
+                np.testing.assert_array_equal(e.usage(), o.usage())
+    assert stats["launches"] >= 1
+    g.close()
+
+
+def test_group_member_steps_alone_too():
+    """A member can still be stepped on its own (ks_step) and agrees with the group path."""
+    from kubesim_amd.engine import Group
+    mode = "feeds_all_lrba"
+    fm, fl, sc = MODES[mode]
+    tr = tracegen.c4_scenario(9, n_nodes=500, n_pods=700)
+    enc = encoded(tr)
+    g = Group(2)
+    a = g.add(tick_seconds=10, filter_mode=fm, filters=fl, scorers=sc)
+    b = g.add(tick_seconds=10, filter_mode=fm, filters=fl, scorers=sc)
+    for e in (a, b):
+        e.load_nodes(enc["alloc"], enc["taint"], enc["label"])
+        e.submit(enc["pods"])
+    a1, rc1 = engine_run(a, 300, 300)  # member alone: ticks 1..300
+    o = make_oracle(tr, mode)
+    o.submit(tr)
+    ob1, orc1 = oracle_run(o, 300)
+    assert_same_binds(a1, ob1)
+    assert rc1 == orc1 == 0
+    (a2, b1), st, _ = g.step(300)      # a: ticks 301..600, b: ticks 1..300
+    np.testing.assert_array_equal(a1, b1)
+    assert st[1] == 0
+    ob2, orc2 = oracle_run(o, 300)     # the oracle may stop with NotFound: so must `a`
+    assert_same_binds(a2, ob2)
+    assert st[0] == orc2
+    g.close()
