@@ -253,9 +253,10 @@ def main_c4(args):
     barrier()
     t_start = time.perf_counter()
     binds, dev_ms, launches, aborted = 0, 0.0, 0, 0
-    for _ in range(args.steps):
-        res, st, stats = g.step(S_pps)
-        binds += sum(len(b) for b in res)
+    for k in range(args.steps):
+        _, cnt, st, stats = g.step(S_pps)
+        log(f"[rank {rank}] step {k}: {stats['step_ms']:.1f} device ms, {stats['launches']} batch rounds")
+        binds += int(cnt.sum())
         dev_ms += stats["step_ms"]
         launches += stats["launches"]
         aborted += sum(1 for x in st if x != 0)

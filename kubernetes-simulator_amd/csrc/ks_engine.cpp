@@ -672,8 +672,11 @@ ks_status ks_step(ks_engine* e, int64_t ticks, ks_bind* out, int64_t cap, int64_
         }
         HIPCHK(e, hipMemcpyAsync(e->h_ctr, e->d_ctr, 5 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
         HIPCHK(e, hipStreamSynchronize(st));
+        const int64_t prev = start;
         start = e->h_ctr[0];
         if (e->h_ctr[2] != 0 || start >= p_hi) break;
+        // every launch commits at least its first pod (resolve_kernel): no progress is a bug
+        if (start <= prev) return fail(e, KS_EDEVICE, "scheduling made no progress at pod %lld", (long long)start);
     }
     HIPCHK(e, hipEventRecord(e->ev[1], st));
     const int64_t new_done = start;
@@ -866,8 +869,13 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
         for (int i = 0; i < S; i++) {
             if (!live[i]) continue;
             ks_engine* e = g->engs[i];
+            const int64_t prev = start[i];
             start[i] = e->h_ctr[0];
             if (e->h_ctr[2] != 0 || start[i] >= p_hi[i]) live[i] = 0;
+            else if (start[i] <= prev) {  // every launch commits at least its first pod
+                g->errmsg = "scheduling made no progress";
+                return KS_EDEVICE;
+            }
         }
     }
     // binds back: one gather into a packed buffer, one copy

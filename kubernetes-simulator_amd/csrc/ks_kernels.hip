@@ -626,7 +626,11 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(const EngineAr
         Prefetch p0;
         prefetch_issue(a, sh, 0, lane, exact, p0);
         prefetch_commit(sh, lane, p0, -1, 0, 0);
-        if (lane == 0) sh.ctl[0].ntab = sh.n_t;
+        // Pod 0 never stops on an exhausted list: its own expiries were applied before the scan
+        // and nothing else has changed yet, so every touched entry still holds its snapshot key
+        // and is evaluated exactly below — a node outside the list cannot beat them.  (Stopping
+        // here would commit nothing, and the next launch would rescan the same state forever.)
+        if (lane == 0) { sh.ctl[0].ntab = sh.n_t; sh.ctl[0].kfull = 0; }
         if (nb > 1) prefetch_issue(a, sh, 1, lane, exact, pf);
     } else if (oslot >= 0 && r < sh.n_t) {
         own = t_node(sh, r);

@@ -213,27 +213,29 @@ class Group:
         self.members.append(e)
         return e
 
-    def step(self, ticks: int, cap: int | None = None, with_binds: bool = True):
-        """Advance every member ``ticks`` ticks.  Returns (list of bind arrays or counts,
-        list of status codes, stats dict)."""
+    def step(self, ticks: int, cap: int | None = None):
+        """Advance every member ``ticks`` ticks.  Returns (binds, counts, statuses, stats):
+        ``binds`` is one structured array (pod, node, status, tick) holding member i's binds at
+        rows [i * cap, i * cap + counts[i]) — :meth:`split` cuts it per member."""
         S = len(self.members)
-        cap = (ticks if cap is None else cap) if with_binds else 0
-        out = (KsBind * max(S * cap, 1))() if with_binds else None
+        cap = ticks if cap is None else cap
+        if getattr(self, "_out_n", -1) < S * cap:  # reused across steps (no per-step 10s of MB)
+            self._out = (KsBind * max(S * cap, 1))()
+            self._out_n = S * cap
         n = np.zeros(S, np.int64)
         st = np.zeros(S, np.int32)
         stats = KsStepStats()
-        rc = self._L.ks_group_step(self.h, ticks, out, cap, _p(n), _p(st), C.byref(stats))
+        rc = self._L.ks_group_step(self.h, ticks, self._out, cap, _p(n), _p(st), C.byref(stats))
         if rc != _lib.KS_OK:
             raise KsError(rc, "ks_group_step failed")
         dt = np.dtype([("pod", "<i8"), ("node", "<i4"), ("status", "<i4"), ("tick", "<i8")])
-        res = []
-        if with_binds:
-            allb = np.frombuffer(out, dtype=dt, count=S * cap) if S * cap else np.zeros(0, dt)
-            for i in range(S):
-                res.append(allb[i * cap:i * cap + min(int(n[i]), cap)].copy())
-        else:
-            res = [int(x) for x in n]
-        return res, [int(x) for x in st], dict(step_ms=stats.step_ms, launches=stats.launches, pods=stats.pods)
+        allb = np.frombuffer(self._out, dtype=dt, count=S * cap) if S * cap else np.zeros(0, dt)
+        self._cap = cap
+        return allb, np.minimum(n, cap), st, dict(step_ms=stats.step_ms, launches=stats.launches, pods=stats.pods)
+
+    def split(self, binds, counts):
+        """Per-member copies of the binds returned by :meth:`step`."""
+        return [binds[i * self._cap:i * self._cap + int(c)].copy() for i, c in enumerate(counts)]
 
     def close(self):
         if getattr(self, "h", None):

@@ -246,8 +246,8 @@ def test_group_scenarios_match_oracle():
         runs.append((e, o))
     aborted = 0
     for chunk in (250, 1000):
-        binds, st, stats = g.step(chunk)
-        for (e, o), eb, rc in zip(runs, binds, st):
+        allb, cnt, st, stats = g.step(chunk)
+        for (e, o), eb, rc in zip(runs, g.split(allb, cnt), st):
             ob, orc = oracle_run(o, chunk)
             assert_same_binds(eb, ob)
             assert rc == orc
@@ -277,7 +277,8 @@ def test_group_member_steps_alone_too():
     ob1, orc1 = oracle_run(o, 300)
     assert_same_binds(a1, ob1)
     assert rc1 == orc1 == 0
-    (a2, b1), st, _ = g.step(300)      # a: ticks 301..600, b: ticks 1..300
+    allb, cnt, st, _ = g.step(300)     # a: ticks 301..600, b: ticks 1..300
+    a2, b1 = g.split(allb, cnt)
     np.testing.assert_array_equal(a1, b1)
     assert st[1] == 0
     ob2, orc2 = oracle_run(o, 300)     # the oracle may stop with NotFound: so must `a`
