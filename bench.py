@@ -198,6 +198,12 @@ def main():
                          "note": "algorithmic bytes = 80 B x (pods x nodes) per scan launch; the scan reuses "
                                  "each node record across the batch's pods, so frac can exceed 1 — traffic is "
                                  "the measured HBM bytes per launch"},
+            "dominant": {"kernel": "resolve_kernel",
+                         "share_of_device_time": st["resolve_ms"] / max(st["scan_ms"] + st["resolve_ms"] + st["other_ms"], 1e-9),
+                         "ns_per_pod": st["resolve_ms"] * 1e6 / max(st["pods"], 1),
+                         "bound": "latency: one workgroup per batch walks its pods in FIFO order, one "
+                                  "barrier-separated dependent step per pod (DESIGN.md §4); no HBM or "
+                                  "MFMA roofline applies"},
             "kernels": {"launches_per_step": launches, "pods_per_launch": pods_per_launch,
                         "scan_avg_ms": scan_avg_ms, "resolve_avg_ms": res_avg_ms,
                         "other_avg_ms": other_avg_ms,
