@@ -479,8 +479,9 @@ hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int
 // per scenario and pod b < batch size: exact top-L over nl sorted lists
 // lists[b*pod_stride + k*list_stride] into out (lists == nullptr: the scenario's own block lists
 // into its candidate lists)
+// nl_max: the largest nl of the launch (<= 64 / L candidates per pod: one wave per pod)
 hipError_t launch_merge(const EngineArgs* d, int S, int B, const uint64_t* lists, int64_t pod_stride, int32_t nl,
-                        int64_t list_stride, uint64_t* out, hipStream_t st);
+                        int64_t list_stride, uint64_t* out, int nl_max, hipStream_t st);
 hipError_t launch_resolve(const EngineArgs* d, int S, int mode, hipStream_t st);
 struct BindSeg {
     const int32_t* node;

@@ -651,19 +651,20 @@ ks_status ks_step(ks_engine* e, int64_t ticks, ks_bind* out, int64_t cap, int64_
             const int G = e->world * e->vsh;
             const int64_t L = ks::kTopL, BL = (int64_t)e->B * L;
             if (G == 1) {
-                HIPCHK(e, ks::launch_merge(d, 1, e->B, nullptr, 0, 0, 0, nullptr, st));
+                HIPCHK(e, ks::launch_merge(d, 1, e->B, nullptr, 0, 0, 0, nullptr, e->nblk, st));
             } else {
                 for (int v = 0; v < e->vsh; v++) {
                     const int p = e->rank * e->vsh + v;
+                    const int nlp = e->part_lo[p + 1] - e->part_lo[p];
                     HIPCHK(e, ks::launch_merge(d, 1, e->B, e->lists + (int64_t)e->part_lo[p] * L, (int64_t)e->nblk * L,
-                                               e->part_lo[p + 1] - e->part_lo[p], L, e->cand_all + p * BL, st));
+                                               nlp, L, e->cand_all + p * BL, nlp, st));
                 }
                 if (e->comm) {
                     const ncclResult_t nr = ncclAllGather(e->cand_all + (int64_t)e->rank * e->vsh * BL, e->cand_all,
                                                           (size_t)e->vsh * BL, ncclUint64, e->comm, st);
                     if (nr != ncclSuccess) return fail(e, KS_EDEVICE, "ncclAllGather: %s", ncclGetErrorString(nr));
                 }
-                HIPCHK(e, ks::launch_merge(d, 1, e->B, e->cand_all, L, G, BL, e->cand, st));
+                HIPCHK(e, ks::launch_merge(d, 1, e->B, e->cand_all, L, G, BL, e->cand, G, st));
             }
             if (ev[3]) HIPCHK(e, hipEventRecord(ev[3], st));
             HIPCHK(e, ks::launch_resolve(d, 1, e->mode, st));
@@ -858,7 +859,7 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
         for (int64_t b = 0; b < nbat; b++) {
             if (!dev(ks::launch_expire_head(g->d_args, S, st)) ||
                 !dev(ks::launch_scan(g->d_args, S, blk_n, B, pg, mode, st)) ||
-                !dev(ks::launch_merge(g->d_args, S, B, nullptr, 0, 0, 0, nullptr, st)) ||
+                !dev(ks::launch_merge(g->d_args, S, B, nullptr, 0, 0, 0, nullptr, blk_n, st)) ||
                 !dev(ks::launch_resolve(g->d_args, S, mode, st)))
                 return KS_EDEVICE;
             launches++;

@@ -227,6 +227,37 @@ __global__ __launch_bounds__(256) void merge_kernel(const EngineArgs* __restrict
     }
 }
 
+// merge_small: the same for nl * L <= 64 candidates per pod (clusters of <= 2048 nodes — a
+// what-if group's scenarios — or a merge of <= 8 shards): one wave per pod, lane = candidate,
+// L rounds of a wave max.  Grid (ceil(B / 4), S).
+__global__ __launch_bounds__(256) void merge_small_kernel(const EngineArgs* __restrict__ A, const uint64_t* src,
+                                                           int64_t pod_stride, int32_t nl, int64_t list_stride,
+                                                           uint64_t* out) {
+    const EngineArgs a = A[blockIdx.y];
+    if (src == nullptr) {
+        src = a.lists;
+        pod_stride = (int64_t)a.nblk * kL;
+        nl = a.nblk;
+        list_stride = kL;
+        out = a.cand;
+    }
+    const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
+    if (a.ctr[kCtrErr] != 0) return;
+    const int64_t nb = min<int64_t>(a.B, end - start);
+    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
+    const int b = blockIdx.x * (blockDim.x / kWave) + wave;
+    if (b >= nb) return;  // wave-uniform: the wave max below needs every lane
+    const int li = lane / kL, le = lane % kL;
+    uint64_t v = li < nl ? src[(int64_t)b * pod_stride + (int64_t)li * list_stride + le] : 0ull;
+#pragma unroll
+    for (int r = 0; r < kL; ++r) {
+        const uint64_t m = wave_max_u64(v);
+        if (lane == 0) out[(int64_t)b * kL + r] = m;
+        const uint64_t hit = __ballot(v == m && m != 0);
+        if (hit && lane == __ffsll((unsigned long long)hit) - 1) v = 0;
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // resolve: one workgroup, sequential over the batch in FIFO order (one bind per tick).
 //
@@ -978,8 +1009,12 @@ hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int
 }
 
 hipError_t launch_merge(const EngineArgs* d, int S, int B, const uint64_t* lists, int64_t pod_stride, int32_t nl,
-                        int64_t list_stride, uint64_t* out, hipStream_t st) {
-    hipLaunchKernelGGL(merge_kernel, dim3(B, S), dim3(256), 0, st, d, lists, pod_stride, nl, list_stride, out);
+                        int64_t list_stride, uint64_t* out, int nl_max, hipStream_t st) {
+    if ((int64_t)nl_max * kL <= kWave)
+        hipLaunchKernelGGL(merge_small_kernel, dim3((B + 3) / 4, S), dim3(256), 0, st, d, lists, pod_stride, nl,
+                           list_stride, out);
+    else
+        hipLaunchKernelGGL(merge_kernel, dim3(B, S), dim3(256), 0, st, d, lists, pod_stride, nl, list_stride, out);
     return hipGetLastError();
 }
 
