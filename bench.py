@@ -79,8 +79,8 @@ def main():
     ap.add_argument("--nodes", type=int, default=50_000)
     ap.add_argument("--pods", type=int, default=1_000_000)
     ap.add_argument("--batch", type=int, default=0, help="pods per scan/resolve batch (0 = engine default)")
-    ap.add_argument("--cpu-sample-pods", type=int, default=4000)
-    ap.add_argument("--cpu-budget-s", type=float, default=15.0)
+    ap.add_argument("--cpu-sample-pods", type=int, default=12000)
+    ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--config", choices=("c3", "c4"), default="c3",
                     help="c3 (default): the metric's 50k-node workload; c4: BASELINE configs[3], "

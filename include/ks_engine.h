@@ -20,6 +20,8 @@
  *   ks_score .................... api.Scorer.Score aggregated over the registered scorers
  *                                 (api/scheduler.go:36, kubesim/kubesim.go:193-206)
  *   ks_usage .................... Σ Pod.ResourceUsage(clock) per node (kubesim/pod/pod.go:47-63)
+ *   ks_pod_status ............... Pod.BuildStatus phase / times (kubesim/pod/pod.go:78-167)
+ *   ks_group_* .................. one KubeSim.Run per what-if scenario, stepped together
  *   ks_last_error ............... the error text Run would return
  *
  * Status codes map 1:1 onto the reference's error kinds (strongerrors):
@@ -159,6 +161,22 @@ ks_status ks_score(ks_engine* eng, int64_t pod, int64_t* score_out);
 
 /* usage_out[n][3]: Σ over pods on each node of ResourceUsage at the current tick. */
 ks_status ks_usage(ks_engine* eng, int64_t* usage_out);
+
+/* Pod status (Pod.BuildStatus, kubesim/pod/pod.go:78-145) at the current tick, for pods
+ * [pod_lo, pod_lo + n) of the FIFO: PENDING = not bound (queued, or the pod an aborted run stopped
+ * at — the reference never stores it); FAILED = bound OverCapacity (PodFailed / CapacityExceeded);
+ * RUNNING / SUCCEEDED = bound Ok and IsRunning (pod.go:67-69) or not.  start_tick = the bind tick
+ * (StartTime = start clock + start_tick * tick), total_seconds = Σ phase seconds as the reference's
+ * int32 sum (FinishedAt = StartTime + total_seconds, pod.go:165-167). */
+enum { KS_PHASE_PENDING = 0, KS_PHASE_RUNNING = 1, KS_PHASE_SUCCEEDED = 2, KS_PHASE_FAILED = 3 };
+typedef struct {
+    int32_t phase;
+    int32_t node;           /* -1 when not bound */
+    int64_t start_tick;     /* -1 when not bound */
+    int32_t total_seconds;
+    int32_t pad;
+} ks_pod_info;
+ks_status ks_pod_status(ks_engine* eng, int64_t pod_lo, int64_t n, ks_pod_info* out);
 
 int64_t ks_current_tick(const ks_engine* eng);
 int64_t ks_queued_pods(const ks_engine* eng);

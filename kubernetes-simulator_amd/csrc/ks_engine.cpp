@@ -112,6 +112,7 @@ struct ks_engine {
     std::vector<int64_t> h_bind_tick, h_fin;
     std::vector<int64_t> h_exp_off{0};
     std::vector<int32_t> h_dur;
+    std::vector<int32_t> h_total_sec;  // Σ phase seconds, int32 wrapping (Pod.totalSeconds)
     std::priority_queue<std::pair<int64_t, int64_t>, std::vector<std::pair<int64_t, int64_t>>,
                         std::greater<std::pair<int64_t, int64_t>>>
         pending;  // (finish tick, pod) not yet attached to a later pod
@@ -475,6 +476,7 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
     std::vector<ks::PodRec> recs(m);
     std::vector<int32_t> dur(m), poff(m), cum(nf);
     std::vector<int64_t> t0(m), fin(m), eoff(m);
+    std::vector<int32_t> tsec(m);
     std::vector<int32_t> epod;
     epod.reserve(m);
     const int64_t epod_base = e->exp_pod.n;
@@ -499,6 +501,7 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
             cum[f] = (int32_t)acc;
         }
         const int32_t S = (int32_t)acc;
+        tsec[i] = S;
         const int64_t d = S > 0 ? ((int64_t)S + e->cfg.tick_seconds - 1) / e->cfg.tick_seconds : 0;
         dur[i] = (int32_t)d;
         t0[i] = bt;
@@ -548,6 +551,7 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
     e->h_bind_tick.insert(e->h_bind_tick.end(), t0.begin(), t0.end());
     e->h_fin.insert(e->h_fin.end(), fin.begin(), fin.end());
     e->h_dur.insert(e->h_dur.end(), dur.begin(), dur.end());
+    e->h_total_sec.insert(e->h_total_sec.end(), tsec.begin(), tsec.end());
     e->h_exp_off.insert(e->h_exp_off.end(), eoff.begin(), eoff.end());
     e->P += m;
     e->F += nf;
@@ -967,6 +971,35 @@ ks_status ks_usage(ks_engine* e, int64_t* usage_out) {
                                e->t0.p, e->dur.p, e->phase_off.p, e->cum_sec.p, e->use.p, e->d_usage, e->st));
     HIPCHK(e, hipMemcpyAsync(usage_out, e->d_usage, sizeof(int64_t) * 3 * e->n, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
+    return KS_OK;
+}
+
+ks_status ks_pod_status(ks_engine* e, int64_t pod_lo, int64_t n, ks_pod_info* out) {
+    if (!e || (n > 0 && !out) || pod_lo < 0 || n < 0 || pod_lo + n > e->P) return KS_EINVAL;
+    if (n == 0) return KS_OK;
+    const int64_t hi = std::min(pod_lo + n, e->done), nb = std::max<int64_t>(hi - pod_lo, 0);
+    std::vector<int32_t> node(nb), status(nb);
+    if (nb) {
+        HIPCHK(e, hipSetDevice(e->device));
+        HIPCHK(e, hipMemcpyAsync(node.data(), e->b_node.p + pod_lo, sizeof(int32_t) * nb, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(e, hipMemcpyAsync(status.data(), e->b_status.p + pod_lo, sizeof(int32_t) * nb, hipMemcpyDeviceToHost, e->st));
+        HIPCHK(e, hipStreamSynchronize(e->st));
+    }
+    for (int64_t i = 0; i < n; i++) {
+        const int64_t q = pod_lo + i;
+        ks_pod_info& o = out[i];
+        o.total_seconds = e->h_total_sec[q];
+        const bool bound = i < nb && node[i] >= 0;
+        o.node = bound ? node[i] : -1;
+        o.start_tick = bound ? e->h_bind_tick[q] : -1;
+        if (!bound) o.phase = KS_PHASE_PENDING;
+        else if (status[i] != KS_POD_OK) o.phase = KS_PHASE_FAILED;  // CapacityExceeded
+        else {
+            // IsRunning (kubesim/pod/pod.go:67-69): passed = (t - t0) * tick < Σ phase seconds
+            const int64_t dt = e->tick - e->h_bind_tick[q];
+            o.phase = (dt >= 0 && dt < e->h_dur[q]) ? KS_PHASE_RUNNING : KS_PHASE_SUCCEEDED;
+        }
+    }
     return KS_OK;
 }
 

@@ -28,7 +28,7 @@ EXPORTED_SYMBOLS = ("ks_create", "ks_destroy", "ks_load_nodes", "ks_submit_pods"
                     "ks_filter", "ks_score", "ks_usage", "ks_current_tick", "ks_queued_pods",
                     "ks_last_error", "ks_last_step_stats", "ks_set_profiling", "ks_debug_counters",
                     "ks_comm_unique_id", "ks_shard", "ks_group_create", "ks_group_destroy",
-                    "ks_group_add", "ks_group_size", "ks_group_step")
+                    "ks_group_add", "ks_group_size", "ks_group_step", "ks_pod_status")
 KS_COMM_ID_BYTES = 128
 
 
@@ -45,6 +45,14 @@ class KsConfig(C.Structure):
 
 class KsBind(C.Structure):
     _fields_ = [("pod", C.c_int64), ("node", C.c_int32), ("status", C.c_int32), ("tick", C.c_int64)]
+
+
+class KsPodInfo(C.Structure):
+    _fields_ = [("phase", C.c_int32), ("node", C.c_int32), ("start_tick", C.c_int64),
+                ("total_seconds", C.c_int32), ("pad", C.c_int32)]
+
+
+KS_PHASE_PENDING, KS_PHASE_RUNNING, KS_PHASE_SUCCEEDED, KS_PHASE_FAILED = 0, 1, 2, 3
 
 
 class KsStepStats(C.Structure):
@@ -102,5 +110,7 @@ def load():
     L.ks_group_size.restype = C.c_int32
     L.ks_group_step.argtypes = [p, C.c_int64, p, C.c_int64, p, p, C.POINTER(KsStepStats)]
     L.ks_group_step.restype = C.c_int
+    L.ks_pod_status.argtypes = [p, C.c_int64, C.c_int64, p]
+    L.ks_pod_status.restype = C.c_int
     _lib = L
     return L

@@ -75,6 +75,7 @@ class Engine:
         self._L = L
         self.h = h
         self.n = 0
+        self._submitted = 0
 
     def close(self):
         if getattr(self, "h", None):
@@ -122,6 +123,7 @@ class Engine:
                 _c(pods["phase_off"], np.int32), _c(pods["phase_sec"], np.int32),
                 _c(pods["phase_use"], np.int64).reshape(-1, 3), _c(pods["flags"], np.uint8)]
         self._check(self._L.ks_submit_pods(self.h, m, *[_p(a) for a in arrs]))
+        self._submitted += m
 
     # -- tick loop ---------------------------------------------------------------------------
     def step(self, ticks: int, cap: int | None = None):
@@ -151,6 +153,16 @@ class Engine:
         out = np.zeros((self.n, 3), np.int64)
         self._check(self._L.ks_usage(self.h, _p(out)))
         return out
+
+    def pod_status(self, pod_lo: int = 0, n: int | None = None):
+        """Pod.BuildStatus phases (kubesim/pod/pod.go:78-145) at the current tick: structured
+        array (phase, node, start_tick, total_seconds); phases _lib.KS_PHASE_*."""
+        n = (self._submitted - pod_lo) if n is None else n
+        out = (_lib.KsPodInfo * max(n, 1))()
+        self._check(self._L.ks_pod_status(self.h, pod_lo, n, out))
+        dt = np.dtype([("phase", "<i4"), ("node", "<i4"), ("start_tick", "<i8"), ("total_seconds", "<i4"),
+                       ("pad", "<i4")])
+        return np.frombuffer(out, dtype=dt, count=n).copy()
 
     @property
     def tick(self):

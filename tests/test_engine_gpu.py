@@ -285,3 +285,43 @@ def test_group_member_steps_alone_too():
     assert_same_binds(a2, ob2)
     assert st[0] == orc2
     g.close()
+
+
+# ---- pod status: Pod.BuildStatus phases -----------------------------------
+def test_pod_status_matches_reference_rules():
+    """Phases from the oracle's binds restated with the reference's rules (kubesim/pod/pod.go:
+    67-69 IsRunning, 78-145 BuildStatus): FAILED for OverCapacity, RUNNING while
+    (t - t0) * tick < Σ phase seconds, else SUCCEEDED; PENDING when not bound."""
+    from kubesim_amd import _lib
+    tr = small_trace(13, n_nodes=60, n_pods=900, arrival="stream")
+    mode = "literal_lrba_filters_ignored"  # filters ignored: OverCapacity binds happen
+    enc = encoded(tr)
+    eng = make_engine(tr, enc, mode)
+    eng.submit(enc["pods"])
+    ora = make_oracle(tr, mode)
+    ora.submit(tr)
+    p = tr["pods"]
+    S = np.add.reduceat(p["phase_sec"].astype(np.int64), p["phase_off"][:-1]) if len(p["phase_sec"]) else None
+    S = np.where(np.diff(p["phase_off"]) > 0, S, 0).astype(np.int64)
+    S32 = ((S + 2**31) % 2**32 - 2**31).astype(np.int64)  # int32 wrapping sum (pod.go:155-162)
+    binds = []
+    for ticks in (150, 400, 1200):
+        eb, erc = engine_run(eng, ticks, ticks)
+        ob, orc = oracle_run(ora, ticks)
+        assert_same_binds(eb, ob)
+        binds.append(eb)
+        allb = np.concatenate(binds)
+        st = eng.pod_status()
+        t = eng.tick
+        exp = np.full(p["m"], _lib.KS_PHASE_PENDING)
+        q = allb["pod"]
+        ok = allb["status"] == 0
+        running = ok & ((t - allb["tick"]) * tr["tick_seconds"] < S32[q])
+        exp[q] = np.where(~ok, _lib.KS_PHASE_FAILED, np.where(running, _lib.KS_PHASE_RUNNING, _lib.KS_PHASE_SUCCEEDED))
+        np.testing.assert_array_equal(st["phase"], exp)
+        np.testing.assert_array_equal(st["node"][q], allb["node"])
+        np.testing.assert_array_equal(st["start_tick"][q], allb["tick"])
+        np.testing.assert_array_equal(st["total_seconds"], S32)
+        assert (st["phase"] == _lib.KS_PHASE_FAILED).any() or ticks < 1200
+        if erc:
+            break
