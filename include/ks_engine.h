@@ -52,6 +52,7 @@ typedef enum {
     KS_ENOTFOUND = 2,
     KS_EDEVICE = 3,
     KS_ENOMEM = 4,
+    KS_ERANGE = 5,  /* valid input outside the engine's exact domain (ks_ingest.h) */
 } ks_status;
 
 /* filter_mode: the reference discards the Filter result (kubesim/kubesim.go:182) —

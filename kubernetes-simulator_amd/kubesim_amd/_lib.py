@@ -11,7 +11,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libks_engine.so")
 
-KS_OK, KS_EINVAL, KS_ENOTFOUND, KS_EDEVICE, KS_ENOMEM = 0, 1, 2, 3, 4
+KS_OK, KS_EINVAL, KS_ENOTFOUND, KS_EDEVICE, KS_ENOMEM, KS_ERANGE = 0, 1, 2, 3, 4, 5
 KS_FILTER_REFERENCE_LITERAL, KS_FILTER_FEEDS_SCORE = 0, 1
 KS_FILTER_FIT, KS_FILTER_TAINT, KS_FILTER_SELECTOR = 1, 2, 4
 KS_SCORER_CONST, KS_SCORER_LEAST_REQUESTED, KS_SCORER_BALANCED = 0, 1, 2
@@ -21,14 +21,18 @@ KS_ABI_VERSION = 1
 KS_ENGINE_FORCE_WIDE = 1
 
 STATUS_NAMES = {KS_OK: "OK", KS_EINVAL: "InvalidArgument", KS_ENOTFOUND: "NotFound",
-                KS_EDEVICE: "DeviceError", KS_ENOMEM: "OutOfMemory"}
+                KS_EDEVICE: "DeviceError", KS_ENOMEM: "OutOfMemory", KS_ERANGE: "OutOfDomain"}
 
-# every symbol include/ks_engine.h declares
+# every symbol include/*.h declares
 EXPORTED_SYMBOLS = ("ks_create", "ks_destroy", "ks_load_nodes", "ks_submit_pods", "ks_step",
                     "ks_filter", "ks_score", "ks_usage", "ks_current_tick", "ks_queued_pods",
                     "ks_last_error", "ks_last_step_stats", "ks_set_profiling", "ks_debug_counters",
                     "ks_comm_unique_id", "ks_shard", "ks_group_create", "ks_group_destroy",
-                    "ks_group_add", "ks_group_size", "ks_group_step", "ks_pod_status")
+                    "ks_group_add", "ks_group_size", "ks_group_step", "ks_pod_status",
+                    # include/ks_ingest.h
+                    "ks_parse_quantity", "ks_parse_simspec", "ks_cluster_parse", "ks_cluster_free",
+                    "ks_cluster_nodes", "ks_cluster_tick", "ks_cluster_start_clock", "ks_cluster_arrays",
+                    "ks_cluster_node_name", "ks_cluster_tolerations", "ks_cluster_selector")
 KS_COMM_ID_BYTES = 128
 
 
@@ -112,5 +116,28 @@ def load():
     L.ks_group_step.restype = C.c_int
     L.ks_pod_status.argtypes = [p, C.c_int64, C.c_int64, p]
     L.ks_pod_status.restype = C.c_int
+    # ingest (include/ks_ingest.h)
+    L.ks_parse_quantity.argtypes = [C.c_char_p, C.POINTER(C.c_int64)]
+    L.ks_parse_quantity.restype = C.c_int
+    L.ks_parse_simspec.argtypes = [C.c_char_p, C.c_int32, C.POINTER(C.c_int32), p, p, p, C.c_char_p, C.c_int32]
+    L.ks_parse_simspec.restype = C.c_int
+    L.ks_cluster_parse.argtypes = [C.c_char_p, C.POINTER(C.c_void_p), C.c_char_p, C.c_int32]
+    L.ks_cluster_parse.restype = C.c_int
+    L.ks_cluster_free.argtypes = [p]
+    L.ks_cluster_free.restype = None
+    L.ks_cluster_nodes.argtypes = [p]
+    L.ks_cluster_nodes.restype = C.c_int64
+    L.ks_cluster_tick.argtypes = [p]
+    L.ks_cluster_tick.restype = C.c_int32
+    L.ks_cluster_start_clock.argtypes = [p]
+    L.ks_cluster_start_clock.restype = C.c_char_p
+    L.ks_cluster_arrays.argtypes = [p, p, p, p]
+    L.ks_cluster_arrays.restype = C.c_int
+    L.ks_cluster_node_name.argtypes = [p, C.c_int64]
+    L.ks_cluster_node_name.restype = C.c_char_p
+    L.ks_cluster_tolerations.argtypes = [p, C.c_int32, p, p, p, p, C.POINTER(C.c_uint64)]
+    L.ks_cluster_tolerations.restype = C.c_int
+    L.ks_cluster_selector.argtypes = [p, C.c_int32, p, p, C.POINTER(C.c_uint64)]
+    L.ks_cluster_selector.restype = C.c_int
     _lib = L
     return L

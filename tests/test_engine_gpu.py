@@ -325,3 +325,36 @@ def test_pod_status_matches_reference_rules():
         assert (st["phase"] == _lib.KS_PHASE_FAILED).any() or ticks < 1200
         if erc:
             break
+
+
+# ---- host ingest end to end: YAML / Quantity / simSpec text -> engine ----
+def test_c1_from_text_through_ingest():
+    """config/sample.yml's cluster and examples/main.go's pods given as TEXT, parsed by the C++
+    ingest (ks_cluster_parse, ks_parse_quantity, ks_parse_simspec) and scheduled on the device:
+    the committed C1 KAT (tests/golden/c1_kat.json) must come out."""
+    from kubesim_amd.engine import Engine
+    from kubesim_amd.ingest import Cluster, parse_quantity, parse_simspec
+    from test_ingest import CONFIG, K
+    with open(os.path.join(GOLDEN, "c1_kat.json")) as f:
+        kat = json.load(f)
+    cfg = CONFIG[:CONFIG.index("  - namespace: other")]            # node-0, node-1 of the sample
+    cfg = cfg[:cfg.index("    taints:")]                          # without the extra taints
+    c = Cluster(cfg)
+    eng = Engine(tick_seconds=c.tick, filter_mode=0, filters=0, scorers=((0, 1, 1),))
+    eng.load_nodes(c.alloc, c.taint, c.label)
+    inp = K["c1_inputs"]
+    req = [parse_quantity(inp["pod_requests"][k])[1] for k in ("cpu", "memory", "nvidia.com/gpu")]
+    phases = parse_simspec(inp["sim_spec"])
+    m = kat["ticks"]
+    names = ("cpu", "memory", "nvidia.com/gpu")
+    pods = dict(m=m, arrival=np.arange(1, m + 1), req=np.tile(req, (m, 1)), keymask=np.full(m, 7, np.uint8),
+                tol=np.zeros(m, np.uint64), sel=np.zeros(m, np.uint64),
+                phase_off=np.arange(0, len(phases) * m + 1, len(phases), dtype=np.int32),
+                phase_sec=np.tile([s for s, _ in phases], m).astype(np.int32),
+                phase_use=np.tile([[u.get(k, 0) for k in names] for _, u in phases], (m, 1)),
+                flags=np.zeros(m, np.uint8))
+    eng.submit(pods)
+    for t, exp in enumerate(kat["binds"], start=1):
+        b = eng.step(1)
+        assert [(int(x["pod"]), int(x["node"]), int(x["tick"]), int(x["status"])) for x in b] == [tuple(exp)]
+        np.testing.assert_array_equal(eng.usage(), np.array(kat["usage"][t - 1], dtype=np.int64))

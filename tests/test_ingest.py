@@ -1,0 +1,178 @@
+"""Host ingest (include/ks_ingest.h, kubernetes-simulator_amd/csrc/ks_ingest.cpp) — CPU only.
+
+Pinned by the reference's own unit-test vectors (tests/golden/reference_kats.json: util_test.go,
+spec_test.go, config_test.go) and by agreement with the independent Quantity / simSpec
+restatement (oracle/quantity.py) on a seeded fuzz set of quantity strings.
+"""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+import quantity as Q
+from kubesim_amd import _lib, encode, tracegen
+from kubesim_amd.engine import KsError
+from kubesim_amd.ingest import Cluster, parse_quantity, parse_simspec
+
+with open(os.path.join(os.path.dirname(__file__), "golden", "reference_kats.json")) as f:
+    K = json.load(f)
+
+
+def test_build_resource_list_kat():
+    ok, bad = K["build_resource_list"]
+    assert {k: parse_quantity(v)[1] for k, v in ok["input"].items()} == ok["expect"]
+    assert parse_quantity(bad["input"]["foo"])[0] == _lib.KS_EINVAL  # "bar": InvalidArgument
+
+
+def test_parse_spec_kat():
+    ok, bad = K["parse_spec"]
+    got = [[sec, use] for sec, use in parse_simspec(ok["input"])]
+    assert got == ok["expect"]
+    with pytest.raises(KsError) as e:
+        parse_simspec(bad["input"])  # misspelled resourceUsagi: errInvalidResourceUsageField
+    assert e.value.code == _lib.KS_EINVAL and "resoruceUsage" in str(e.value)
+
+
+def _fuzz_quantities(n, seed=7):
+    rng = random.Random(seed)
+    sufs = ["", "n", "u", "m", "k", "M", "G", "T", "P", "E", "Ki", "Mi", "Gi", "Ti", "Pi", "Ei",
+            "e3", "E-2", "e+4", "e0", "e", "x", "KiB", "mm", "e1.5"]
+    out = ["0", "", "-0", "+5", "1.", ".5", "0.000", "007", "1.G", "--1", "1e", "1E18", "1e-9", "1e-10"]
+    for _ in range(n):
+        num = "".join(rng.choice("0123456789") for _ in range(rng.randint(0, 12)))
+        den = "".join(rng.choice("0123456789") for _ in range(rng.randint(0, 6)))
+        s = rng.choice(["", "", "", "-", "+"]) + num + (("." + den) if rng.random() < 0.4 else "") + rng.choice(sufs)
+        out.append(s)
+    return out
+
+
+def test_quantity_matches_restatement():
+    """Same accept / reject and the same exact milli value as oracle/quantity.py."""
+    for s in _fuzz_quantities(4000):
+        rc, milli = parse_quantity(s)
+        try:
+            v = Q.parse_quantity(s)
+        except Q.QuantityError:
+            assert rc == _lib.KS_EINVAL, (s, rc)
+            continue
+        m = Q.to_milli(v)
+        if m is None or m < 0 or m >= 1 << 63:
+            assert rc == _lib.KS_ERANGE, (s, rc, m)
+        else:
+            assert rc == _lib.KS_OK and milli == m, (s, rc, milli, m)
+
+
+def test_simspec_edge_cases():
+    assert parse_simspec("") == []
+    assert parse_simspec("# nothing\n") == []
+    two = "- seconds: 3\n  resourceUsage: {}\n- resourceUsage:\n    cpu: \"250m\"\n"
+    assert parse_simspec(two) == [(3, {}), (0, {"cpu": 250})]
+    for bad in ("- seconds: 3\n", "seconds: 3\n", "- seconds: x\n  resourceUsage:\n    cpu: 1\n",
+                "- seconds: 1\n  resourceUsage:\n    cpu: 1x\n"):
+        with pytest.raises(KsError) as e:
+            parse_simspec(bad)
+        assert e.value.code == _lib.KS_EINVAL, bad
+    with pytest.raises(KsError) as e:  # a resource the engine does not model
+        parse_simspec("- seconds: 1\n  resourceUsage:\n    ephemeral-storage: 1Gi\n")
+    assert e.value.code == _lib.KS_ERANGE
+
+
+CONFIG = """# cluster config in the reference's schema (kubesim/config/config.go:15-41)
+logLevel: debug
+tick: 10
+startClock: 2019-01-01T00:00:00+09:00
+cluster:
+  nodes:
+  - namespace: default
+    name: node-0
+    capacity:
+      cpu: 4
+      memory: 8Gi
+      nvidia.com/gpu: 1
+      pods: 2
+    labels:
+      beta.kubernetes.io/os: simulated
+  - namespace: default
+    name: node-1
+    capacity:
+      cpu: 8
+      memory: 16Gi
+      nvidia.com/gpu: 2
+      pods: 4
+    labels:
+      beta.kubernetes.io/os: simulated
+    taints:
+    - key: dedicated
+      value: batch
+      effect: NoSchedule
+    - key: spot
+      value: "yes"
+      effect: PreferNoSchedule
+  - namespace: other
+    name: node-2
+    capacity:
+      cpu: 500m
+      memory: "1.5Gi"
+"""
+
+
+def test_cluster_config_matches_c1_inputs():
+    c = Cluster(CONFIG)
+    assert c.n == 3 and c.tick == 10 and c.start_clock == "2019-01-01T00:00:00+09:00"
+    assert c.names == ["default/node-0", "default/node-1", "other/node-2"]
+    nodes = K["c1_inputs"]["nodes"]
+    for i in range(2):
+        exp = [Q.to_milli(Q.parse_quantity(nodes[i][k])) for k in ("cpu", "memory", "nvidia.com/gpu")]
+        assert list(c.alloc[i, :3]) == exp and c.alloc[i, 3] == int(nodes[i]["pods"])
+    assert list(c.alloc[2]) == [500, int(1.5 * 2**30) * 1000, -1, 0]  # gpu absent: -1, pods: 0
+    # one NoSchedule taint in the dictionary (PreferNoSchedule never filters); one label pair
+    assert list(c.taint) == [0, 1, 0] and list(c.label) == [1, 1, 0]
+    assert c.tolerations([("dedicated", "Equal", "batch", "NoSchedule")]) == 1
+    assert c.tolerations([("dedicated", "Equal", "other", "")]) == 0
+    assert c.tolerations([("", "Exists", "", "")]) == 1          # empty key + Exists: everything
+    assert c.tolerations([("dedicated", "Exists", "", "NoExecute")]) == 0
+    assert c.tolerations([("dedicated", "Bogus", "batch", "")]) == 0
+    assert c.selector([("beta.kubernetes.io/os", "simulated")]) == 1
+    assert c.selector([("zone", "a")]) == 1 << 63
+
+
+def test_cluster_config_errors():
+    bad_effect = CONFIG.replace("effect: NoSchedule", "effect: Invalid")  # config_test.go TestBuildTaint
+    with pytest.raises(KsError) as e:
+        Cluster(bad_effect)
+    assert e.value.code == _lib.KS_EINVAL
+    with pytest.raises(KsError) as e:
+        Cluster(CONFIG.replace("cpu: 500m", "cpu: 5x"))  # BuildResourceList: InvalidArgument
+    assert e.value.code == _lib.KS_EINVAL
+    dup = CONFIG.replace("name: node-2", "name: node-0")  # nodes keyed by name (kubesim.go:37-47)
+    c = Cluster(dup)
+    assert c.names == ["default/node-1", "other/node-0"]
+
+
+def test_tolerations_match_python_encoder():
+    """ks_cluster_tolerations against the vectorised ToleratesTaint of kubesim_amd.encode on a
+    seeded C3-like trace's taint dictionary."""
+    tr = tracegen.c3_trace(n_nodes=300, n_pods=400)
+    st = tr["strings"]
+    nd = tr["nodes"]
+    eff = {1: "NoSchedule", 2: "PreferNoSchedule", 3: "NoExecute"}
+    lines = ["cluster:", "  nodes:"]
+    for i in range(nd["n"]):
+        lines += [f"  - name: n{i}", "    capacity:", "      cpu: 1", "      pods: 1", "    taints:"]
+        a, b = nd["taint_off"][i], nd["taint_off"][i + 1]
+        if a == b:
+            lines[-1] = "    taints: []"
+        for k, v, e in nd["taint"][a:b]:
+            lines += [f"    - key: \"{st[k]}\"", f"      value: \"{st[v]}\"", f"      effect: {eff[int(e)]}"]
+    c = Cluster("\n".join(lines) + "\n")
+    enc = encode.encode_trace(tr)
+    np.testing.assert_array_equal(c.taint, enc["taint"])
+    p = tr["pods"]
+    ops = {tracegen.OP_EQUAL: "Equal", tracegen.OP_EXISTS: "Exists", tracegen.OP_INVALID: "Bogus"}
+    effn = {0: "", 1: "NoSchedule", 2: "PreferNoSchedule", 3: "NoExecute"}
+    for q in range(p["m"]):
+        a, b = p["tol_off"][q], p["tol_off"][q + 1]
+        tols = [(st[k], ops[int(o)], st[v], effn[int(e)]) for k, o, v, e in p["tol"][a:b]]
+        assert c.tolerations(tols) == int(enc["pods"]["tol"][q]), (q, tols)
