@@ -93,15 +93,16 @@ __global__ __launch_bounds__(256) void expire_head_kernel(const EngineArgs* __re
 }
 
 // ------------------------------------------------------------------------------------------
-// scan: grid (blk_n, ceil(B / PG), S).  Each wave owns 64 nodes (lane = node); for each of the
-// workgroup's PG pods it extracts its exact top-L keys.  Scores are small integers, so the
-// top-L of a wave is usually one or two "tie classes": take the max score, every lane at it
-// (lowest lanes first), repeat below it — a 32-bit wave max + ballot per class.  The four
-// wave lists are then merged by rank (each list is sorted) into the block's top-L.
+// scan: grid (blk_n, ceil(B / PG), S).  A workgroup owns one 256-node block (lane = node within
+// its wave's 64) and PG pods.  Phase 1: every wave evaluates its nodes for all PG pods into an
+// LDS key table (one u32 total+1 per pod and node).  Phase 2: one wave per pod extracts the
+// block's exact top-L from the 256 keys (4 per lane).  Scores are small integers, so the top-L
+// is usually one or two "tie classes": take the max, every node at it in node order, repeat below
+// it — a lane max of 4, a 32-bit wave max and 4 ballots per class.
 // ------------------------------------------------------------------------------------------
 template <int kMode>
 __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict__ A) {
-    __shared__ uint64_t wl[kMaxPG][kScanWaves][kL];  // per-pod, per-wave top-L lists
+    extern __shared__ uint32_t kv[];  // [PG][kBlockNodes]: total+1 per (pod, node of the block)
     const EngineArgs a = A[blockIdx.z];
     if ((int)blockIdx.x >= a.blk_n) return;  // a group's scenarios may differ in size
     const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
@@ -111,53 +112,43 @@ __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict_
     if (pg0 >= nb) return;
     const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
     const int blk = a.blk_lo + blockIdx.x;
-    const uint32_t base = (uint32_t)blk * kBlockNodes + wave * kWave;
-    const int64_t node = (int64_t)base + lane;
+    const uint32_t blk_base = (uint32_t)blk * kBlockNodes;
+    const int64_t node = (int64_t)blk_base + threadIdx.x;
     const bool valid = node < a.c.n_nodes;
     NodeV n{};
     if (node < (int64_t)a.c.nwb * kWave) n = load_node(a.s, node);
     const int np = (int)min<int64_t>(a.PG, nb - pg0);
     for (int b = 0; b < np; ++b) {
         const PodRec p = a.pods[start + pg0 + b];
-        uint32_t rem = valid ? eval_t<kMode>(a.c, p, n) : 0u;
-        int cnt = 0;
-        for (int r = 0; r < kL && cnt < kL; ++r) {
-            const uint32_t m = wave_max_u32(rem);
-            if (m == 0) break;
-            const uint64_t mask = __ballot(rem == m);
-            if (rem == m) {
-                const int rank = cnt + popc_below(mask, lane);
-                if (rank < kL) wl[b][wave][rank] = make_key(m, base + lane);
-                rem = 0;
-            }
-            cnt += __popcll(mask);
-        }
-        if (lane >= cnt && lane < kL) wl[b][wave][lane] = 0ull;
+        kv[b * kBlockNodes + threadIdx.x] = valid ? eval_t<kMode>(a.c, p, n) : 0u;
     }
     __syncthreads();
-    // merge: 32 candidates per pod (4 lists x L), two pods per wave pass; the rank of a
-    // candidate = its position in its own list + the entries of the other lists above it.
-    const int half = lane >> 5, l32 = lane & 31;
-    const int li = l32 / kL, le = l32 % kL;
-    for (int b0 = wave * 2; b0 < np; b0 += kScanWaves * 2) {
-        const int b = b0 + half;
-        const uint64_t c = b < np ? wl[b][li][le] : 0ull;
-        const uint64_t nz = __ballot(c != 0);
-        if (b < np) {
-            uint64_t* out = a.lists + ((int64_t)(pg0 + b) * a.nblk + blk) * kL;
-            if (c != 0) {
-                int rank = le;
+    for (int b = wave; b < np; b += kScanWaves) {
+        uint32_t v[kScanWaves];
 #pragma unroll
-                for (int o = 0; o < kScanWaves; ++o) {
-                    if (o == li) continue;
+        for (int u = 0; u < kScanWaves; ++u) v[u] = kv[b * kBlockNodes + u * kWave + lane];  // node u*64 + lane
+        uint64_t* out = a.lists + ((int64_t)(pg0 + b) * a.nblk + blk) * kL;
+        int cnt = 0;
+        for (int r = 0; r < kL && cnt < kL; ++r) {
+            uint32_t lm = v[0];
 #pragma unroll
-                    for (int k = 0; k < kL; ++k) rank += wl[b][o][k] > c ? 1 : 0;
+            for (int u = 1; u < kScanWaves; ++u) lm = lm > v[u] ? lm : v[u];
+            const uint32_t m = wave_max_u32(lm);
+            if (m == 0) break;
+            int below = cnt;  // nodes of this class before (u, lane) in node order
+#pragma unroll
+            for (int u = 0; u < kScanWaves; ++u) {
+                const uint64_t mask = __ballot(v[u] == m);
+                if (v[u] == m) {
+                    const int rank = below + popc_below(mask, lane);
+                    if (rank < kL) out[rank] = make_key(m, blk_base + u * kWave + lane);
+                    v[u] = 0;
                 }
-                if (rank < kL) out[rank] = c;
+                below += __popcll(mask);
             }
-            const int total = __popcll((nz >> (half * 32)) & 0xFFFFFFFFull);
-            if (l32 < kL && l32 >= total) out[l32] = 0ull;
+            cnt = below;
         }
+        if (lane >= cnt && lane < kL) out[lane] = 0ull;
     }
 }
 
@@ -999,10 +990,11 @@ hipError_t launch_expire_head(const EngineArgs* d, int S, hipStream_t st) {
 hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int mode, hipStream_t st) {
     if (blk_n > 0 && S > 0) {
         const dim3 g(blk_n, (B + PG - 1) / PG, S);
+        const size_t lds = sizeof(uint32_t) * kBlockNodes * PG;
         switch (mode) {
-            case kEvalTiny: hipLaunchKernelGGL(scan_kernel<kEvalTiny>, g, dim3(kBlockNodes), 0, st, d); break;
-            case kEvalNarrow: hipLaunchKernelGGL(scan_kernel<kEvalNarrow>, g, dim3(kBlockNodes), 0, st, d); break;
-            default: hipLaunchKernelGGL(scan_kernel<kEvalWide>, g, dim3(kBlockNodes), 0, st, d); break;
+            case kEvalTiny: hipLaunchKernelGGL(scan_kernel<kEvalTiny>, g, dim3(kBlockNodes), lds, st, d); break;
+            case kEvalNarrow: hipLaunchKernelGGL(scan_kernel<kEvalNarrow>, g, dim3(kBlockNodes), lds, st, d); break;
+            default: hipLaunchKernelGGL(scan_kernel<kEvalWide>, g, dim3(kBlockNodes), lds, st, d); break;
         }
     }
     return hipGetLastError();
