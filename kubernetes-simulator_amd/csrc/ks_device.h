@@ -262,11 +262,13 @@ __host__ __device__ __forceinline__ uint32_t eval_total1_tiny(const Cfg& c, cons
     const bool fit_on = c.filter_feeds && (c.filters & kFilterFit);
     const bool taint_on = c.filter_feeds && (c.filters & kFilterTaint);
     const bool sel_on = c.filter_feeds && (c.filters & kFilterSelector);
+    // bitwise, not short-circuit: no branch, so the pod record stays in SGPRs (scan_kernel)
+    const uint32_t km = p.keymask;
     bool ok = c.has_scorers != 0;
-    ok &= !fit_on || ((n.nr < n.ap) & (!(p.keymask & 1) || uc <= ac) & (!(p.keymask & 2) || um <= am) &
-                      (!(p.keymask & 4) || rg + qg <= ag));
-    ok &= !taint_on || (n.taint & ~p.tol) == 0;
-    ok &= !sel_on || (n.label & p.sel) == p.sel;
+    ok &= !fit_on | ((n.nr < n.ap) & (!(km & 1) | (uc <= ac)) & (!(km & 2) | (um <= am)) &
+                     (!(km & 4) | (rg + qg <= ag)));
+    ok &= !taint_on | ((n.taint & ~p.tol) == 0);
+    ok &= !sel_on | ((n.label & p.sel) == p.sel);
     const bool lc_on = ac > 0 && uc <= ac, lm_on = am > 0 && um <= am;
     const int32_t acs = ac > 0 ? ac : 1, ams = am > 0 ? am : 1;
     const float iac = rcp_est((float)acs), iam = rcp_est((float)ams);  // node-invariant: hoisted
@@ -408,6 +410,22 @@ __host__ __device__ __forceinline__ uint32_t prune_tmax(const Cfg& c, const Prun
     if (fc > -kBoundLR && fm > -kBoundLR)
         total += c.w_ba * (int32_t)(10.f - 10.f * fabsf(fc - fm) + kBoundBA);
     return (uint32_t)total;
+}
+
+// Wave-uniform load through the constant address space: the compiler emits s_load (scalar cache,
+// SGPR result) instead of a flat vector load per lane.  Only for data no kernel in flight writes
+// (pod records, the batch counters written by an earlier kernel of the stream).
+// (Copied dword by dword: a struct copy would go through a generic memcpy and lose the space.)
+template <typename T>
+__device__ __forceinline__ T sload(const T* p) {
+    static_assert(sizeof(T) % 4 == 0, "sload: dword-sized types only");
+    typedef const __attribute__((address_space(4))) uint32_t* cp;
+    const cp q = (cp)p;
+    T v;
+    uint32_t* d = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 4); ++i) d[i] = q[i];
+    return v;
 }
 
 __host__ __device__ __forceinline__ uint64_t make_key(uint32_t total1, uint32_t node) {

@@ -105,8 +105,8 @@ __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict_
     extern __shared__ uint32_t kv[];  // [PG][kBlockNodes]: total+1 per (pod, node of the block)
     const EngineArgs a = A[blockIdx.z];
     if ((int)blockIdx.x >= a.blk_n) return;  // a group's scenarios may differ in size
-    const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
-    if (a.ctr[kCtrErr] != 0) return;
+    const int64_t start = sload(a.ctr + kCtrStart), end = sload(a.ctr + kCtrEnd);
+    if (sload(a.ctr + kCtrErr) != 0) return;
     const int64_t nb = min<int64_t>(a.B, end - start);
     const int pg0 = blockIdx.y * a.PG;
     if (pg0 >= nb) return;
@@ -119,8 +119,9 @@ __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict_
     if (node < (int64_t)a.c.nwb * kWave) n = load_node(a.s, node);
     const int np = (int)min<int64_t>(a.PG, nb - pg0);
     for (int b = 0; b < np; ++b) {
-        const PodRec p = a.pods[start + pg0 + b];
-        kv[b * kBlockNodes + threadIdx.x] = valid ? eval_t<kMode>(a.c, p, n) : 0u;
+        const PodRec p = sload(a.pods + start + pg0 + b);  // uniform: SGPRs, scalar cache
+        const uint32_t t = eval_t<kMode>(a.c, p, n);       // branch-free; padding lanes discarded
+        kv[b * kBlockNodes + threadIdx.x] = valid ? t : 0u;
     }
     __syncthreads();
     for (int b = wave; b < np; b += kScanWaves) {

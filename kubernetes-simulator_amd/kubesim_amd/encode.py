@@ -47,6 +47,26 @@ def _or_reduce_csr(bits: np.ndarray, off: np.ndarray) -> np.ndarray:
     return out
 
 
+def _unique_rows(rows: np.ndarray):
+    """Sorted distinct rows of a small non-negative int table and each row's index into them.
+
+    Rows are packed into one int64 key when the columns fit (lexicographic order is kept),
+    which is much faster than ``np.unique(axis=0)`` on millions of rows."""
+    rows = rows.astype(np.int64)
+    ncol = rows.shape[1]
+    bits = 63 // ncol
+    if rows.min() >= 0 and rows.max() < (1 << bits):
+        key = np.zeros(len(rows), dtype=np.int64)
+        for c in range(ncol):
+            key = (key << bits) | rows[:, c]
+        uk, inv = np.unique(key, return_inverse=True)
+        mask = (1 << bits) - 1
+        uniq = np.stack([(uk >> (bits * (ncol - 1 - c))) & mask for c in range(ncol)], axis=1)
+        return uniq, inv.reshape(-1)
+    uniq, inv = np.unique(rows, axis=0, return_inverse=True)
+    return uniq, inv.reshape(-1)
+
+
 def encode_nodes(nodes: dict):
     """Return ``(alloc[n][4] i64, taint[n] u64, label[n] u64, taint_dict, label_dict)``."""
     n = nodes["n"]
@@ -60,23 +80,26 @@ def encode_nodes(nodes: dict):
 
     t = nodes["taint"]
     filt = (t[:, 2] == NO_SCHEDULE) | (t[:, 2] == NO_EXECUTE) if len(t) else np.zeros(0, bool)
-    trip = [tuple(int(x) for x in r) for r in t[filt]] if len(t) else []
-    taint_dict = sorted(set(trip))
-    if len(taint_dict) > MAX_TAINT_BITS:
-        raise EncodeError(f"{len(taint_dict)} distinct NoSchedule/NoExecute taints > {MAX_TAINT_BITS} (W=1)")
-    tindex = {d: i for i, d in enumerate(taint_dict)}
     tbits = np.zeros(len(t), dtype=np.uint64)
-    for i in np.nonzero(filt)[0]:
-        tbits[i] = np.uint64(1) << np.uint64(tindex[tuple(int(x) for x in t[i])])
+    taint_dict = []
+    if filt.any():
+        # sorted distinct rows: the order of sorted(set(tuples)).
+        uniq, inv = _unique_rows(t[filt])
+        taint_dict = [tuple(int(x) for x in r) for r in uniq]
+        if len(taint_dict) > MAX_TAINT_BITS:
+            raise EncodeError(f"{len(taint_dict)} distinct NoSchedule/NoExecute taints > {MAX_TAINT_BITS} (W=1)")
+        tbits[filt] = np.left_shift(np.uint64(1), inv.reshape(-1).astype(np.uint64))
     node_taint = _or_reduce_csr(tbits, nodes["taint_off"])
 
     lab = nodes["label"]
-    pairs = sorted(set((int(k), int(v)) for k, v in lab)) if len(lab) else []
-    if len(pairs) > MAX_LABEL_BITS:
-        raise EncodeError(f"{len(pairs)} distinct label pairs > {MAX_LABEL_BITS} (W=1)")
-    lindex = {d: i for i, d in enumerate(pairs)}
-    lbits = np.array([np.uint64(1) << np.uint64(lindex[(int(r[0]), int(r[1]))]) for r in lab], dtype=np.uint64) \
-        if len(lab) else np.zeros(0, dtype=np.uint64)
+    pairs = []
+    lbits = np.zeros(len(lab), dtype=np.uint64)
+    if len(lab):
+        uniq, inv = _unique_rows(lab)
+        pairs = [(int(r[0]), int(r[1])) for r in uniq]
+        if len(pairs) > MAX_LABEL_BITS:
+            raise EncodeError(f"{len(pairs)} distinct label pairs > {MAX_LABEL_BITS} (W=1)")
+        lbits = np.left_shift(np.uint64(1), inv.reshape(-1).astype(np.uint64))
     node_label = _or_reduce_csr(lbits, nodes["label_off"])
     assert n == len(alloc)
     return alloc, node_taint, node_label, taint_dict, pairs
