@@ -20,12 +20,20 @@
  * changes no result.  Build-defined plugins: resource fit,
  * taint/toleration and node-selector filters; constant, LeastRequested and
  * BalancedAllocation scorers in exact integer arithmetic.
+ *
+ * ko_set_threads(s, T > 1) runs the per-node loops (node totals, filters, scores, argmax) on T
+ * OpenMP threads — the multi-core CPU baseline of SURVEY.md §8(d).  Every node's work is
+ * independent and the argmax combines per-thread winners in node order, so results are the
+ * same as with one thread.
  */
 #include "ks_oracle.h"
 
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 typedef unsigned __int128 u128;
 
@@ -73,6 +81,7 @@ struct ko_sim {
     int64_t* nrun;    /* [n] */
     uint8_t* cand;
     int64_t* score;
+    int threads; /* OpenMP threads for the per-node loops (1 = serial) */
 };
 
 #define GROW(ptr, type, count)                                                  \
@@ -92,6 +101,7 @@ ko_sim* ko_create(const ko_config* cfg, int64_t n, const int64_t* alloc, const u
     ko_sim* s = (ko_sim*)calloc(1, sizeof(ko_sim));
     s->cfg = *cfg;
     s->n = n;
+    s->threads = 1;
     s->alloc = (int64_t*)dupmem(alloc, sizeof(int64_t) * 4 * (size_t)n);
     s->alloc_has = (uint8_t*)dupmem(alloc_has, (size_t)n);
     s->taint_off = (int32_t*)dupmem(taint_off, sizeof(int32_t) * (size_t)(n + 1));
@@ -125,6 +135,7 @@ void ko_destroy(ko_sim* s) {
 }
 
 int64_t ko_tick(const ko_sim* s) { return s->tick; }
+void ko_set_threads(ko_sim* s, int threads) { s->threads = threads > 1 ? threads : 1; }
 const char* ko_last_error(const ko_sim* s) { return s->errmsg; }
 
 int ko_submit(ko_sim* s, int64_t m, const int64_t* arrival, const int64_t* req,
@@ -203,6 +214,7 @@ static int is_running(const ko_sim* s, int64_t p, int64_t t) {
 
 /* totalResourceRequest + runningPodsNum (node.go:97-118) for every node at tick t. */
 static void node_views(ko_sim* s, int64_t t) {
+#pragma omp parallel for schedule(static) num_threads(s->threads) if (s->threads > 1)
     for (int64_t nd = 0; nd < s->n; nd++) {
         ivec* L = &s->live[nd];
         int64_t tot[3] = {0, 0, 0};
@@ -322,47 +334,84 @@ static int filter_pass(const ko_sim* s, int64_t nd, int64_t p, uint32_t which) {
 /* scheduleOneFilter (kubesim.go:168-188) + the score map of scheduleOneScore (:190-206).
  * cand[n] = node has an entry in nodeScore. */
 static void filter_and_score(ko_sim* s, int64_t p) {
-    /* Filter loop: filter-major, each filter sees the survivors of the previous one. */
-    for (int64_t nd = 0; nd < s->n; nd++) s->cand[nd] = 1;
     static const uint32_t order[3] = {KO_FILTER_FIT, KO_FILTER_TAINT, KO_FILTER_SELECTOR};
-    for (int f = 0; f < 3; f++) {
-        if (!(s->cfg.filters & order[f])) continue;
-        for (int64_t nd = 0; nd < s->n; nd++)
-            if (s->cand[nd]) s->cand[nd] = (uint8_t)filter_pass(s, nd, p, order[f]);
-    }
-    if (s->cfg.filter_mode == KO_FILTER_REFERENCE_LITERAL) {
-        /* kubesim.go:182 reassigns a local only: scoring sees the unfiltered node list. */
+#pragma omp parallel num_threads(s->threads) if (s->threads > 1)
+    {
+        /* Filter loop: filter-major, each filter sees the survivors of the previous one. */
+#pragma omp for schedule(static)
         for (int64_t nd = 0; nd < s->n; nd++) s->cand[nd] = 1;
-    }
-    for (int64_t nd = 0; nd < s->n; nd++) s->score[nd] = 0;
-    if (s->cfg.n_scorers == 0)
-        for (int64_t nd = 0; nd < s->n; nd++) s->cand[nd] = 0; /* nodeScore stays empty */
-    for (int i = 0; i < s->cfg.n_scorers; i++) {
-        int64_t w = s->cfg.scorer_weight[i];
+        for (int f = 0; f < 3; f++) {
+            if (!(s->cfg.filters & order[f])) continue;
+#pragma omp for schedule(static)
+            for (int64_t nd = 0; nd < s->n; nd++)
+                if (s->cand[nd]) s->cand[nd] = (uint8_t)filter_pass(s, nd, p, order[f]);
+        }
+#pragma omp for schedule(static)
         for (int64_t nd = 0; nd < s->n; nd++) {
-            if (!s->cand[nd]) continue;
-            int64_t sc;
-            switch (s->cfg.scorer_kind[i]) {
-                case KO_SCORER_CONST: sc = s->cfg.scorer_value[i]; break;
-                case KO_SCORER_LEAST_REQUESTED: sc = score_lr(s, nd, p); break;
-                default: sc = score_ba(s, nd, p); break;
+            /* kubesim.go:182 reassigns a local only: in the literal mode scoring sees the
+             * unfiltered node list.  With no scorers nodeScore stays empty. */
+            if (s->cfg.filter_mode == KO_FILTER_REFERENCE_LITERAL) s->cand[nd] = 1;
+            if (s->cfg.n_scorers == 0) s->cand[nd] = 0;
+            s->score[nd] = 0;
+        }
+        for (int i = 0; i < s->cfg.n_scorers; i++) {
+            int64_t w = s->cfg.scorer_weight[i];
+#pragma omp for schedule(static)
+            for (int64_t nd = 0; nd < s->n; nd++) {
+                if (!s->cand[nd]) continue;
+                int64_t sc;
+                switch (s->cfg.scorer_kind[i]) {
+                    case KO_SCORER_CONST: sc = s->cfg.scorer_value[i]; break;
+                    case KO_SCORER_LEAST_REQUESTED: sc = score_lr(s, nd, p); break;
+                    default: sc = score_ba(s, nd, p); break;
+                }
+                s->score[nd] += sc * w;
             }
-            s->score[nd] += sc * w;
         }
     }
+}
+
+/* argmax over nodeScore, scoreMax = -1, strict '>' (kubesim.go:208-215); deterministic order =
+ * node index, so ties go to the lowest index.  Threaded: thread k scans the k-th contiguous
+ * index range and the ranges' winners are combined in index order. */
+#define KO_MAX_THREADS 256
+static int64_t argmax_node(const ko_sim* s) {
+    int64_t best = -1, bn = -1;
+    if (s->threads <= 1) {
+        for (int64_t nd = 0; nd < s->n; nd++)
+            if (s->cand[nd] && s->score[nd] > best) {
+                best = s->score[nd];
+                bn = nd;
+            }
+        return bn;
+    }
+    int64_t tb[KO_MAX_THREADS], tn[KO_MAX_THREADS];
+    const int nt = s->threads < KO_MAX_THREADS ? s->threads : KO_MAX_THREADS;
+    for (int k = 0; k < nt; k++) tb[k] = tn[k] = -1;
+#pragma omp parallel for schedule(static, 1) num_threads(nt)
+    for (int k = 0; k < nt; k++) {
+        const int64_t lo = s->n * k / nt, hi = s->n * (k + 1) / nt;
+        int64_t b = -1, n = -1;
+        for (int64_t nd = lo; nd < hi; nd++)
+            if (s->cand[nd] && s->score[nd] > b) {
+                b = s->score[nd];
+                n = nd;
+            }
+        tb[k] = b;
+        tn[k] = n;
+    }
+    for (int k = 0; k < nt; k++)
+        if (tn[k] >= 0 && tb[k] > best) {
+            best = tb[k];
+            bn = tn[k];
+        }
+    return bn;
 }
 
 static int schedule_one(ko_sim* s, int64_t p, int64_t t, int64_t* out_node, int32_t* out_status) {
     node_views(s, t);
     filter_and_score(s, p);
-    /* argmax over nodeScore, scoreMax = -1, strict '>' (kubesim.go:208-215); deterministic
-     * order = node index, so ties go to the lowest index. */
-    int64_t best = -1, bn = -1;
-    for (int64_t nd = 0; nd < s->n; nd++)
-        if (s->cand[nd] && s->score[nd] > best) {
-            best = s->score[nd];
-            bn = nd;
-        }
+    const int64_t bn = argmax_node(s);
     if (bn < 0) {
         snprintf(s->errmsg, sizeof s->errmsg, "node \"\" not found (pod %lld)", (long long)p);
         return KO_ENOTFOUND; /* kubesim.go:217-220 */

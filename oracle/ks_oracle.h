@@ -77,6 +77,8 @@ void ko_usage(ko_sim* s, int64_t* out);
 int ko_eval(ko_sim* s, int64_t pod, uint8_t* feasible, int64_t* score);
 
 int64_t ko_tick(const ko_sim* s);
+/* Per-node loops on `threads` OpenMP threads (default 1); results are identical. */
+void ko_set_threads(ko_sim* s, int threads);
 const char* ko_last_error(const ko_sim* s);
 
 #ifdef __cplusplus

@@ -35,6 +35,7 @@ def lib():
         L.ko_step.argtypes = [p, C.c_int64, p, p, p, p, C.c_int64, p]
         L.ko_usage.argtypes = [p, p]
         L.ko_eval.argtypes = [p, C.c_int64, p, p]
+        L.ko_set_threads.argtypes = [p, C.c_int]
         L.ko_tick.restype = C.c_int64
         L.ko_tick.argtypes = [p]
         L.ko_last_error.restype = C.c_char_p
@@ -75,6 +76,10 @@ class COracle:
                       _c(nd["label_off"], np.int32), _c(nd["label"], np.int32)]
         self.h = lib().ko_create(C.byref(cfg), self.n, *[_ptr(a) for a in self._keep])
         self.m = 0
+
+    def set_threads(self, n: int):
+        """Run the per-node loops on n OpenMP threads (identical results)."""
+        lib().ko_set_threads(self.h, int(n))
 
     def close(self):
         if self.h:

@@ -80,3 +80,21 @@ def test_error_semantics():
     co2.submit(tr)
     b, rc = co2.step(10)
     assert rc == 2 and len(b["pod"]) == 0 and co2.tick == 1
+
+
+@pytest.mark.parametrize("mode", sorted(MODES))
+def test_threaded_oracle_matches_serial(mode):
+    """ko_set_threads (the multi-core CPU baseline) changes no bind, tick, status or usage."""
+    tr = small_trace(29, n_nodes=3000, n_pods=400)
+    out = []
+    for threads in (1, 4):
+        co = make_oracle(tr, mode)
+        co.set_threads(threads)
+        co.submit(tr)
+        b, rc = co.step(400, cap=400)
+        out.append((b, rc, co.usage()))
+    (b1, rc1, u1), (b4, rc4, u4) = out
+    assert rc1 == rc4
+    for k in ("pod", "node", "tick", "status"):
+        np.testing.assert_array_equal(b1[k], b4[k])
+    np.testing.assert_array_equal(u1, u4)
