@@ -91,9 +91,10 @@ typedef struct {
 } ks_config;
 
 /* engine_flags: the engine picks the narrowest exact evaluator the scaled capacities allow
- * (tiny int32 / narrow 32x32->64 / wide 64/128-bit).  FORCE_WIDE keeps the wide one, NO_TINY
- * skips the tiny one; all are exact, the flags exist to test them against each other. */
-enum { KS_ENGINE_FORCE_WIDE = 1, KS_ENGINE_NO_TINY = 2 };
+ * (micro 24-bit / tiny int32 / narrow 32x32->64 / wide 64/128-bit).  FORCE_WIDE keeps the wide
+ * one, NO_TINY skips tiny and micro, NO_MICRO skips micro; all are exact, the flags exist to test
+ * them against each other. */
+enum { KS_ENGINE_FORCE_WIDE = 1, KS_ENGINE_NO_TINY = 2, KS_ENGINE_NO_MICRO = 4 };
 
 typedef struct {
     int64_t pod;    /* FIFO index (submission order) */
@@ -202,6 +203,11 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
  * [4] batches that committed early (top-L list exhausted), [16..31] resolver phase cycle
  * sums in a -DKS_STAMPS diagnostic build (tests/dev/diag_resolve.py). */
 ks_status ks_debug_counters(ks_engine* eng, int64_t* out32);
+/* Device self-test of an evaluator identity the exactness argument rests on (no engine needed).
+ * test 0: the micro evaluator's correction-free LeastRequested floor for every (x, A) with
+ * 0 <= x <= A < 2^16 (ks_device.h).  *failures = mismatching cases (0 = pass). */
+enum { KS_SELFTEST_LR_MICRO = 0 };
+ks_status ks_selftest(int32_t device, int32_t test, int64_t* failures);
 void ks_set_profiling(ks_engine* eng, int enable);
 
 #ifdef __cplusplus

@@ -289,12 +289,80 @@ __host__ __device__ __forceinline__ uint32_t eval_total1_tiny(const Cfg& c, cons
     return ok ? (uint32_t)total + 1u : 0u;
 }
 
-// Evaluator variants: 0 wide (64/128-bit), 1 narrow (capacities < 2^29), 2 tiny (see above).
-enum : int { kEvalWide = 0, kEvalNarrow = 1, kEvalTiny = 2 };
+// ---------------------------------------------------------------------------------------------
+// Micro evaluator: every scaled capacity below 2^16 and Ac * Am below 2^24 (C2-C5 after the gcd
+// scaling).  Requests are clamped to 2^17.  Every product has both factors below 2^24, so each
+// is one full-rate 24-bit multiply (v_mul_u32_u24) instead of a 32-bit one.  LeastRequested
+// needs no correction step: for integers 0 <= x <= A < 2^16, floor(10 x / A) =
+// trunc(fma(x, r, 2^-17)) with r = 10 * rcp(A).  The fma's value is within 2.3e-6 of 10x/A + 2^-17
+// (v_rcp 1 ulp, two roundings, 10x/A <= 10).  At an integer k = 10x/A the bias (7.6e-6) keeps it
+// >= k; otherwise 10x/A <= k + 1 - 1/A and bias + error (9.9e-6) < 1/A (> 1.5e-5) keeps it < k + 1.
+// Checked on the device for every (x, A) pair (ks_selftest).  BalancedAllocation keeps the exact
+// correction step of the tiny evaluator.
+// ---------------------------------------------------------------------------------------------
+constexpr int64_t kMicroCap = 1LL << 16;
+constexpr int64_t kMicroProd = 1LL << 24;
+constexpr int64_t kMicroReq = 1LL << 17;
+constexpr float kMicroBias = 1.0f / 131072.0f;  // 2^-17
+
+__host__ __device__ __forceinline__ int32_t clamp_micro(int64_t q) { return (int32_t)(q < kMicroReq ? q : kMicroReq); }
+
+// a * b for 0 <= a, b < 2^24 (full-rate 24-bit multiply on the device)
+__host__ __device__ __forceinline__ int32_t mul24(int32_t a, int32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (int32_t)__umul24((unsigned)a, (unsigned)b);
+#else
+    return a * b;
+#endif
+}
+
+// floor(10 x / A) for 0 <= x <= A < 2^16 given r = 10 * rcp_est(A) (exactness: above)
+__host__ __device__ __forceinline__ int32_t lr10_micro(int32_t x, float r) {
+    return (int32_t)fmaf((float)x, r, kMicroBias);
+}
+
+__host__ __device__ __forceinline__ uint32_t eval_total1_micro(const Cfg& c, const PodRec& p, const NodeV& n) {
+    const int32_t ac = (int32_t)n.ac, am = (int32_t)n.am, ag = (int32_t)n.ag;
+    const int32_t rc = (int32_t)n.rc, rm = (int32_t)n.rm, rg = (int32_t)n.rg;
+    const int32_t qc = clamp_micro(p.req[0]), qm = clamp_micro(p.req[1]), qg = clamp_micro(p.req[2]);
+    const int32_t uc = rc + qc, um = rm + qm;
+    const bool fit_on = c.filter_feeds && (c.filters & kFilterFit);
+    const bool taint_on = c.filter_feeds && (c.filters & kFilterTaint);
+    const bool sel_on = c.filter_feeds && (c.filters & kFilterSelector);
+    const uint32_t km = p.keymask;
+    bool ok = c.has_scorers != 0;
+    ok &= !fit_on | ((n.nr < n.ap) & (!(km & 1) | (uc <= ac)) & (!(km & 2) | (um <= am)) &
+                     (!(km & 4) | (rg + qg <= ag)));
+    ok &= !taint_on | ((n.taint & ~p.tol) == 0);
+    ok &= !sel_on | ((n.label & p.sel) == p.sel);
+    const bool lc_on = ac > 0 && uc <= ac, lm_on = am > 0 && um <= am;
+    const int32_t acs = ac > 0 ? ac : 1, ams = am > 0 ? am : 1;
+    const float iac = rcp_est((float)acs), iam = rcp_est((float)ams);  // node-invariant: hoisted
+    const float rc10 = 10.f * iac, rm10 = 10.f * iam;
+    const int32_t lc = lc_on ? lr10_micro(ac - uc, rc10) : 0;
+    const int32_t lm = lm_on ? lr10_micro(am - um, rm10) : 0;
+    const bool ba_on = ac > 0 && am > 0 && uc < ac && um < am;
+    const int32_t ucs = ba_on ? uc : 0, ums = ba_on ? um : 0;
+    const int32_t D = mul24(acs, ams), a = mul24(ucs, ams), b = mul24(ums, acs);
+    const int32_t X = a > b ? a - b : b - a;
+    const int32_t N = mul24(D - X, 10);
+    int32_t q = (int32_t)(10.f - 10.f * fabsf((float)ucs * iac - (float)ums * iam));
+    q = q < 0 ? 0 : (q > 10 ? 10 : q);
+    const int32_t t = mul24(q, D);
+    q += (N >= t + D) ? 1 : 0;
+    q -= (N < t) ? 1 : 0;
+    const int32_t total = c.const_total + c.w_lr * ((lc + lm) >> 1) + c.w_ba * (ba_on ? q : 0);
+    return ok ? (uint32_t)total + 1u : 0u;
+}
+
+// Evaluator variants: 0 wide (64/128-bit), 1 narrow (capacities < 2^29), 2 tiny, 3 micro (above).
+// A larger value is a narrower domain; each evaluator is exact on every narrower domain.
+enum : int { kEvalWide = 0, kEvalNarrow = 1, kEvalTiny = 2, kEvalMicro = 3 };
 
 template <int kMode>
 __host__ __device__ __forceinline__ uint32_t eval_t(const Cfg& c, const PodRec& p, const NodeV& n) {
-    if constexpr (kMode == kEvalTiny) return eval_total1_tiny(c, p, n);
+    if constexpr (kMode == kEvalMicro) return eval_total1_micro(c, p, n);
+    else if constexpr (kMode == kEvalTiny) return eval_total1_tiny(c, p, n);
     else if constexpr (kMode == kEvalNarrow) return eval_total1_narrow(c, p, n);
     else return eval_total1(c, p, n);
 }
@@ -513,6 +581,7 @@ hipError_t launch_eval_pod(const Cfg& c, const NodeSoA& s, const PodRec* pod, ui
                            int64_t* score, int mode, hipStream_t st);
 hipError_t launch_flush(const NodeSoA& s, const PodRec* pods, const int64_t* fin, int64_t t, int64_t n_done,
                         const int32_t* b_node, const int32_t* b_status, uint8_t* expired, hipStream_t st);
+hipError_t launch_selftest_lr_micro(unsigned long long* bad, hipStream_t st);
 hipError_t launch_usage(int64_t q_lo, int64_t q_hi, int64_t t, int32_t tick_s, const int32_t* b_node,
                         const int32_t* b_status, const int64_t* t0, const int32_t* dur, const int32_t* phase_off,
                         const int32_t* cum_sec, const int64_t* use, unsigned long long* usage, hipStream_t st);

@@ -36,6 +36,7 @@
 #include <limits>
 #include <queue>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/ks_engine.h"
@@ -205,8 +206,12 @@ void update_mode(ks_engine* e) {
     for (int k = 0; k < 3; k++) m[k] = e->max_alloc[k] / e->scale[k];
     const bool narrow = m[0] < ks::kNarrowCap && m[1] < ks::kNarrowCap && m[2] < ks::kNarrowCap;
     const bool tiny = m[0] < ks::kTinyCap && m[1] < ks::kTinyCap && m[2] < ks::kTinyCap && m[0] * m[1] < ks::kTinyCap;
+    const bool micro = m[0] < ks::kMicroCap && m[1] < ks::kMicroCap && m[2] < ks::kMicroCap &&
+                       m[0] * m[1] < ks::kMicroProd;
+    const bool no_tiny = (e->flags & KS_ENGINE_NO_TINY) != 0;
     e->mode = (e->flags & KS_ENGINE_FORCE_WIDE) ? ks::kEvalWide
-            : (tiny && !(e->flags & KS_ENGINE_NO_TINY)) ? ks::kEvalTiny
+            : (micro && !no_tiny && !(e->flags & KS_ENGINE_NO_MICRO)) ? ks::kEvalMicro
+            : (tiny && !no_tiny) ? ks::kEvalTiny
             : narrow ? ks::kEvalNarrow : ks::kEvalWide;
 }
 
@@ -229,7 +234,8 @@ ks_status engine_init(const ks_config* cfg, ks_engine** out) {
     if (cfg->filters & ~7u) return KS_EINVAL;
     if (cfg->n_scorers < 0 || cfg->n_scorers > 8) return KS_EINVAL;
     if (cfg->batch_pods < 0 || cfg->batch_pods > kMaxBatch) return KS_EINVAL;
-    if (cfg->engine_flags & ~(uint32_t)(KS_ENGINE_FORCE_WIDE | KS_ENGINE_NO_TINY)) return KS_EINVAL;
+    if (cfg->engine_flags & ~(uint32_t)(KS_ENGINE_FORCE_WIDE | KS_ENGINE_NO_TINY | KS_ENGINE_NO_MICRO))
+        return KS_EINVAL;
     int64_t const_total = 0, w_lr = 0, w_ba = 0;
     for (int i = 0; i < cfg->n_scorers; i++) {
         const ks_scorer& sc = cfg->scorers[i];
@@ -730,8 +736,8 @@ struct ks_group {
     ks::BindSeg* d_seg = nullptr;       // [cap]
     ks::BindSeg* h_seg = nullptr;       // pinned
     int32_t* d_out = nullptr;           // packed binds: node, then status
+    int32_t* h_out = nullptr;           // pinned mirror of d_out
     int64_t out_cap = 0;
-    std::vector<int32_t> h_out;
     hipEvent_t ev[2] = {nullptr, nullptr};
     std::string errmsg;
 };
@@ -773,6 +779,7 @@ void ks_group_destroy(ks_group* g) {
     if (g->d_seg) (void)hipFree(g->d_seg);
     if (g->h_seg) (void)hipHostFree(g->h_seg);
     if (g->d_out) (void)hipFree(g->d_out);
+    if (g->h_out) (void)hipHostFree(g->h_out);
     for (auto ev : g->ev) if (ev) (void)hipEventDestroy(ev);
     if (g->st) (void)hipStreamDestroy(g->st);
     delete g;
@@ -818,7 +825,7 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
     if (hipSetDevice(g->device) != hipSuccess) return KS_EDEVICE;
     std::vector<int64_t> p_hi(S, 0), t_end(S, 0);
     std::vector<char> live(S, 0);
-    int mode = ks::kEvalTiny, blk_n = 0, B = g->engs[0]->B;
+    int mode = ks::kEvalMicro, blk_n = 0, B = g->engs[0]->B;
     int64_t blocks = 0;
     for (int i = 0; i < S; i++) {
         ks_engine* e = g->engs[i];
@@ -894,26 +901,43 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
     }
     if (total > g->out_cap) {
         if (g->d_out) (void)hipFree(g->d_out);
-        g->d_out = nullptr;
+        if (g->h_out) (void)hipHostFree(g->h_out);
+        g->d_out = g->h_out = nullptr;
         g->out_cap = std::max<int64_t>(total, 2 * g->out_cap);
-        if (!dev(hipMalloc(&g->d_out, sizeof(int32_t) * 2 * g->out_cap))) return KS_EDEVICE;
+        if (!dev(hipMalloc(&g->d_out, sizeof(int32_t) * 2 * g->out_cap)) ||
+            !dev(hipHostMalloc(&g->h_out, sizeof(int32_t) * 2 * g->out_cap, hipHostMallocDefault))) {
+            g->out_cap = 0;
+            return KS_EDEVICE;
+        }
     }
-    g->h_out.resize(2 * std::max<int64_t>(total, 1));
     if (total) {
         if (!dev(hipMemcpyAsync(g->d_seg, g->h_seg, sizeof(ks::BindSeg) * S, hipMemcpyHostToDevice, st)) ||
             !dev(ks::launch_gather_binds(g->d_seg, S, max_n, g->d_out, g->d_out + total, st)) ||
-            !dev(hipMemcpyAsync(g->h_out.data(), g->d_out, sizeof(int32_t) * 2 * total, hipMemcpyDeviceToHost, st)))
+            !dev(hipMemcpyAsync(g->h_out, g->d_out, sizeof(int32_t) * 2 * total, hipMemcpyDeviceToHost, st)))
             return KS_EDEVICE;
     }
     if (!dev(hipEventRecord(g->ev[1], st)) || !dev(hipStreamSynchronize(st))) return KS_EDEVICE;
     float ms = 0;
     (void)hipEventElapsedTime(&ms, g->ev[0], g->ev[1]);
-    for (int i = 0; i < S; i++) {
-        ks_engine* e = g->engs[i];
-        if (status_out[i] != KS_OK || !t_end[i]) continue;
-        const ks::BindSeg& sg = g->h_seg[i];
-        status_out[i] = step_finish(e, t_end[i], start[i], g->h_out.data() + sg.off, g->h_out.data() + total + sg.off,
-                                    out ? out + (int64_t)i * cap : nullptr, out ? cap : 0, &n_out[i]);
+    // unpack into the caller's ks_bind rows: members are independent, so large groups fill them
+    // on several host threads (this is host-memory-bound: 24 B written per bind)
+    auto finish = [&](int lo, int hi) {
+        for (int i = lo; i < hi; i++) {
+            ks_engine* e = g->engs[i];
+            if (status_out[i] != KS_OK || !t_end[i]) continue;
+            const ks::BindSeg& sg = g->h_seg[i];
+            status_out[i] = step_finish(e, t_end[i], start[i], g->h_out + sg.off, g->h_out + total + sg.off,
+                                        out ? out + (int64_t)i * cap : nullptr, out ? cap : 0, &n_out[i]);
+        }
+    };
+    const int nth = total >= (1 << 18) ? std::min<int>(S, std::clamp<int>((int)std::thread::hardware_concurrency(), 1, 8)) : 1;
+    if (nth <= 1) {
+        finish(0, S);
+    } else {
+        std::vector<std::thread> pool;
+        for (int k = 1; k < nth; k++) pool.emplace_back(finish, (int)((int64_t)S * k / nth), (int)((int64_t)S * (k + 1) / nth));
+        finish(0, (int)((int64_t)S / nth));
+        for (auto& th : pool) th.join();
     }
     if (stats) {
         *stats = ks_step_stats{};
@@ -1023,6 +1047,22 @@ ks_status ks_debug_counters(ks_engine* e, int64_t* out32) {
 
 void ks_set_profiling(ks_engine* e, int enable) {
     if (e) e->profiling = enable != 0;
+}
+
+ks_status ks_selftest(int32_t device, int32_t test, int64_t* failures) {
+    if (!failures || test != KS_SELFTEST_LR_MICRO) return KS_EINVAL;
+    *failures = -1;
+    if (hipSetDevice(device) != hipSuccess) return KS_EDEVICE;
+    unsigned long long* d = nullptr;
+    unsigned long long h = 0;
+    bool ok = hipMalloc(&d, sizeof h) == hipSuccess;
+    ok = ok && hipMemset(d, 0, sizeof h) == hipSuccess;
+    ok = ok && ks::launch_selftest_lr_micro(d, nullptr) == hipSuccess;
+    ok = ok && hipMemcpy(&h, d, sizeof h, hipMemcpyDeviceToHost) == hipSuccess;
+    if (d) (void)hipFree(d);
+    if (!ok) return KS_EDEVICE;
+    *failures = (int64_t)h;
+    return KS_OK;
 }
 
 }  // extern "C"

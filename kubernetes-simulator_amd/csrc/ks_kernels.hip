@@ -18,9 +18,10 @@
 //                list scores below every list entry.  winner = max(those).  If all L entries
 //                are touched the batch commits early and the next batch rescans.
 //
-// Every kernel that evaluates exists three times, one per evaluator (ks_device.h): kEvalTiny
-// (int32 math; capacities and Ac*Am < 2^26), kEvalNarrow (capacities < 2^29), kEvalWide
-// (64/128-bit, any capacity < 2^59).  The host picks the narrowest that holds.
+// Every kernel that evaluates exists four times, one per evaluator (ks_device.h): kEvalMicro
+// (capacities < 2^16, Ac*Am < 2^24: 24-bit multiplies, correction-free LeastRequested),
+// kEvalTiny (int32 math; capacities and Ac*Am < 2^26), kEvalNarrow (capacities < 2^29),
+// kEvalWide (64/128-bit, any capacity < 2^59).  The host picks the narrowest that holds.
 //
 // Packed key: (total + 1) << 32 | (0xFFFFFFFF - node); 0 = no candidate (NotFound).  Max key =
 // highest total, ties to the lowest node index.
@@ -32,6 +33,10 @@ constexpr int kScanWaves = 4;            // 256-thread scan workgroups, one 256-
 constexpr int kBlockNodes = kScanWaves * kWave;
 constexpr int kL = kTopL;                // candidate list length per pod
 constexpr int kMaxPG = 32;               // pods per scan workgroup (LDS list staging)
+#ifndef KS_SCAN_UNROLL
+#define KS_SCAN_UNROLL 4
+#endif
+constexpr int kScanUnroll = KS_SCAN_UNROLL;  // pods evaluated together per scan loop step
 constexpr int kResolveThreads = 1024;    // 16 waves
 constexpr int kOwnerWave0 = 3;           // waves 3..15 own the touched entries, except
 #ifndef KS_WRITER_WAVE
@@ -118,9 +123,23 @@ __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict_
     NodeV n{};
     if (node < (int64_t)a.c.nwb * kWave) n = load_node(a.s, node);
     const int np = (int)min<int64_t>(a.PG, nb - pg0);
-    for (int b = 0; b < np; ++b) {
-        const PodRec p = sload(a.pods + start + pg0 + b);  // uniform: SGPRs, scalar cache
-        const uint32_t t = eval_t<kMode>(a.c, p, n);       // branch-free; padding lanes discarded
+    const PodRec* pp = a.pods + start + pg0;
+    int b = 0;
+    // kScanUnroll pods at a time: their scalar loads share one wait and the independent
+    // evaluations interleave (instruction-level parallelism within the wave)
+    for (; b + kScanUnroll <= np; b += kScanUnroll) {
+        PodRec p[kScanUnroll];
+#pragma unroll
+        for (int u = 0; u < kScanUnroll; ++u) p[u] = sload(pp + b + u);  // uniform: SGPRs, scalar cache
+#pragma unroll
+        for (int u = 0; u < kScanUnroll; ++u) {
+            const uint32_t t = eval_t<kMode>(a.c, p[u], n);  // branch-free; padding lanes discarded
+            kv[(b + u) * kBlockNodes + threadIdx.x] = valid ? t : 0u;
+        }
+    }
+    for (; b < np; ++b) {
+        const PodRec p = sload(pp + b);
+        const uint32_t t = eval_t<kMode>(a.c, p, n);
         kv[b * kBlockNodes + threadIdx.x] = valid ? t : 0u;
     }
     __syncthreads();
@@ -182,9 +201,18 @@ __global__ __launch_bounds__(256) void merge_kernel(const EngineArgs* __restrict
     for (int k = 0; k < kL; ++k) top[k] = 0;
     const uint64_t* lists = src + (int64_t)b * pod_stride;
     for (int blk = tid; blk < nl; blk += 256) {
+        // the whole list in one round trip (four 16-byte loads), then the insertions
+        const ulonglong2* lp = reinterpret_cast<const ulonglong2*>(lists + (int64_t)blk * list_stride);
+        uint64_t lv[kL];
+#pragma unroll
+        for (int k = 0; k < kL / 2; ++k) {
+            const ulonglong2 w = lp[k];
+            lv[2 * k] = w.x;
+            lv[2 * k + 1] = w.y;
+        }
 #pragma unroll
         for (int k = 0; k < kL; ++k) {
-            uint64_t v = lists[(int64_t)blk * list_stride + k];
+            uint64_t v = lv[k];
             if (v <= top[kL - 1]) break;  // block lists are sorted: nothing further can enter
 #pragma unroll
             for (int s = 0; s < kL; ++s) {
@@ -993,6 +1021,7 @@ hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int
         const dim3 g(blk_n, (B + PG - 1) / PG, S);
         const size_t lds = sizeof(uint32_t) * kBlockNodes * PG;
         switch (mode) {
+            case kEvalMicro: hipLaunchKernelGGL(scan_kernel<kEvalMicro>, g, dim3(kBlockNodes), lds, st, d); break;
             case kEvalTiny: hipLaunchKernelGGL(scan_kernel<kEvalTiny>, g, dim3(kBlockNodes), lds, st, d); break;
             case kEvalNarrow: hipLaunchKernelGGL(scan_kernel<kEvalNarrow>, g, dim3(kBlockNodes), lds, st, d); break;
             default: hipLaunchKernelGGL(scan_kernel<kEvalWide>, g, dim3(kBlockNodes), lds, st, d); break;
@@ -1013,6 +1042,7 @@ hipError_t launch_merge(const EngineArgs* d, int S, int B, const uint64_t* lists
 
 hipError_t launch_resolve(const EngineArgs* d, int S, int mode, hipStream_t st) {
     switch (mode) {
+        case kEvalMicro: hipLaunchKernelGGL(resolve_kernel<kEvalMicro>, dim3(S), dim3(kResolveThreads), 0, st, d); break;
         case kEvalTiny: hipLaunchKernelGGL(resolve_kernel<kEvalTiny>, dim3(S), dim3(kResolveThreads), 0, st, d); break;
         case kEvalNarrow: hipLaunchKernelGGL(resolve_kernel<kEvalNarrow>, dim3(S), dim3(kResolveThreads), 0, st, d); break;
         default: hipLaunchKernelGGL(resolve_kernel<kEvalWide>, dim3(S), dim3(kResolveThreads), 0, st, d); break;
@@ -1047,10 +1077,30 @@ hipError_t launch_eval_pod(const Cfg& c, const NodeSoA& s, const PodRec* pod, ui
                            int64_t* score, int mode, hipStream_t st) {
     const dim3 g((c.n_nodes + 255) / 256);
     switch (mode) {
+        case kEvalMicro: hipLaunchKernelGGL(eval_pod_kernel<kEvalMicro>, g, dim3(256), 0, st, c, s, pod, filters, mask, score); break;
         case kEvalTiny: hipLaunchKernelGGL(eval_pod_kernel<kEvalTiny>, g, dim3(256), 0, st, c, s, pod, filters, mask, score); break;
         case kEvalNarrow: hipLaunchKernelGGL(eval_pod_kernel<kEvalNarrow>, g, dim3(256), 0, st, c, s, pod, filters, mask, score); break;
         default: hipLaunchKernelGGL(eval_pod_kernel<kEvalWide>, g, dim3(256), 0, st, c, s, pod, filters, mask, score); break;
     }
+    return hipGetLastError();
+}
+
+// Self-test of the micro evaluator's correction-free LeastRequested floor: every (x, A) pair with
+// 0 <= x <= A < 2^16 against the exact integer floor (one thread per A).
+__global__ __launch_bounds__(256) void selftest_lr_micro_kernel(unsigned long long* bad) {
+    const int32_t A = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x) + 1;
+    if (A >= kMicroCap) return;
+    const float r = 10.f * rcp_est((float)A);
+    unsigned long long nbad = 0;
+    for (int32_t x = 0; x <= A; ++x) {
+        const int64_t q = lr10_micro(x, r), y = 10ll * x;
+        nbad += (q * A <= y && y < (q + 1) * A) ? 0ull : 1ull;
+    }
+    if (nbad) atomicAdd(bad, nbad);
+}
+
+hipError_t launch_selftest_lr_micro(unsigned long long* bad, hipStream_t st) {
+    hipLaunchKernelGGL(selftest_lr_micro_kernel, dim3((unsigned)((kMicroCap + 255) / 256)), dim3(256), 0, st, bad);
     return hipGetLastError();
 }
 

@@ -19,6 +19,9 @@ KS_POD_OK, KS_POD_OVER_CAPACITY = 0, 1
 KS_PODFLAG_BAD_KEY, KS_PODFLAG_BAD_SPEC = 1, 2
 KS_ABI_VERSION = 1
 KS_ENGINE_FORCE_WIDE = 1
+KS_ENGINE_NO_TINY = 2
+KS_ENGINE_NO_MICRO = 4
+KS_SELFTEST_LR_MICRO = 0
 
 STATUS_NAMES = {KS_OK: "OK", KS_EINVAL: "InvalidArgument", KS_ENOTFOUND: "NotFound",
                 KS_EDEVICE: "DeviceError", KS_ENOMEM: "OutOfMemory", KS_ERANGE: "OutOfDomain"}
@@ -26,7 +29,7 @@ STATUS_NAMES = {KS_OK: "OK", KS_EINVAL: "InvalidArgument", KS_ENOTFOUND: "NotFou
 # every symbol include/*.h declares
 EXPORTED_SYMBOLS = ("ks_create", "ks_destroy", "ks_load_nodes", "ks_submit_pods", "ks_step",
                     "ks_filter", "ks_score", "ks_usage", "ks_current_tick", "ks_queued_pods",
-                    "ks_last_error", "ks_last_step_stats", "ks_set_profiling", "ks_debug_counters",
+                    "ks_last_error", "ks_last_step_stats", "ks_set_profiling", "ks_debug_counters", "ks_selftest",
                     "ks_comm_unique_id", "ks_shard", "ks_group_create", "ks_group_destroy",
                     "ks_group_add", "ks_group_size", "ks_group_step", "ks_pod_status",
                     # include/ks_ingest.h
@@ -100,6 +103,8 @@ def load():
     L.ks_debug_counters.restype = C.c_int
     L.ks_set_profiling.argtypes = [p, C.c_int]
     L.ks_set_profiling.restype = None
+    L.ks_selftest.argtypes = [C.c_int32, C.c_int32, p]
+    L.ks_selftest.restype = C.c_int
     L.ks_comm_unique_id.argtypes = [p]
     L.ks_comm_unique_id.restype = C.c_int
     L.ks_shard.argtypes = [p, C.c_int32, C.c_int32, p, C.c_int32]

@@ -194,6 +194,16 @@ def engine_for_trace(trace, enc, **cfg):
     return eng
 
 
+def selftest(test: int = _lib.KS_SELFTEST_LR_MICRO, device: int = 0) -> int:
+    """Run a device self-test (include/ks_engine.h, ks_selftest); returns the failure count."""
+    L = _lib.load()
+    n = C.c_int64(-1)
+    rc = L.ks_selftest(device, test, C.byref(n))
+    if rc != 0:
+        raise KsError(rc, "ks_selftest failed")
+    return n.value
+
+
 def comm_unique_id() -> bytes:
     """A fresh RCCL communicator id for :meth:`Engine.shard` (create on rank 0 only)."""
     L = _lib.load()

@@ -53,14 +53,53 @@ def test_c1_kat():
         np.testing.assert_array_equal(eng.usage(), np.array(kat["usage"][t - 1], dtype=np.int64))
 
 
-@pytest.mark.parametrize("wide", [0, 1, 2])
+@pytest.mark.parametrize("wide", [0, 1, 2, 4])
 @pytest.mark.parametrize("mode", sorted(MODES))
 @pytest.mark.parametrize("seed", [1, 2])
 def test_lockstep_small(mode, seed, wide):
-    """Every evaluator variant against the oracle: 0 = engine's choice (tiny int32 for these
-    capacities), 1 = forced 64/128-bit, 2 = no tiny (narrow 32x32->64)."""
+    """Every evaluator variant against the oracle: 0 = engine's choice (micro 24-bit for these
+    capacities), 1 = forced 64/128-bit, 2 = no tiny (narrow 32x32->64), 4 = no micro (tiny)."""
     tr = small_trace(seed, n_nodes=400, n_pods=300, arrival="stream")
     _lockstep(tr, mode, 400, engine_flags=wide)
+
+
+def test_micro_lr_floor_selftest():
+    """The micro evaluator's correction-free LeastRequested floor, every (x, A) pair with
+    0 <= x <= A < 2^16, on the device (ks_selftest)."""
+    from kubesim_amd.engine import selftest
+    assert selftest() == 0
+
+
+def test_micro_capacity_sweep_scores_match_oracle():
+    """Every cpu capacity 1..65535 milli-units (the whole micro domain) with memory 1..255 MiB
+    (Ac * Am up to the 2^24 edge): filter and score of pods with small and large requests match
+    the oracle node for node."""
+    n = 65535
+    tr = small_trace(47, n_nodes=n, n_pods=24, taints=False, labels=False, tolerations=False, selectors=False)
+    nd, p = tr["nodes"], tr["pods"]
+    nd["alloc"][:, 0] = np.arange(1, n + 1)
+    nd["alloc"][:, 1] = ((np.arange(n) * 7919) % 255 + 1) << 20
+    nd["alloc"][:, 3] = 110
+    nd["alloc_has"][:] |= 11  # cpu, memory, pods
+    req_c = [0, 1, 2, 3, 5, 7, 10, 64, 99, 100, 255, 1000, 4095, 4096, 9999, 32767, 32768, 65534, 65535,
+             70000, 1, 500, 12345, 60000]
+    p["req"][:, 0] = req_c[: p["m"]]
+    p["req"][:, 1] = (np.arange(p["m"]) * 37 % 256) << 20
+    p["req_has"][:] |= 3
+    mode = "feeds_all_lrba"
+    enc = encoded(tr)
+    eng = make_engine(tr, enc, mode)
+    eng.submit(enc["pods"])
+    ora = make_oracle(tr, mode)
+    ora.submit(tr)
+    for pod in range(p["m"]):
+        feas, score = ora.eval(pod)
+        np.testing.assert_array_equal(eng.filter(pod), feas)
+        np.testing.assert_array_equal(eng.score(pod), score, err_msg=f"pod {pod}")
+    eb, erc = engine_run(eng, p["m"], p["m"])
+    ob, orc = oracle_run(ora, p["m"])
+    assert erc == orc
+    assert_same_binds(eb, ob)
 
 
 def test_narrow_capacities_use_narrow_evaluator():
