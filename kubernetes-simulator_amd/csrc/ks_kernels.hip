@@ -693,6 +693,13 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(const EngineAr
     }
     __syncthreads();
     KS_STAMP(g5);
+#if !KS_KEEP_IDLE_OWNERS
+    // The table grows by at most one entry per pod, so owner waves whose first entry lies past
+    // n_t + nb can never own one: they end here.  s_barrier waits only for the surviving waves of
+    // the workgroup (CDNA ISA, S_BARRIER), and their threads have no share in the write-back
+    // (tid >= 64 * (oslot + 3) > n_t + nb >= the final table size).
+    if (oslot >= 0 && oslot * kWave >= sh.n_t + nb) return;
+#endif
 
 #ifdef KS_STAMPS
     uint64_t acc_work = 0, acc_wait = 0, acc_sub[8] = {0, 0, 0, 0, 0, 0, 0, 0}, acc_cnt[4] = {0, 0, 0, 0};
