@@ -496,6 +496,15 @@ __device__ __forceinline__ T sload(const T* p) {
     return v;
 }
 
+// The same pointer in the global address space: global_load / global_store instead of flat_.
+// A flat access is counted in lgkmcnt as well as vmcnt, so the s_waitcnt lgkmcnt(0) that every
+// LDS wait and every __syncthreads() carries would also wait for it — an HBM round trip on the
+// resolver's per-pod barrier.  A global access is counted in vmcnt only.
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gptr(T* p) {
+    return (__attribute__((address_space(1))) T*)p;
+}
+
 __host__ __device__ __forceinline__ uint64_t make_key(uint32_t total1, uint32_t node) {
     return total1 ? (((uint64_t)total1 << 32) | (uint64_t)(0xFFFFFFFFu - node)) : 0ull;
 }

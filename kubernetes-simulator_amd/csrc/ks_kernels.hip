@@ -445,7 +445,7 @@ __device__ __forceinline__ NodeV stage_node(const ResolveShared& sh, int b) {
 
 // field f (0..9, NodeV order) of node i: the SoA is one allocation with a fixed field stride
 __device__ __forceinline__ int64_t node_field(const NodeSoA& s, int f, int64_t i) {
-    return s.ac[(int64_t)f * (s.am - s.ac) + i];
+    return gptr(s.ac)[(int64_t)f * (s.am - s.ac) + i];
 }
 
 __device__ __forceinline__ int32_t key_node(uint64_t key) { return (int32_t)(0xFFFFFFFFu - (uint32_t)key); }
@@ -546,7 +546,7 @@ __device__ __forceinline__ void expire_on(const ResolveShared& sh, int e0, int e
             hit = q == j ? ok : (sh.ex_entry[x] == t && sh.ex_ok[x] != 0);
             r0 = sh.ex_req[x][0]; r1 = sh.ex_req[x][1]; r2 = sh.ex_req[x][2];
         }
-        if (hit && expired) expired[q] = 1;
+        if (hit && expired) gptr(expired)[q] = 1;
         uint64_t m = __ballot(hit);
         while (m) {
             const int l = __ffsll((unsigned long long)m) - 1;
@@ -834,8 +834,8 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(const EngineAr
                 sh.dirty[t] = i + 1;
                 const int slot = pci.exp_slot;
                 if (slot >= 0) { sh.ex_entry[slot] = t; sh.ex_ok[slot] = ok ? 1 : 0; }
-                a.b_node[j] = nd;
-                a.b_status[j] = ok ? 0 : 1;
+                gptr(a.b_node)[j] = nd;
+                gptr(a.b_status)[j] = ok ? 0 : 1;
             }
         } else if (wave == 2) {
             if (has_next && e1 > e0 && !(KS_ABL & 4)) {
@@ -856,7 +856,7 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(const EngineAr
                             atomicAdd((unsigned long long*)&sh.ts[6][tq], (unsigned long long)-r2);
                             atomicAdd((unsigned long long*)&sh.ts[7][tq], (unsigned long long)-1ll);
                             sh.dirty[tq] = i + 1;
-                            a.expired[q] = 1;
+                            gptr(a.expired)[q] = 1;
                         }
                     }
                 }

@@ -33,10 +33,18 @@ d = c1 - c0
 D = d[16:]
 pods = D[4]
 print(f"B={B} pods={st['pods']} wall {dt*1e3:.1f} ms  -> {32768/dt:.0f} pods/s")
-for k, name in ((0, "wave0 work"), (1, "wave0 wait"), (2, "owner0 work"), (3, "owner0 wait"),
-                (5, "owner0 top"), (6, "bind+expiry"), (7, "eval+fold"), (8, "walk commit"), (9, "walk issue")):
+# layout (ks_kernels.hip, KS_STAMPS): D = ctr[16..31]; D[0]/D[1] wave 0 work / barrier wait,
+# D[2] wave 1 work, D[3] wave 2 work, D[15] wave 3 (first owner) work; D[5..8] wave 3 segments
+# (top, load, exclusion, eval); D[11..14] wave 1 segments (fetch+fit, expiries, -, eval);
+# ctr[5..7] wave 0 segments (insert, commit, issue); D[9] owner lanes past the prune, D[10] owner
+# waves evaluating
+for k, name in ((0, "w0 work"), (1, "w0 wait"), (2, "w1 work"), (3, "w2 work"), (15, "w3 work"),
+                (5, "w3 top"), (6, "w3 load"), (7, "w3 excl"), (8, "w3 eval"),
+                (11, "w1 fetch+fit"), (12, "w1 expiries"), (14, "w1 eval")):
     print(f"  {name:12s} {D[k]/max(pods,1):9.0f} cycles/pod")
-for k, name in ((10, "owner0 evals"), (11, "exact fallbk")):
+for k, name in ((5, "w0 insert"), (6, "w0 commit"), (7, "w0 issue")):
+    print(f"  {name:12s} {d[k]/max(pods,1):9.0f} cycles/pod")
+for k, name in ((9, "owner lanes"), (10, "owner waves")):
     print(f"  {name:12s} {D[k]/max(pods,1):9.2f} per pod")
 L = max(d[14] or st["launches"], 1)
 print(f"  launches {d[14]}  pods/launch {pods / L:.1f}  expiries/launch {d[15] / L:.1f}")
