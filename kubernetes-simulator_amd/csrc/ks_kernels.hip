@@ -173,15 +173,14 @@ __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict_
 }
 
 // ------------------------------------------------------------------------------------------
-// merge: grid (B, S), one 256-thread workgroup per pod; exact top-L over nl sorted lists (the
-// scan's block lists of one shard, or the shards' all-gathered lists).  src == nullptr: the
-// scenario's own block lists into its candidate lists.
+// merge: grid (B, S), one workgroup per pod (256 threads, or 1024 for more than 1024 lists);
+// exact top-L over nl sorted lists (the scan's block lists of one shard, or the shards'
+// all-gathered lists).  src == nullptr: the scenario's own block lists into its candidate lists.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void merge_kernel(const EngineArgs* __restrict__ A, const uint64_t* src,
-                                                     int64_t pod_stride, int32_t nl, int64_t list_stride,
-                                                     uint64_t* out) {
-    __shared__ uint64_t red[4];
-    __shared__ int32_t owner[4];
+constexpr int kMergeMaxWaves = 16;
+__global__ __launch_bounds__(1024) void merge_kernel(const EngineArgs* __restrict__ A, const uint64_t* src,
+                                                      int64_t pod_stride, int32_t nl, int64_t list_stride,
+                                                      uint64_t* out) {
     const EngineArgs a = A[blockIdx.y];
     if (src == nullptr) {
         src = a.lists;
@@ -200,7 +199,8 @@ __global__ __launch_bounds__(256) void merge_kernel(const EngineArgs* __restrict
 #pragma unroll
     for (int k = 0; k < kL; ++k) top[k] = 0;
     const uint64_t* lists = src + (int64_t)b * pod_stride;
-    for (int blk = tid; blk < nl; blk += 256) {
+    const int nthr = blockDim.x, nwav = nthr / kWave;
+    for (int blk = tid; blk < nl; blk += nthr) {
         // the whole list in one round trip (four 16-byte loads), then the insertions
         const ulonglong2* lp = reinterpret_cast<const ulonglong2*>(lists + (int64_t)blk * list_stride);
         uint64_t lv[kL];
@@ -223,7 +223,9 @@ __global__ __launch_bounds__(256) void merge_kernel(const EngineArgs* __restrict
             }
         }
     }
-    // L rounds: the workgroup max of the thread heads; its owner advances
+    // each wave: L rounds of its max thread head (the owner advances), no barrier; then wave 0
+    // merges the wave lists (<= 128 candidates, two per lane) the same way
+    __shared__ uint64_t wl[kMergeMaxWaves][kL];
     int head = 0;
     for (int r = 0; r < kL; ++r) {
         uint64_t h = 0;
@@ -231,19 +233,22 @@ __global__ __launch_bounds__(256) void merge_kernel(const EngineArgs* __restrict
         for (int k = 0; k < kL; ++k) h = (k == head) ? top[k] : h;
         const uint64_t m = wave_max_u64(h);
         const uint64_t hit = __ballot(h == m && m != 0);
-        if (lane == 0) {
-            red[wave] = m;
-            owner[wave] = hit ? wave * 64 + __ffsll((unsigned long long)hit) - 1 : -1;
-        }
-        __syncthreads();
-        uint64_t best = 0;
-        int who = -1;
+        if (lane == 0) wl[wave][r] = m;
+        if (hit && lane == __ffsll((unsigned long long)hit) - 1) head++;
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    const int nc = nwav * kL;  // candidates: lane l holds c[l] and c[l + 64]
+    uint64_t v0 = lane < nc ? wl[lane / kL][lane % kL] : 0ull;
+    uint64_t v1 = lane + kWave < nc ? wl[(lane + kWave) / kL][(lane + kWave) % kL] : 0ull;
 #pragma unroll
-        for (int w = 0; w < 4; ++w)
-            if (red[w] > best) { best = red[w]; who = owner[w]; }
-        if (tid == 0) out[(int64_t)b * kL + r] = best;
-        if (tid == who) head++;
-        __syncthreads();
+    for (int r = 0; r < kL; ++r) {
+        const uint64_t m = wave_max_u64(v0 > v1 ? v0 : v1);
+        if (lane == 0) out[(int64_t)b * kL + r] = m;
+        if (m == 0) continue;
+        const uint64_t h0 = __ballot(v0 == m), h1 = __ballot(v1 == m);  // keys are distinct
+        if (h0 && lane == __ffsll((unsigned long long)h0) - 1) v0 = 0;
+        if (!h0 && h1 && lane == __ffsll((unsigned long long)h1) - 1) v1 = 0;
     }
 }
 
@@ -1043,7 +1048,8 @@ hipError_t launch_merge(const EngineArgs* d, int S, int B, const uint64_t* lists
         hipLaunchKernelGGL(merge_small_kernel, dim3((B + 3) / 4, S), dim3(256), 0, st, d, lists, pod_stride, nl,
                            list_stride, out);
     else
-        hipLaunchKernelGGL(merge_kernel, dim3(B, S), dim3(256), 0, st, d, lists, pod_stride, nl, list_stride, out);
+        hipLaunchKernelGGL(merge_kernel, dim3(B, S), dim3(nl_max > 1024 ? 1024 : 256), 0, st, d, lists, pod_stride, nl,
+                           list_stride, out);
     return hipGetLastError();
 }
 
