@@ -261,7 +261,7 @@ def main_c4(args):
     for s in range(lo, lo + per):
         tr = tracegen.c4_scenario(s, n_nodes=args.scenario_nodes, n_pods=args.scenario_pods)
         enc = encode.encode_trace(tr)
-        e = g.add(tick_seconds=tr["tick_seconds"], filter_mode=1, filters=7, scorers=scorers)
+        e = g.add(tick_seconds=tr["tick_seconds"], filter_mode=1, filters=7, scorers=scorers, batch_pods=args.batch)
         e.load_nodes(enc["alloc"], enc["taint"], enc["label"])
         e.submit(enc["pods"])
     log(f"[rank {rank}] {per} scenarios ready in {time.perf_counter() - t0:.1f}s; {S_pps} ticks per step")
