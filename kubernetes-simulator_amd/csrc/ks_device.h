@@ -570,7 +570,8 @@ int block_nodes();
 // expiries due before each scenario's batch head
 hipError_t launch_expire_head(const EngineArgs* d, int S, hipStream_t st);
 // scan of each scenario's blocks [blk_lo, blk_lo + blk_n); grid x = the largest blk_n
-hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int mode, hipStream_t st);
+// key16: every total + 1 < 2^16 (scan_kernel's 16-bit key table)
+hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int mode, bool key16, hipStream_t st);
 // per scenario and pod b < batch size: exact top-L over nl sorted lists
 // lists[b*pod_stride + k*list_stride] into out (lists == nullptr: the scenario's own block lists
 // into its candidate lists)

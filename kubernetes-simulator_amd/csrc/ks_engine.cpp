@@ -49,6 +49,9 @@ constexpr int64_t kMaxNodes = 1LL << 24;  // node ids fit the packed key; lists 
 constexpr int64_t kMaxValue = 1LL << 59;
 constexpr int kMaxBatch = 256;
 constexpr int kDefaultBatch = 256;
+#ifndef KS_PG_MIN_WG
+#define KS_PG_MIN_WG 2048  // scan workgroups to keep when raising the pods per workgroup
+#endif
 constexpr int kProfEv = 5;  // per launch: expire_head | scan | merge (+exchange) | resolve
 constexpr int64_t kNever = std::numeric_limits<int64_t>::max();
 
@@ -199,6 +202,11 @@ ks::EngineArgs make_args(ks_engine* e) {
     a.B = e->B;
     a.PG = e->PG;
     return a;
+}
+
+// every total + 1 fits the scan's 16-bit key table (weights and constant values are >= 0)
+bool key16(const ks_engine* e) {
+    return (int64_t)e->dc.const_total + 10 * ((int64_t)e->dc.w_lr + e->dc.w_ba) + 1 < (1 << 16);
 }
 
 void update_mode(ks_engine* e) {
@@ -427,7 +435,7 @@ ks_status ks_load_nodes(ks_engine* e, int64_t n, const int64_t* alloc, const uin
     // workgroups (8 per CU) per scan
     int pg = 1;
     while (pg < ks::max_pods_per_scan_wg() && pg < e->B &&
-           (int64_t)e->blk_n * ((e->B + pg * 2 - 1) / (pg * 2)) >= 2048)
+           (int64_t)e->blk_n * ((e->B + pg * 2 - 1) / (pg * 2)) >= KS_PG_MIN_WG)
         pg *= 2;
     e->PG = pg;
     HIPCHK(e, hipMalloc(&e->lists, sizeof(uint64_t) * (size_t)e->B * e->nblk * ks::kTopL));
@@ -661,7 +669,7 @@ ks_status ks_step(ks_engine* e, int64_t ticks, ks_bind* out, int64_t cap, int64_
             if (ev[0]) HIPCHK(e, hipEventRecord(ev[0], st));
             HIPCHK(e, ks::launch_expire_head(d, 1, st));
             if (ev[1]) HIPCHK(e, hipEventRecord(ev[1], st));
-            HIPCHK(e, ks::launch_scan(d, 1, e->blk_n, e->B, e->PG, e->mode, st));
+            HIPCHK(e, ks::launch_scan(d, 1, e->blk_n, e->B, e->PG, e->mode, key16(e), st));
             if (ev[2]) HIPCHK(e, hipEventRecord(ev[2], st));
             const int G = e->world * e->vsh;
             const int64_t L = ks::kTopL, BL = (int64_t)e->B * L;
@@ -827,7 +835,11 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
     std::vector<int64_t> p_hi(S, 0), t_end(S, 0);
     std::vector<char> live(S, 0);
     int mode = ks::kEvalMicro, blk_n = 0, B = 0;  // B: the largest member batch (grid size)
-    for (ks_engine* e : g->engs) B = std::max(B, e->B);
+    bool k16 = true;
+    for (ks_engine* e : g->engs) {
+        B = std::max(B, e->B);
+        k16 = k16 && key16(e);
+    }
     int64_t blocks = 0;
     for (int i = 0; i < S; i++) {
         ks_engine* e = g->engs[i];
@@ -871,7 +883,7 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
         if (nbat == 0) break;
         for (int64_t b = 0; b < nbat; b++) {
             if (!dev(ks::launch_expire_head(g->d_args, S, st)) ||
-                !dev(ks::launch_scan(g->d_args, S, blk_n, B, pg, mode, st)) ||
+                !dev(ks::launch_scan(g->d_args, S, blk_n, B, pg, mode, k16, st)) ||
                 !dev(ks::launch_merge(g->d_args, S, B, nullptr, 0, 0, 0, nullptr, blk_n, st)) ||
                 !dev(ks::launch_resolve(g->d_args, S, mode, st)))
                 return KS_EDEVICE;

@@ -105,9 +105,12 @@ __global__ __launch_bounds__(256) void expire_head_kernel(const EngineArgs* __re
 // is usually one or two "tie classes": take the max, every node at it in node order, repeat below
 // it — a lane max of 4, a 32-bit wave max and 4 ballots per class.
 // ------------------------------------------------------------------------------------------
-template <int kMode>
+// KT: the key table's word, uint16_t when every total + 1 < 2^16 (the host's check on the scorer
+// weights) — half the LDS per workgroup, so more workgroups fit a CU.
+template <int kMode, typename KT>
 __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict__ A) {
-    extern __shared__ uint32_t kv[];  // [PG][kBlockNodes]: total+1 per (pod, node of the block)
+    extern __shared__ uint32_t kv_raw[];
+    KT* const kv = reinterpret_cast<KT*>(kv_raw);  // [PG][kBlockNodes]: total+1 per (pod, node of the block)
     const EngineArgs a = A[blockIdx.z];
     if ((int)blockIdx.x >= a.blk_n) return;  // a group's scenarios may differ in size
     const int64_t start = sload(a.ctr + kCtrStart), end = sload(a.ctr + kCtrEnd);
@@ -134,19 +137,19 @@ __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict_
 #pragma unroll
         for (int u = 0; u < kScanUnroll; ++u) {
             const uint32_t t = eval_t<kMode>(a.c, p[u], n);  // branch-free; padding lanes discarded
-            kv[(b + u) * kBlockNodes + threadIdx.x] = valid ? t : 0u;
+            kv[(b + u) * kBlockNodes + threadIdx.x] = (KT)(valid ? t : 0u);
         }
     }
     for (; b < np; ++b) {
         const PodRec p = sload(pp + b);
         const uint32_t t = eval_t<kMode>(a.c, p, n);
-        kv[b * kBlockNodes + threadIdx.x] = valid ? t : 0u;
+        kv[b * kBlockNodes + threadIdx.x] = (KT)(valid ? t : 0u);
     }
     __syncthreads();
     for (int b = wave; b < np; b += kScanWaves) {
         uint32_t v[kScanWaves];
 #pragma unroll
-        for (int u = 0; u < kScanWaves; ++u) v[u] = kv[b * kBlockNodes + u * kWave + lane];  // node u*64 + lane
+        for (int u = 0; u < kScanWaves; ++u) v[u] = (uint32_t)kv[b * kBlockNodes + u * kWave + lane];  // node u*64 + lane
         uint64_t* out = a.lists + ((int64_t)(pg0 + b) * a.nblk + blk) * kL;
         int cnt = 0;
         for (int r = 0; r < kL && cnt < kL; ++r) {
@@ -1028,16 +1031,23 @@ hipError_t launch_expire_head(const EngineArgs* d, int S, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int mode, hipStream_t st) {
+template <typename KT>
+static void launch_scan_t(const EngineArgs* d, const dim3& g, size_t lds, int mode, hipStream_t st) {
+    switch (mode) {
+        case kEvalMicro: hipLaunchKernelGGL((scan_kernel<kEvalMicro, KT>), g, dim3(kBlockNodes), lds, st, d); break;
+        case kEvalTiny: hipLaunchKernelGGL((scan_kernel<kEvalTiny, KT>), g, dim3(kBlockNodes), lds, st, d); break;
+        case kEvalNarrow: hipLaunchKernelGGL((scan_kernel<kEvalNarrow, KT>), g, dim3(kBlockNodes), lds, st, d); break;
+        default: hipLaunchKernelGGL((scan_kernel<kEvalWide, KT>), g, dim3(kBlockNodes), lds, st, d); break;
+    }
+}
+
+hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int mode, bool key16, hipStream_t st) {
     if (blk_n > 0 && S > 0) {
         const dim3 g(blk_n, (B + PG - 1) / PG, S);
-        const size_t lds = sizeof(uint32_t) * kBlockNodes * PG;
-        switch (mode) {
-            case kEvalMicro: hipLaunchKernelGGL(scan_kernel<kEvalMicro>, g, dim3(kBlockNodes), lds, st, d); break;
-            case kEvalTiny: hipLaunchKernelGGL(scan_kernel<kEvalTiny>, g, dim3(kBlockNodes), lds, st, d); break;
-            case kEvalNarrow: hipLaunchKernelGGL(scan_kernel<kEvalNarrow>, g, dim3(kBlockNodes), lds, st, d); break;
-            default: hipLaunchKernelGGL(scan_kernel<kEvalWide>, g, dim3(kBlockNodes), lds, st, d); break;
-        }
+        if (key16)
+            launch_scan_t<uint16_t>(d, g, sizeof(uint16_t) * kBlockNodes * PG, mode, st);
+        else
+            launch_scan_t<uint32_t>(d, g, sizeof(uint32_t) * kBlockNodes * PG, mode, st);
     }
     return hipGetLastError();
 }
