@@ -578,7 +578,11 @@ hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int
 // nl_max: the largest nl of the launch (<= 64 / L candidates per pod: one wave per pod)
 hipError_t launch_merge(const EngineArgs* d, int S, int B, const uint64_t* lists, int64_t pod_stride, int32_t nl,
                         int64_t list_stride, uint64_t* out, int nl_max, hipStream_t st);
-hipError_t launch_resolve(const EngineArgs* d, int S, int mode, hipStream_t st);
+// small: the RSmall resolver (batches <= small_resolver_max_batch() pods, clusters <=
+// small_resolver_max_nodes() nodes; half the LDS, two resolvers per CU)
+hipError_t launch_resolve(const EngineArgs* d, int S, int mode, bool small, hipStream_t st);
+int small_resolver_max_batch();
+int small_resolver_max_nodes();
 struct BindSeg {
     const int32_t* node;
     const int32_t* status;

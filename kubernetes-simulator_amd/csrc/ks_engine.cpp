@@ -209,6 +209,11 @@ bool key16(const ks_engine* e) {
     return (int64_t)e->dc.const_total + 10 * ((int64_t)e->dc.w_lr + e->dc.w_ba) + 1 < (1 << 16);
 }
 
+// the half-size resolver holds this engine's batches (ks_kernels.hip, RSmall)
+bool small_resolver(const ks_engine* e) {
+    return e->B <= ks::small_resolver_max_batch() && e->dc.n_nodes <= ks::small_resolver_max_nodes();
+}
+
 void update_mode(ks_engine* e) {
     int64_t m[3];
     for (int k = 0; k < 3; k++) m[k] = e->max_alloc[k] / e->scale[k];
@@ -690,7 +695,7 @@ ks_status ks_step(ks_engine* e, int64_t ticks, ks_bind* out, int64_t cap, int64_
                 HIPCHK(e, ks::launch_merge(d, 1, e->B, e->cand_all, L, G, BL, e->cand, G, st));
             }
             if (ev[3]) HIPCHK(e, hipEventRecord(ev[3], st));
-            HIPCHK(e, ks::launch_resolve(d, 1, e->mode, st));
+            HIPCHK(e, ks::launch_resolve(d, 1, e->mode, small_resolver(e), st));
             if (ev[4]) HIPCHK(e, hipEventRecord(ev[4], st));
             launches++;
         }
@@ -835,10 +840,11 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
     std::vector<int64_t> p_hi(S, 0), t_end(S, 0);
     std::vector<char> live(S, 0);
     int mode = ks::kEvalMicro, blk_n = 0, B = 0;  // B: the largest member batch (grid size)
-    bool k16 = true;
+    bool k16 = true, small = true;
     for (ks_engine* e : g->engs) {
         B = std::max(B, e->B);
         k16 = k16 && key16(e);
+        small = small && small_resolver(e);
     }
     int64_t blocks = 0;
     for (int i = 0; i < S; i++) {
@@ -885,7 +891,7 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
             if (!dev(ks::launch_expire_head(g->d_args, S, st)) ||
                 !dev(ks::launch_scan(g->d_args, S, blk_n, B, pg, mode, k16, st)) ||
                 !dev(ks::launch_merge(g->d_args, S, B, nullptr, 0, 0, 0, nullptr, blk_n, st)) ||
-                !dev(ks::launch_resolve(g->d_args, S, mode, st)))
+                !dev(ks::launch_resolve(g->d_args, S, mode, small, st)))
                 return KS_EDEVICE;
             launches++;
         }

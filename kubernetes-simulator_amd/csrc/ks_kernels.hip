@@ -46,15 +46,29 @@ constexpr int kOwnerWave0 = 3;           // waves 3..15 own the touched entries,
 #define KS_PRIO 0
 #endif
 constexpr int kWriterWave = KS_WRITER_WAVE;  // the bind's bookkeeping writer (off the critical path)
-constexpr int kOwnerWaves = kResolveThreads / kWave - kOwnerWave0 - 1;
-constexpr int kOwners = kOwnerWaves * kWave;
-constexpr int kTMax = 768;               // touched-node table (LDS); <= kOwners
-constexpr int kHash = 2048;              // open-addressing node -> entry map (LDS)
-constexpr int kMaxBatchR = 256;          // pods per resolve launch
-constexpr int kMaxExp = kTMax - kMaxBatchR;  // expiries pre-inserted per batch
-constexpr int kFilterBits = 1 << 16;     // touched filter indexed by node & 0xFFFF (no false
-                                         // negatives; exact below 65,536 nodes)
-static_assert(kTMax <= kOwners, "one touched entry per owner thread");
+// Resolver size classes (the LDS footprint): touched-node table entries, open-addressing node ->
+// entry map slots (log2), pods per launch, touched filter bits (log2; the filter is exact — no
+// hash confirmation — for clusters of at most that many nodes).  RBig: any cluster, 256-pod
+// batches, 1024 threads, ~150 KB of LDS (one workgroup per CU).  RSmall: batches of <= 128 pods
+// of clusters of <= 8,192 nodes (what-if scenarios), 512 threads (4 owner waves), ~56 KB, so two
+// resolvers share a CU (registers: 2 x 8 waves of <= 128 VGPRs).
+template <int THREADS, int TMAX, int HASH_LOG2, int MAXB, int FBITS_LOG2>
+struct RCfg {
+    static constexpr int kThreads = THREADS;
+    static constexpr int kTMax = TMAX;
+    static constexpr int kHashLog2 = HASH_LOG2;
+    static constexpr int kHash = 1 << HASH_LOG2;
+    static constexpr int kMaxBatchR = MAXB;
+    static constexpr int kMaxExp = TMAX - MAXB;  // expiries pre-inserted per batch
+    static constexpr int kFilterBits = 1 << FBITS_LOG2;
+    static_assert(kWriterWave < THREADS / kWave, "the writer wave exists");
+    static_assert(TMAX <= (THREADS / kWave - kOwnerWave0 - 1) * kWave, "one touched entry per owner thread");
+    static_assert(TMAX - MAXB <= THREADS, "one thread per pre-inserted expiry");
+};
+using RBig = RCfg<kResolveThreads, 768, 11, 256, 16>;
+using RSmall = RCfg<512, 256, 10, 128, 13>;
+constexpr int kMaxBatchR = RBig::kMaxBatchR;
+constexpr int kSmallMaxNodes = RSmall::kFilterBits;
 
 enum : int64_t { kCtrStart = 0, kCtrEnd = 1, kCtrErr = 2, kCtrErrPod = 3, kCtrEarly = 4 };
 enum : uint32_t { kFlagBadKey = 1, kFlagBadSpec = 2 };
@@ -336,7 +350,11 @@ struct alignas(16) PodCtl {
     int32_t pad[3];
 };
 
+template <class C>
 struct ResolveShared {
+    using Cfg = C;
+    static constexpr int kTMax = C::kTMax, kHash = C::kHash, kMaxBatchR = C::kMaxBatchR, kMaxExp = C::kMaxExp,
+                         kFilterBits = C::kFilterBits;
     int64_t ts[8][kTMax];       // touched-node state: ac am ag ap rc rm rg nr
     uint64_t tu[2][kTMax];      // taint label
     int32_t tnode[kTMax];
@@ -359,7 +377,7 @@ struct ResolveShared {
 };
 
 constexpr int kEntUntouched = 1023;
-static_assert(kTMax < kEntUntouched, "entry index fits 10 bits");
+static_assert(RBig::kTMax < kEntUntouched, "entry index fits 10 bits");
 
 __device__ __forceinline__ uint64_t ikey(uint64_t key, int ent) {
     const uint32_t node = 0xFFFFFFFFu - (uint32_t)key;
@@ -392,11 +410,16 @@ __device__ __forceinline__ uint64_t stamp() {
 #define KS_STAMP(var)
 #endif
 
-__device__ __forceinline__ uint32_t hslot(int32_t node) { return ((uint32_t)node * 2654435761u) >> (32 - 11); }
+template <class SH>
+__device__ __forceinline__ uint32_t hslot(int32_t node) {
+    return ((uint32_t)node * 2654435761u) >> (32 - SH::Cfg::kHashLog2);
+}
 
 // entry index of `node` in the touched table, or -1
-__device__ __forceinline__ int h_find(const ResolveShared& sh, int32_t node) {
-    uint32_t s = hslot(node);
+template <class SH>
+__device__ __forceinline__ int h_find(const SH& sh, int32_t node) {
+    constexpr int kHash = SH::kHash;
+    uint32_t s = hslot<SH>(node);
     for (int i = 0; i < kHash; ++i) {
         const int32_t k = sh.hkey[s];
         if (k == node) return sh.hval[s];
@@ -407,8 +430,10 @@ __device__ __forceinline__ int h_find(const ResolveShared& sh, int32_t node) {
 }
 
 // single-lane insert of a node known to be absent
-__device__ __forceinline__ void h_insert(ResolveShared& sh, int32_t node, int32_t idx) {
-    uint32_t s = hslot(node);
+template <class SH>
+__device__ __forceinline__ void h_insert(SH& sh, int32_t node, int32_t idx) {
+    constexpr int kHash = SH::kHash, kFilterBits = SH::kFilterBits;
+    uint32_t s = hslot<SH>(node);
     while (sh.hkey[s] != -1) s = (s + 1) & (kHash - 1);
     sh.hkey[s] = node;
     sh.hval[s] = idx;
@@ -418,7 +443,9 @@ __device__ __forceinline__ void h_insert(ResolveShared& sh, int32_t node, int32_
 
 // touched? — one LDS read; the filter is exact (node & 0xFFFF is injective) when the cluster has
 // at most kFilterBits nodes, otherwise a set bit is confirmed in the hash
-__device__ __forceinline__ bool is_touched(const ResolveShared& sh, int32_t node, bool exact) {
+template <class SH>
+__device__ __forceinline__ bool is_touched(const SH& sh, int32_t node, bool exact) {
+    constexpr int kFilterBits = SH::kFilterBits;
     const uint32_t f = (uint32_t)node & (kFilterBits - 1);
     if (!((sh.tfilt[f >> 5] >> (f & 31)) & 1u)) return false;
     return exact || h_find(sh, node) >= 0;
@@ -426,7 +453,9 @@ __device__ __forceinline__ bool is_touched(const ResolveShared& sh, int32_t node
 
 // table insert of an in-loop winner: with an exact filter only the filter bit (the hash is
 // consulted only by the batch-start pre-insert and by inexact filters)
-__device__ __forceinline__ void t_insert(ResolveShared& sh, int32_t node, int32_t idx, bool exact) {
+template <class SH>
+__device__ __forceinline__ void t_insert(SH& sh, int32_t node, int32_t idx, bool exact) {
+    constexpr int kFilterBits = SH::kFilterBits;
     if (exact) {
         const uint32_t f = (uint32_t)node & (kFilterBits - 1);
         atomicOr(&sh.tfilt[f >> 5], 1u << (f & 31));
@@ -435,7 +464,8 @@ __device__ __forceinline__ void t_insert(ResolveShared& sh, int32_t node, int32_
     }
 }
 
-__device__ __forceinline__ NodeV t_node(const ResolveShared& sh, int e) {
+template <class SH>
+__device__ __forceinline__ NodeV t_node(const SH& sh, int e) {
     NodeV v;
     v.ac = sh.ts[0][e]; v.am = sh.ts[1][e]; v.ag = sh.ts[2][e]; v.ap = sh.ts[3][e];
     v.rc = sh.ts[4][e]; v.rm = sh.ts[5][e]; v.rg = sh.ts[6][e]; v.nr = sh.ts[7][e];
@@ -443,7 +473,8 @@ __device__ __forceinline__ NodeV t_node(const ResolveShared& sh, int e) {
     return v;
 }
 
-__device__ __forceinline__ NodeV stage_node(const ResolveShared& sh, int b) {
+template <class SH>
+__device__ __forceinline__ NodeV stage_node(const SH& sh, int b) {
     NodeV v;
     v.ac = sh.stage[b][0]; v.am = sh.stage[b][1]; v.ag = sh.stage[b][2]; v.ap = sh.stage[b][3];
     v.rc = sh.stage[b][4]; v.rm = sh.stage[b][5]; v.rg = sh.stage[b][6]; v.nr = sh.stage[b][7];
@@ -509,7 +540,8 @@ struct Prefetch {
 // winner lower bound: the first untouched entry when pod p is decided is key1 or key2 (or none:
 // then the batch stops at a full list, or the list is short and the bound is 0), so key2 — or
 // key1 when the list is full and has no second — is <= it.
-__device__ __forceinline__ void prefetch_issue(const EngineArgs& a, ResolveShared& sh, int p, int lane, bool exact,
+template <class SH>
+__device__ __forceinline__ void prefetch_issue(const EngineArgs& a, SH& sh, int p, int lane, bool exact,
                                                Prefetch& pf) {
     const uint64_t c = lane < kL ? sh.cand[p][lane] : 0ull;
     const bool ok = c != 0 && !is_touched(sh, key_node(c), exact);
@@ -527,7 +559,8 @@ __device__ __forceinline__ void prefetch_issue(const EngineArgs& a, ResolveShare
 
 // Wave 0: pod p's best untouched list node given that `winner` just joined the table (-1:
 // none): stage its record, fold its key into ctl[bslot].best, set kfull.
-__device__ __forceinline__ void prefetch_commit(ResolveShared& sh, int lane, const Prefetch& pf, int32_t winner,
+template <class SH>
+__device__ __forceinline__ void prefetch_commit(SH& sh, int lane, const Prefetch& pf, int32_t winner,
                                                 int stage_buf, int bslot) {
     const int slot = (pf.key1 != 0 && key_node(pf.key1) == winner) ? 1 : 0;
     const uint64_t key = slot ? pf.key2 : pf.key1;
@@ -542,7 +575,8 @@ __device__ __forceinline__ void prefetch_commit(ResolveShared& sh, int lane, con
 // j's own included when it was bound Ok and runs one tick — subtracted from n.  Lane-parallel:
 // one LDS round for the whole range; the (usually zero or one) hits are folded via a ballot.
 // Marks them expired when `expired` is given (the writer wave).
-__device__ __forceinline__ void expire_on(const ResolveShared& sh, int e0, int e1, int t, int64_t j, bool ok,
+template <class SH>
+__device__ __forceinline__ void expire_on(const SH& sh, int e0, int e1, int t, int64_t j, bool ok,
                                           int lane, NodeV& n, uint8_t* expired) {
     for (int x0 = e0; x0 < e1; x0 += kWave) {
         const int x = x0 + lane;
@@ -567,9 +601,11 @@ __device__ __forceinline__ void expire_on(const ResolveShared& sh, int e0, int e
     }
 }
 
-template <int kMode>
-__global__ __launch_bounds__(kResolveThreads) void resolve_kernel(const EngineArgs* __restrict__ A) {
-    __shared__ ResolveShared sh;
+template <int kMode, class C>
+__global__ __launch_bounds__(C::kThreads) void resolve_kernel(const EngineArgs* __restrict__ A) {
+    constexpr int kTMax = C::kTMax, kHash = C::kHash, kMaxBatchR = C::kMaxBatchR, kMaxExp = C::kMaxExp,
+                  kFilterBits = C::kFilterBits, kResolveThreads = C::kThreads;
+    __shared__ ResolveShared<C> sh;
     const EngineArgs a = A[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid >> 6;
     const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
@@ -635,13 +671,12 @@ __global__ __launch_bounds__(kResolveThreads) void resolve_kernel(const EngineAr
     // kResolveThreads): claim the node's hash slot with a CAS (duplicates find it), number the
     // claimed slots, then read the entry back.  Entry numbering order is immaterial: an entry
     // index only names a node, it never takes part in a comparison between distinct nodes.
-    static_assert(kMaxExp <= kResolveThreads, "one thread per pre-inserted expiry");
     const bool pre_want = tid < e_cnt && sh.ex_ok[tid];
     int pre_slot = -1;
     bool pre_claim = false;
     if (pre_want) {
         const int32_t nd = sh.ex_node[tid];
-        uint32_t hs = hslot(nd);
+        uint32_t hs = hslot<ResolveShared<C>>(nd);
         for (;;) {  // the table holds <= kMaxExp < kHash nodes: terminates
             const int32_t prev = atomicCAS(&sh.hkey[hs], -1, nd);
             if (prev == -1 || prev == nd) { pre_slot = (int)hs; pre_claim = prev == -1; break; }
@@ -1023,6 +1058,8 @@ __global__ __launch_bounds__(256) void rescale_kernel(NodeSoA s, int64_t n_pad, 
 // Launchers, called by ks_engine.cpp.
 // ---------------------------------------------------------------------------------------------
 int max_batch_pods() { return kMaxBatchR; }
+int small_resolver_max_batch() { return RSmall::kMaxBatchR; }
+int small_resolver_max_nodes() { return kSmallMaxNodes; }
 int max_pods_per_scan_wg() { return kMaxPG; }
 int block_nodes() { return kBlockNodes; }
 
@@ -1063,13 +1100,21 @@ hipError_t launch_merge(const EngineArgs* d, int S, int B, const uint64_t* lists
     return hipGetLastError();
 }
 
-hipError_t launch_resolve(const EngineArgs* d, int S, int mode, hipStream_t st) {
+template <class C>
+static void launch_resolve_t(const EngineArgs* d, int S, int mode, hipStream_t st) {
     switch (mode) {
-        case kEvalMicro: hipLaunchKernelGGL(resolve_kernel<kEvalMicro>, dim3(S), dim3(kResolveThreads), 0, st, d); break;
-        case kEvalTiny: hipLaunchKernelGGL(resolve_kernel<kEvalTiny>, dim3(S), dim3(kResolveThreads), 0, st, d); break;
-        case kEvalNarrow: hipLaunchKernelGGL(resolve_kernel<kEvalNarrow>, dim3(S), dim3(kResolveThreads), 0, st, d); break;
-        default: hipLaunchKernelGGL(resolve_kernel<kEvalWide>, dim3(S), dim3(kResolveThreads), 0, st, d); break;
+        case kEvalMicro: hipLaunchKernelGGL((resolve_kernel<kEvalMicro, C>), dim3(S), dim3(C::kThreads), 0, st, d); break;
+        case kEvalTiny: hipLaunchKernelGGL((resolve_kernel<kEvalTiny, C>), dim3(S), dim3(C::kThreads), 0, st, d); break;
+        case kEvalNarrow: hipLaunchKernelGGL((resolve_kernel<kEvalNarrow, C>), dim3(S), dim3(C::kThreads), 0, st, d); break;
+        default: hipLaunchKernelGGL((resolve_kernel<kEvalWide, C>), dim3(S), dim3(C::kThreads), 0, st, d); break;
     }
+}
+
+hipError_t launch_resolve(const EngineArgs* d, int S, int mode, bool small, hipStream_t st) {
+    if (small)
+        launch_resolve_t<RSmall>(d, S, mode, st);
+    else
+        launch_resolve_t<RBig>(d, S, mode, st);
     return hipGetLastError();
 }
 
