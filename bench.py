@@ -177,6 +177,13 @@ def main():
     eng.step(S)
     st = eng.last_step_stats()
     eng.set_profiling(False)
+    # per-tick node usage: one ks_usage call = zero + usage kernel over the
+    # pods that may still run + the [N][3] copy to the host
+    eng.usage()
+    t_u = time.perf_counter()
+    for _ in range(10):
+        eng.usage()
+    usage_ms = (time.perf_counter() - t_u) * 100.0
 
     if rank == 0:
         nodes = args.nodes
@@ -230,6 +237,8 @@ def main():
                         "scan_avg_ms": scan_avg_ms, "resolve_avg_ms": res_avg_ms,
                         "other_avg_ms": other_avg_ms,
                         "profiled_step_ms": st["step_ms"]},
+            "usage_query": {"ms_per_call": usage_ms, "nodes": nodes,
+                            "note": "ks_usage wall time incl. the 24 B/node copy to the host"},
             "cpu_baseline": cpu,
             "host": {"cpu": platform.processor() or platform.machine(), "nproc": os.cpu_count()},
         }
