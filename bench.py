@@ -31,6 +31,17 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 BYTES_PER_EVAL = 80     # alloc[4] + reqTotal[3] + nRunning + taint + label
 
 
+def _device(local_rank: int) -> int:
+    """One rank per GPU; with fewer visible GPUs than ranks (a one-GPU rehearsal of N > 1) ranks
+    share them round-robin.  torch.cuda.device_count() does not initialise the GPU."""
+    try:
+        import torch
+        n = torch.cuda.device_count()
+    except ImportError:
+        n = 0
+    return local_rank % n if n > 0 else local_rank
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -116,7 +127,7 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = _device(int(os.environ.get("LOCAL_RANK", "0")))
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -254,7 +265,7 @@ def main_c4(args):
     ranges (weak scaling, no collective).  A step = `pods-per-step` ticks of every scenario."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = _device(int(os.environ.get("LOCAL_RANK", "0")))
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -340,7 +351,7 @@ def main_c5(args):
     --vshards > 1 (virtual shards on one GPU, the exchange without RCCL)."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = _device(int(os.environ.get("LOCAL_RANK", "0")))
     dist = None
     if world > 1:
         import torch.distributed as dist
