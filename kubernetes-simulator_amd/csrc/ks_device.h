@@ -367,86 +367,8 @@ __host__ __device__ __forceinline__ uint32_t eval_t(const Cfg& c, const PodRec& 
     else return eval_total1(c, p, n);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Guarded float evaluator (the common path of scan and resolve).  Feasibility stays integer;
-// the three floors — floor(10 (A - u) / A) per LeastRequested resource and
-// floor(10 (1 - |uc/Ac - um/Am|)) — are computed in float from per-node reciprocals ic = 1/Ac,
-// im = 1/Am.  Error bounds (float rounding 2^-24 per op, v_rcp 1 ulp): the LR argument is off by
-// < 3.2e-6, the BA argument by < 6.5e-6.  When the fractional part of an argument is at least
-// kGuardLR / kGuardBA away from an integer the float floor equals the exact one; otherwise
-// `need` is set and the caller re-evaluates that lane exactly (eval_t) — rare, and a wave with no
-// such lane skips the exact code entirely.
-// ---------------------------------------------------------------------------------------------
-constexpr float kGuardLR = 1.0e-5f;
-constexpr float kGuardBA = 2.0e-5f;
-
-__host__ __device__ __forceinline__ float node_rcp(int64_t A) { return A > 0 ? rcp_est((float)A) : 0.f; }
-
-__host__ __device__ __forceinline__ int32_t floor_guarded(float y, float guard, bool& need) {
-    const int32_t q = (int32_t)y;  // y >= 0
-    const float fr = y - (float)q;
-    need |= (fr < guard) | (fr > 1.f - guard);
-    return q;
-}
-
-template <int kMode>
-__host__ __device__ __forceinline__ uint32_t eval_fast(const Cfg& c, const PodRec& p, const NodeV& n, float ic,
-                                                       float im, bool& need) {
-    if (!c.has_scorers) return 0;
-    int64_t uc, um;
-    if constexpr (kMode != kEvalWide) {
-        const int32_t qc = clamp_req(p.req[0]), qm = clamp_req(p.req[1]);
-        const int32_t ucn = (int32_t)n.rc + qc, umn = (int32_t)n.rm + qm;
-        if (c.filter_feeds) {
-            bool ok = true;
-            if (c.filters & kFilterFit) {
-                ok &= n.nr < n.ap;
-                if (p.keymask & 1) ok &= ucn <= (int32_t)n.ac;
-                if (p.keymask & 2) ok &= umn <= (int32_t)n.am;
-                if (p.keymask & 4) ok &= (int32_t)n.rg + clamp_req(p.req[2]) <= (int32_t)n.ag;
-            }
-            if (c.filters & kFilterTaint) ok &= (n.taint & ~p.tol) == 0;
-            if (c.filters & kFilterSelector) ok &= (n.label & p.sel) == p.sel;
-            if (!ok) return 0;
-        }
-        uc = ucn;
-        um = umn;
-    } else {
-        if (c.filter_feeds) {
-            bool ok = true;
-            if (c.filters & kFilterFit) ok &= fits(p, n);
-            if (c.filters & kFilterTaint) ok &= (n.taint & ~p.tol) == 0;
-            if (c.filters & kFilterSelector) ok &= (n.label & p.sel) == p.sel;
-            if (!ok) return 0;
-        }
-        uc = n.rc + p.req[0];
-        um = n.rm + p.req[1];
-    }
-    int32_t total = c.const_total;
-    if (c.w_lr) {
-        int32_t lc = 0, lm = 0;
-        if (n.ac > 0 && uc <= n.ac) lc = floor_guarded((float)(n.ac - uc) * (10.f * ic), kGuardLR, need);
-        if (n.am > 0 && um <= n.am) lm = floor_guarded((float)(n.am - um) * (10.f * im), kGuardLR, need);
-        total += c.w_lr * ((lc + lm) >> 1);
-    }
-    if (c.w_ba && n.ac > 0 && n.am > 0 && uc < n.ac && um < n.am) {
-        const float d = fabsf((float)uc * ic - (float)um * im);
-        total += c.w_ba * floor_guarded(10.f - 10.f * d, kGuardBA, need);
-    }
-    return (uint32_t)total + 1u;
-}
-
-// eval_t through the guarded float path (exact: falls back per lane)
-template <int kMode>
-__host__ __device__ __forceinline__ uint32_t eval_g(const Cfg& c, const PodRec& p, const NodeV& n, float ic, float im) {
-    bool need = false;
-    uint32_t t = eval_fast<kMode>(c, p, n, ic, im, need);
-    if (need) t = eval_t<kMode>(c, p, n);
-    return t;
-}
-
-// Pod-dependent upper bound of the total, used by the resolver to skip exact evaluations that
-// cannot reach a known lower bound.  Per entry the resolver keeps b = (A - r) / A and 1/A in
+// Pod-dependent upper bound of the total, used by the resolver's owner waves to pass the decider
+// only the touched entries that can reach a pod's lower bound.  Per entry the resolver keeps b = (A - r) / A and 1/A in
 // float; for a pod with requests q, f = b - q/A = (A - u) / A and
 //   LeastRequested  floor(10 f)              <= floor(10 f~ + kBoundLR)
 //   Balanced        floor(10 (1 - |fc - fm|)) <= floor(10 (1 - |fc~ - fm~|) + kBoundBA)
@@ -528,16 +450,6 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
     const uint32_t mh = wave_max_u32(hi);
     const uint32_t ml = wave_max_u32(hi == mh ? lo : 0u);
     return ((uint64_t)mh << 32) | ml;
-}
-
-// Best key of a wave's 64 nodes (lane l holds node base + l): the max total and, among
-// ties, the lowest lane — a 32-bit max plus one ballot instead of a 64-bit reduction.
-__device__ __forceinline__ uint64_t wave_best_key(uint32_t total1, uint32_t base) {
-    uint32_t m = wave_max_u32(total1);
-    if (m == 0) return 0ull;
-    uint64_t hit = __ballot(total1 == m);
-    uint32_t lane = (uint32_t)__ffsll((unsigned long long)hit) - 1u;
-    return make_key(m, base + lane);
 }
 
 // Arguments of the batch kernels (expire_head / scan / resolve).

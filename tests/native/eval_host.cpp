@@ -50,23 +50,3 @@ extern "C" void ks_host_prune_batch(const ks::Cfg* c, int64_t n, const int64_t* 
         tmax[i] = ks::prune_tmax(*c, ks::prune_prep(*c, v), (float)p.req[0], (float)p.req[1]);
     }
 }
-// guarded float evaluator: total1 through eval_g and the fraction of lanes that needed the exact path
-extern "C" double ks_host_fast_batch(const ks::Cfg* c, int64_t n, const int64_t* alloc, const int64_t* run,
-                                     const int64_t* req, int narrow, uint32_t* total1_g) {
-    int64_t needs = 0;
-    for (int64_t i = 0; i < n; i++) {
-        ks::NodeV v{};
-        v.ac = alloc[i * 4 + 0]; v.am = alloc[i * 4 + 1]; v.ag = alloc[i * 4 + 2]; v.ap = alloc[i * 4 + 3];
-        v.rc = run[i * 3 + 0]; v.rm = run[i * 3 + 1]; v.rg = run[i * 3 + 2]; v.nr = 0;
-        ks::PodRec p{};
-        p.req[0] = req[i * 3 + 0]; p.req[1] = req[i * 3 + 1]; p.req[2] = req[i * 3 + 2];
-        p.keymask = 0x7;
-        const float ic = ks::node_rcp(v.ac), im = ks::node_rcp(v.am);
-        bool need = false;
-        if (narrow) (void)ks::eval_fast<ks::kEvalNarrow>(*c, p, v, ic, im, need);
-        else (void)ks::eval_fast<ks::kEvalWide>(*c, p, v, ic, im, need);
-        needs += need;
-        total1_g[i] = narrow ? ks::eval_g<ks::kEvalNarrow>(*c, p, v, ic, im) : ks::eval_g<ks::kEvalWide>(*c, p, v, ic, im);
-    }
-    return n ? (double)needs / n : 0.0;
-}

@@ -41,8 +41,6 @@ def lib():
     L.ks_host_ba_n_batch.argtypes = [C.c_int64] + [p()] * 5
     L.ks_host_ba_batch.argtypes = [C.c_int64] + [p()] * 5
     L.ks_host_prune_batch.argtypes = [C.POINTER(Cfg), C.c_int64] + [p()] * 7
-    L.ks_host_fast_batch.argtypes = [C.POINTER(Cfg), C.c_int64, p(), p(), p(), C.c_int, p()]
-    L.ks_host_fast_batch.restype = C.c_double
     return L
 
 
@@ -154,36 +152,6 @@ def test_prune_bound_sound(lib, feeds, const, w_lr, w_ba, cap_bits):
     assert (total <= tm[live].astype(np.int64)).all(), "prune bound below the exact total"
     # and the bound is useful: mostly within a couple of points of the exact total
     assert np.mean(tm[live].astype(np.int64) - total) < 0.2 * (w_lr + w_ba) + 0.5
-
-
-@pytest.mark.parametrize("feeds,const,w_lr,w_ba", [(1, 0, 1, 1), (0, 0, 1, 1), (1, 5, 2, 0), (0, 3, 0, 3),
-                                                   (0, 1000, 50, 50)])
-@pytest.mark.parametrize("cap_bits", [20, 28, 50])
-def test_guarded_float_eval_exact(lib, feeds, const, w_lr, w_ba, cap_bits):
-    """eval_g (float floors + exact fallback near integer boundaries) == the exact evaluator."""
-    rng = np.random.default_rng(cap_bits * 7 + w_lr * 3 + w_ba + const + feeds)
-    n = 60_000
-    alloc, run, req = _nodes(rng, n, cap_bits)
-    # boundary-heavy cases: u a multiple of A/10 (LR exact integers), balanced (BA = 10)
-    k = rng.integers(0, 11, n)
-    sel = rng.random(n) < 0.2
-    run[sel, 0] = 0
-    req[sel, 0] = (np.maximum(alloc[sel, 0], 0) * k[sel]) // 10
-    sel2 = rng.random(n) < 0.1
-    run[sel2, :2] = 0
-    ratio = req[sel2, 0] / np.maximum(alloc[sel2, 0], 1).astype(np.float64)
-    req[sel2, 1] = (ratio * np.maximum(alloc[sel2, 1], 0)).astype(np.int64)
-    assert (req >= 0).all()
-    c = Cfg(n_nodes=n, nwb=0, filter_feeds=feeds, filters=1 if feeds else 0, has_scorers=1, w_lr=w_lr,
-            w_ba=w_ba, const_total=const, tick_seconds=1)
-    t1 = np.zeros(n, np.uint32); t1n = np.zeros(n, np.uint32); tm = np.zeros(n, np.uint32)
-    t1t = np.zeros(n, np.uint32)
-    lib.ks_host_prune_batch(C.byref(c), n, _p(alloc), _p(run), _p(req), _p(t1), _p(t1n), _p(tm), _p(t1t))
-    narrow = cap_bits < 29
-    g = np.zeros(n, np.uint32)
-    frac = lib.ks_host_fast_batch(C.byref(c), n, _p(alloc), _p(run), _p(req), 1 if narrow else 0, _p(g))
-    np.testing.assert_array_equal(g, t1n if narrow else t1)
-    assert frac < 0.3  # the boundary-heavy mix above; random states need the fallback far less
 
 
 @pytest.mark.parametrize("feeds,const,w_lr,w_ba", [(1, 0, 1, 1), (0, 0, 1, 1), (1, 5, 2, 0), (0, 3, 0, 3)])
