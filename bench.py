@@ -14,6 +14,15 @@ region is K ks_step calls bracketed by a barrier + device synchronisation.
 N > 1 (torchrun): every rank runs an independent what-if replica of the workload
 (BASELINE.json configs[3] style: cluster replica × pod trace, seed ^ rank) on its own GPU;
 no data-path collective — weak scaling; value = all ranks' evals ÷ the slowest rank's time.
+
+Alongside (field "c5_sharded", every N): BASELINE.json configs[4] — one 1M-node cluster
+node-sharded across the N ranks (ks_shard: each rank scans its node range, one RCCL all-gather
+of the per-pod candidate lists per batch), total work fixed as N grows (strong scaling): the
+north star's scaling target.  Skipped (with the reason) when ranks share a GPU.
+
+roofline: "frac" is the whole path's fraction of the 80-B-per-evaluation model at 8 TB/s
+(SURVEY.md §8(d)): evals/s x 80 B / 8 TB/s.  The scan kernel's measured HBM traffic (PMC,
+profiles/pmc_scan.json) and the resolver's per-pod latency are reported under it.
 """
 from __future__ import annotations
 
@@ -86,15 +95,16 @@ def cpu_baseline(trace, scorers, sample_pods, budget_s):
                                "sample": f"first {d_st} pods, one thread ({t_st:.1f} s)"})
 
 
-def load_traffic(n_launch_pods):
-    """HBM bytes per scan launch from the committed PMC profile (FETCH_SIZE ×2 gfx950
-    correction + WRITE_SIZE, per MI355X_MICROARCH.md §HBM), if present."""
+def load_traffic():
+    """Measured HBM bytes per scan launch (2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of
+    MI355X_MICROARCH.md §HBM) from the committed PMC summary, if present."""
     p = os.path.join(ROOT, "profiles", "pmc_scan.json")
     if not os.path.exists(p):
         return None
     with open(p) as f:
         d = json.load(f)
-    return d.get("hbm_bytes_per_scan_launch")
+    b = d.get("hbm_bytes_per_scan_launch")
+    return {"bytes": b, "source": d.get("source", "profiles/pmc_scan.json")} if b else None
 
 
 def main():
@@ -119,6 +129,10 @@ def main():
     ap.add_argument("--c5-nodes", type=int, default=1 << 20)
     ap.add_argument("--c5-pods", type=int, default=100_000)
     ap.add_argument("--vshards", type=int, default=1, help="c5: virtual node shards per rank")
+    ap.add_argument("--no-c5", action="store_true", help="c3: skip the C5 node-sharded leg")
+    ap.add_argument("--c5-steps", type=int, default=4, help="c3: timed steps of the C5 leg")
+    ap.add_argument("--c5-timeout", type=float, default=240.0,
+                    help="c3: seconds the C5 leg may take before it is abandoned (the C3 line still prints)")
     args = ap.parse_args()
     if args.config == "c4":
         return main_c4(args)
@@ -188,13 +202,20 @@ def main():
     eng.step(S)
     st = eng.last_step_stats()
     eng.set_profiling(False)
-    # per-tick node usage: one ks_usage call = zero + usage kernel over the
-    # pods that may still run + the [N][3] copy to the host
-    eng.usage()
+    # per-tick node usage: ks_usage_at = zero + usage kernel over the pod
+    # blocks that may run at t (run-interval index) + the [N][3] copy; the digest covers every
+    # tick of the last step's window
+    t_now = eng.tick
+    eng.usage_at(t_now)
     t_u = time.perf_counter()
-    for _ in range(10):
-        eng.usage()
+    for k in range(10):
+        eng.usage_at(t_now - 1000 * k)
     usage_ms = (time.perf_counter() - t_u) * 100.0
+    t_u = time.perf_counter()
+    eng.usage_digest(t_now - S + 1, t_now + 1)
+    digest_ms = (time.perf_counter() - t_u) * 1e3
+    eng.close()
+    line = None
 
     if rank == 0:
         nodes = args.nodes
@@ -206,10 +227,12 @@ def main():
         scan_avg_ms = st["scan_ms"] / launches
         res_avg_ms = st["resolve_ms"] / launches
         other_avg_ms = st["other_ms"] / launches
-        # algorithmic bytes of one scan launch: 80 B per (pod, node) eval
-        scan_alg_bytes = BYTES_PER_EVAL * pods_per_launch * nodes
-        achieved = scan_alg_bytes / (scan_avg_ms * 1e-3) / 1e9 if scan_avg_ms > 0 else None
-        traffic = load_traffic(pods_per_launch)
+        # the whole path against the 80-B model: evals/s x 80 B
+        achieved = value * BYTES_PER_EVAL / 1e9
+        traffic = load_traffic()
+        scan_s = scan_avg_ms * 1e-3
+        scan_model = BYTES_PER_EVAL * pods_per_launch * nodes
+        res_ns_pod = st["resolve_ms"] * 1e6 / max(st["pods"], 1)
         cpu = None
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(trace, scorers, args.cpu_sample_pods, args.cpu_budget_s)
@@ -233,28 +256,44 @@ def main():
                        "batch_pods": args.batch or 256},
             "pods_per_s": pods_per_s,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-                         "kernel": "scan_kernel",
-                         "note": "algorithmic bytes = 80 B x (pods x nodes) per scan launch; the scan reuses "
-                                 "each node record across the batch's pods, so frac can exceed 1 — traffic is "
-                                 "the measured HBM bytes per launch"},
-            "dominant": {"kernel": "resolve_kernel",
-                         "share_of_device_time": st["resolve_ms"] / max(st["scan_ms"] + st["resolve_ms"] + st["other_ms"], 1e-9),
-                         "ns_per_pod": st["resolve_ms"] * 1e6 / max(st["pods"], 1),
-                         "bound": "latency: one workgroup per batch walks its pods in FIFO order, one "
-                                  "barrier-separated dependent step per pod (DESIGN.md §4); no HBM or "
-                                  "MFMA roofline applies"},
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic["bytes"] if traffic else None,
+                         "kernel": "whole path per batch (expire_head + scan + merge + resolve)",
+                         "model": "80 B per (pod, node) evaluation (SURVEY.md 8(d)) x evals/s over the timed "
+                                  "region; traffic = measured HBM bytes per scan launch (PMC)",
+                         "scan": {"ms_per_launch": scan_avg_ms, "pods_per_launch": pods_per_launch,
+                                  "model_bytes_per_launch": scan_model,
+                                  "measured_bytes_per_launch": traffic["bytes"] if traffic else None,
+                                  "measured_gbs": traffic["bytes"] / scan_s / 1e9 if traffic and scan_s > 0 else None,
+                                  "measured_frac": traffic["bytes"] / scan_s / 1e9 / HBM_PEAK_GBS
+                                  if traffic and scan_s > 0 else None,
+                                  "node_record_reuse": scan_model / traffic["bytes"] if traffic else None,
+                                  "traffic_source": traffic["source"] if traffic else None,
+                                  "bound": "VALU issue: fused Filter+Score evaluations + top-L extraction per "
+                                           "256-node block (SQ counters in profiles/)"},
+                         "resolve": {"ns_per_pod": res_ns_pod, "cycles_per_pod_at_2_4ghz": res_ns_pod * 2.4,
+                                     "share_of_device_time": st["resolve_ms"] / max(st["scan_ms"] + st["resolve_ms"]
+                                                                                   + st["other_ms"], 1e-9),
+                                     "bound": "latency: one workgroup per batch walks its pods in FIFO order "
+                                              "(DESIGN.md 4); no HBM or MFMA roofline applies"}},
             "kernels": {"launches_per_step": launches, "pods_per_launch": pods_per_launch,
                         "scan_avg_ms": scan_avg_ms, "resolve_avg_ms": res_avg_ms,
                         "other_avg_ms": other_avg_ms,
                         "profiled_step_ms": st["step_ms"]},
-            "usage_query": {"ms_per_call": usage_ms, "nodes": nodes,
-                            "note": "ks_usage wall time incl. the 24 B/node copy to the host"},
+            "usage_query": {"ms_per_call": usage_ms, "nodes": nodes, "tick": t_now,
+                            "digest_ms": digest_ms, "digest_ticks": S,
+                            "note": "ks_usage_at wall time at ticks near the end of the run, incl. the "
+                                    "24 B/node copy to the host; digest = every tick of the last step's window"},
+            "c5_sharded": None,
             "cpu_baseline": cpu,
             "host": {"cpu": platform.processor() or platform.machine(), "nproc": os.cpu_count()},
         }
+    if not args.no_c5:
+        c5 = c5_leg(args, rank, world, local, dist, line=line)
+        if rank == 0:
+            line["c5_sharded"] = c5
+    if rank == 0:
         print(json.dumps(line), flush=True)
-    eng.close()
     if dist is not None:
         dist.destroy_process_group()
 
@@ -343,22 +382,39 @@ def main_c4(args):
         dist.destroy_process_group()
 
 
-def main_c5(args):
+def c5_leg(args, rank, world, local, dist, steps=None, warmup=1, line=None):
     """BASELINE.json configs[4]: one 1M-node cluster (tracegen C5, seed 0x5EED0005) node-sharded
     across the ranks — rank r scans its contiguous node range, the per-pod top-L candidate lists
     are all-gathered over RCCL once per batch, every rank resolves the same binds (ks_shard).
     Total work is fixed as N grows: strong scaling.  At N=1 the engine is unsharded unless
-    --vshards > 1 (virtual shards on one GPU, the exchange without RCCL)."""
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = _device(int(os.environ.get("LOCAL_RANK", "0")))
-    dist = None
+    --vshards > 1 (virtual shards on one GPU, the exchange without RCCL).  Returns rank 0's
+    result dict (None on other ranks); a leg that cannot run says why."""
+    import threading
+    steps = args.c5_steps if steps is None else steps
     if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
+        try:
+            import torch
+            n_dev = torch.cuda.device_count()
+        except ImportError:
+            n_dev = 0
+        if n_dev < world:
+            return {"skipped": f"{world} ranks share {n_dev} GPU(s): RCCL needs one GPU per rank"}
+    box = {"line": line} if line is not None else {}
+    timer = None
+    if args.c5_timeout > 0:
+        def _abandon():
+            # the C5 leg hung (e.g. an RCCL rendezvous): the C3 line must still come out
+            box["timeout"] = True
+            if rank == 0 and "line" in box:
+                box["line"]["c5_sharded"] = {"error": f"abandoned after {args.c5_timeout:.0f} s"}
+                print(json.dumps(box["line"]), flush=True)
+            os._exit(0 if rank == 0 else 3)
+        timer = threading.Timer(args.c5_timeout, _abandon)
+        timer.daemon = True
+        timer.start()
     from kubesim_amd import encode, tracegen
     from kubesim_amd.engine import Engine, comm_unique_id
-    need = (args.steps + args.warmup + 1) * args.pods_per_step
+    need = (steps + warmup + 1) * args.pods_per_step
     n_pods = max(args.c5_pods, need)
     t0 = time.perf_counter()
     trace = tracegen.c5_trace(n_nodes=args.c5_nodes, n_pods=n_pods)
@@ -367,16 +423,17 @@ def main_c5(args):
     eng = Engine(tick_seconds=trace["tick_seconds"], filter_mode=1, filters=7, scorers=scorers,
                  device=local, batch_pods=args.batch)
     if world > 1:
-        box = [comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(box, src=0)
-        eng.shard(world, rank, box[0], args.vshards)
+        idbox = [comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(idbox, src=0)
+        eng.shard(world, rank, idbox[0], args.vshards)
     elif args.vshards > 1:
         eng.shard(1, 0, None, args.vshards)
     eng.load_nodes(enc["alloc"], enc["taint"], enc["label"])
     eng.submit(enc["pods"])
+    del trace, enc
     log(f"[rank {rank}] C5 {args.c5_nodes} nodes x {n_pods} pods ready in {time.perf_counter() - t0:.1f}s")
     S = args.pods_per_step
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         eng.step(S)
 
     def barrier():
@@ -392,9 +449,9 @@ def main_c5(args):
     barrier()
     t_start = time.perf_counter()
     binds = 0
-    for k in range(args.steps):
+    for k in range(steps):
         binds += len(eng.step(S))
-        log(f"[rank {rank}] step {k} done")
+        log(f"[rank {rank}] C5 step {k} done")
     t_el = time.perf_counter() - t_start
     barrier()
     if dist is not None:
@@ -406,27 +463,44 @@ def main_c5(args):
     eng.step(S)
     st = eng.last_step_stats()
     eng.set_profiling(False)
-    if rank == 0:
-        nodes = args.c5_nodes
-        launches = max(st["launches"], 1)
-        line = {
-            "metric": "pod-node Filter+Score evals/sec and pods bound/sec (C5 1M-node sharded cluster)",
-            "value": binds * nodes / t_el, "unit": "evals/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": t_el * 1e3 / args.steps, "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "int64",
-            "data": "synthetic (tracegen C5, seed 0x5EED0005)",
-            "config": {"workload": "C5: one 1M-node cluster, Filter(fit+taint+selector) -> Score(LR+BA) -> "
-                                   "argmax -> bind, node-sharded scan, per-batch RCCL candidate all-gather",
-                       "nodes": nodes, "pods_per_step": S, "trace_pods": n_pods,
-                       "parallelism": f"node-shards/{world}" + (f"x{args.vshards}v" if args.vshards > 1 else ""),
-                       "batch_pods": args.batch or 256},
-            "pods_per_s": binds / t_el,
-            "kernels": {"launches_per_step": launches, "pods_per_launch": st["pods"] / launches,
-                        "scan_avg_ms": st["scan_ms"] / launches, "resolve_avg_ms": st["resolve_ms"] / launches,
-                        "other_avg_ms": st["other_ms"] / launches, "profiled_step_ms": st["step_ms"]},
-        }
-        print(json.dumps(line), flush=True)
     eng.close()
+    if timer is not None:
+        timer.cancel()
+    if rank != 0:
+        return None
+    nodes = args.c5_nodes
+    launches = max(st["launches"], 1)
+    return {
+        "metric": "pod-node Filter+Score evals/sec and pods bound/sec (C5 1M-node sharded cluster)",
+        "value": binds * nodes / t_el, "unit": "evals/s", "n_gpus": world, "steps": steps,
+        "warmup": warmup, "ms_per_step": t_el * 1e3 / steps, "scaling": "strong",
+        "pods_per_s": binds / t_el,
+        "data": "synthetic (tracegen C5, seed 0x5EED0005)",
+        "config": {"workload": "C5: one 1M-node cluster, Filter(fit+taint+selector) -> Score(LR+BA) -> "
+                               "argmax -> bind, node-sharded scan, per-batch RCCL candidate all-gather",
+                   "nodes": nodes, "pods_per_step": S, "trace_pods": n_pods,
+                   "parallelism": f"node-shards/{world}" + (f"x{args.vshards}v" if args.vshards > 1 else ""),
+                   "batch_pods": args.batch or 256},
+        "kernels": {"launches_per_step": launches, "pods_per_launch": st["pods"] / launches,
+                    "scan_avg_ms": st["scan_ms"] / launches, "resolve_avg_ms": st["resolve_ms"] / launches,
+                    "other_avg_ms": st["other_ms"] / launches, "profiled_step_ms": st["step_ms"]},
+    }
+
+
+def main_c5(args):
+    """--config c5: the C5 leg alone, printed as the line."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = _device(int(os.environ.get("LOCAL_RANK", "0")))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    args.c5_timeout = 0
+    line = c5_leg(args, rank, world, local, dist, steps=args.steps, warmup=args.warmup)
+    if rank == 0:
+        line.update({"higher_is_better": True, "vs_baseline": None, "dtype": "int64"})
+        print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

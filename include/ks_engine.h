@@ -19,8 +19,10 @@
  *   ks_filter ................... api.Filter.Filter for every node (api/scheduler.go:19)
  *   ks_score .................... api.Scorer.Score aggregated over the registered scorers
  *                                 (api/scheduler.go:36, kubesim/kubesim.go:193-206)
- *   ks_usage .................... Σ Pod.ResourceUsage(clock) per node (kubesim/pod/pod.go:47-63)
+ *   ks_usage / ks_usage_at ...... Σ Pod.ResourceUsage(clock) per node (kubesim/pod/pod.go:47-63)
+ *   ks_usage_digest ............. the same for every tick of a window, as a fingerprint
  *   ks_pod_status ............... Pod.BuildStatus phase / times (kubesim/pod/pod.go:78-167)
+ *   ks_pod_lookup / ks_node_pods  Node.GetPod / GetPodStatus / GetPodList (kubesim/node/node.go:62-93)
  *   ks_group_* .................. one KubeSim.Run per what-if scenario, stepped together
  *   ks_last_error ............... the error text Run would return
  *
@@ -29,7 +31,8 @@
  *   KS_ENOTFOUND NotFound — no node selected; the run stops exactly as kubesim.go:217-220
  *   KS_EDEVICE   HIP / RCCL failure (no reference counterpart)
  * After KS_ENOTFOUND or a bind-time KS_EINVAL the run is aborted: later ks_step calls return
- * the same code, as Run would have returned.
+ * the same code, as Run would have returned.  A KS_EDEVICE from ks_step / ks_group_step is
+ * sticky too (the engine's tick and binds stay at the last completed step).
  *
  * Units: cpu, memory and nvidia.com/gpu quantities are int64 milli-units (exact for every
  * resource.Quantity that is a whole number of milli-units); the pods capacity is
@@ -44,7 +47,7 @@
 extern "C" {
 #endif
 
-#define KS_ABI_VERSION 1
+#define KS_ABI_VERSION 2  /* 2: ks_submit_pods takes key_id */
 
 typedef enum {
     KS_OK = 0,
@@ -146,11 +149,21 @@ ks_status ks_load_nodes(ks_engine* eng, int64_t n, const int64_t* alloc, const u
  * (non-decreasing; <= the current tick means "next tick").  req[m][3] container-summed
  * requests with keymask (1 cpu, 2 memory, 4 gpu); tol = dictionary taints tolerated; sel =
  * dictionary labels required (bit 63 = impossible); simSpec as CSR: phase_off[m+1],
- * phase_sec[Φ] (int32), phase_use[Φ][3]; flags = KS_PODFLAG_* (may be NULL). */
+ * phase_sec[Φ] (int32), phase_use[Φ][3]; flags = KS_PODFLAG_* (may be NULL).
+ *
+ * key_id[m] (may be NULL: every pod its own key, key id = FIFO index): the caller's interned
+ * "namespace-name" pod key (kubesim/node/node.go:146-160).  Node.CreatePod stores the pod under
+ * its key, replacing a same-key pod already stored on that node (node.go:58,
+ * kubesim/pod/podmap.go:27-29); a replaced pod that is still running stops counting toward the
+ * node's totals at that moment.  The engine keeps placements exact by refusing, with KS_ERANGE
+ * and nothing appended, a pod whose key was used by an earlier pod that may still be running at
+ * the new pod's bind tick (the only case in which the replacement can change a placement or a
+ * usage; which node each lands on is not known at submit).  Reused keys of finished pods are
+ * accepted and resolved exactly by ks_pod_lookup / ks_node_pods. */
 ks_status ks_submit_pods(ks_engine* eng, int64_t m, const int64_t* arrival_tick,
                          const int64_t* req, const uint8_t* keymask, const uint64_t* tol,
                          const uint64_t* sel, const int32_t* phase_off, const int32_t* phase_sec,
-                         const int64_t* phase_use, const uint8_t* flags);
+                         const int64_t* phase_use, const uint8_t* flags, const int64_t* key_id);
 
 /* Advance `ticks` ticks.  Writes up to `cap` binds to out (one per tick that had a queued
  * pod) and the number of binds made to *n_out. */
@@ -163,6 +176,30 @@ ks_status ks_score(ks_engine* eng, int64_t pod, int64_t* score_out);
 
 /* usage_out[n][3]: Σ over pods on each node of ResourceUsage at the current tick. */
 ks_status ks_usage(ks_engine* eng, int64_t* usage_out);
+
+/* usage_out[n][3] at any past tick 0 <= t <= the current tick (Pod.ResourceUsage,
+ * kubesim/pod/pod.go:47-63, sampled after tick t's bind): placements of every pod bound by t are
+ * final, so any tick of a batched ks_step can be read back.  Cost: the pods that may run at t
+ * (an index over run intervals skips finished pods), not the run's length. */
+ks_status ks_usage_at(ks_engine* eng, int64_t t, int64_t* usage_out);
+
+/* Per-tick usage digest for ticks t_lo <= t < t_hi (t_hi - 1 <= the current tick, t_hi - t_lo
+ * <= 2^20): out[(t - t_lo) * 6 + k] for k = 0..2 is Σ over nodes of usage[node][k] at tick t, and
+ * for k = 3..5 Σ over nodes of ks_node_mix(node) * usage[node][k - 3] (mod 2^64) — a per-tick
+ * fingerprint of the whole [n][3] usage matrix, computed from the pods' phase segments
+ * (difference arrays + a prefix sum) instead of one [n][3] reduction per tick. */
+ks_status ks_usage_digest(ks_engine* eng, int64_t t_lo, int64_t t_hi, uint64_t* out);
+/* the digest's node weight: z = (node + 1) * 0x9E3779B97F4A7C15, then the splitmix64 finaliser
+ * (z ^= z >> 30; z *= 0xBF58476D1CE4E5B9; z ^= z >> 27; z *= 0x94D049BB133111EB; z ^= z >> 31) */
+uint64_t ks_node_mix(int64_t node);
+
+/* Name-keyed queries over the binds made so far (Node.GetPod / GetPodStatus / GetPodList,
+ * kubesim/node/node.go:62-93).  ks_pod_lookup: the FIFO index of the pod stored on `node` under
+ * key_id (the last one bound there), KS_ENOTFOUND if none ("pod %q not found").  ks_node_pods:
+ * the FIFO indices of every pod stored on `node` (one per key, any bind status), in FIFO order;
+ * writes min(count, cap) and the count to *n_out.  Phases/times: ks_pod_status. */
+ks_status ks_pod_lookup(ks_engine* eng, int32_t node, int64_t key_id, int64_t* pod_out);
+ks_status ks_node_pods(ks_engine* eng, int32_t node, int64_t* pods_out, int64_t cap, int64_t* n_out);
 
 /* Pod status (Pod.BuildStatus, kubesim/pod/pod.go:78-145) at the current tick, for pods
  * [pod_lo, pod_lo + n) of the FIFO: PENDING = not bound (queued, or the pod an aborted run stopped

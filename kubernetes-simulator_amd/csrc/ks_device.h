@@ -508,8 +508,17 @@ hipError_t launch_eval_pod(const Cfg& c, const NodeSoA& s, const PodRec* pod, ui
 hipError_t launch_flush(const NodeSoA& s, const PodRec* pods, const int64_t* fin, int64_t t, int64_t n_done,
                         const int32_t* b_node, const int32_t* b_status, uint8_t* expired, hipStream_t st);
 hipError_t launch_selftest_lr_micro(unsigned long long* bad, hipStream_t st);
-hipError_t launch_usage(int64_t q_lo, int64_t q_hi, int64_t t, int32_t tick_s, const int32_t* b_node,
-                        const int32_t* b_status, const int64_t* t0, const int32_t* dur, const int32_t* phase_off,
-                        const int32_t* cum_sec, const int64_t* use, unsigned long long* usage, hipStream_t st);
+// usage queries: grids of candidate pod blocks of usage_block_pods() pods each (pods < q_hi)
+int usage_block_pods();
+hipError_t launch_usage(const int32_t* blocks, int64_t nblocks, int64_t q_hi, int64_t t, int32_t tick_s,
+                        const int32_t* b_node, const int32_t* b_status, const int64_t* t0, const int32_t* dur,
+                        const int32_t* phase_off, const int32_t* cum_sec, const int64_t* use,
+                        unsigned long long* usage, hipStream_t st);
+// diff: [6][t_hi - t_lo + 1] zeroed; out: [t_hi - t_lo][6]
+hipError_t launch_usage_digest(const int32_t* blocks, int64_t nblocks, int64_t q_hi, int64_t t_lo, int64_t t_hi,
+                               int32_t tick_s, const int32_t* b_node, const int32_t* b_status, const int64_t* t0,
+                               const int32_t* dur, const uint8_t* preg, const int32_t* phase_off,
+                               const int32_t* cum_sec, const int64_t* use, unsigned long long* diff,
+                               unsigned long long* out, hipStream_t st);
 
 }  // namespace ks

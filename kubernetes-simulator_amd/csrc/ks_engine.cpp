@@ -37,6 +37,7 @@
 #include <queue>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/ks_engine.h"
@@ -54,6 +55,9 @@ constexpr int kDefaultBatch = 256;
 #endif
 constexpr int kProfEv = 5;  // per launch: expire_head | scan | merge (+exchange) | resolve
 constexpr int64_t kNever = std::numeric_limits<int64_t>::max();
+constexpr int64_t kUBlk = 256;   // usage index: pods per block (= the usage kernels' workgroup)
+constexpr int64_t kUSup = 64;    // blocks per super block
+constexpr int64_t kMaxDigestTicks = 1 << 20;
 
 // Growable device array (stream-ordered copies on growth).
 template <typename T>
@@ -127,9 +131,22 @@ struct ks_engine {
     int mode = ks::kEvalWide;  // evaluator variant (ks_device.h)
     uint32_t flags = 0;        // KS_ENGINE_*
     std::vector<int64_t> h_exp_pos;  // global exp_pod index holding pod q's own expiry, or -1
+    // pod keys (Node.CreatePod's pods.Store(key, pod), kubesim/node/node.go:58)
+    std::vector<int64_t> h_key;
+    std::unordered_map<int64_t, int64_t> key_end;  // key -> latest run end among pods with it
+    // host mirror of the binds (name-keyed queries): node (-1 = not bound) and status
+    std::vector<int32_t> h_node;
+    std::vector<int8_t> h_status;
+    // name-keyed index over binds [0, idx_upto), extended on each query
+    int64_t idx_upto = 0;
+    std::vector<std::vector<int64_t>> node_pods;      // per node: every pod bound there, FIFO
+    // run-interval index for the usage queries: pod q may run only in [t0, end) (end = t0 when
+    // it never runs); per block of kUBlk pods and per super block of kUSup blocks the max end
+    std::vector<int64_t> h_end, blk_end, sup_end;
+    DVec<uint8_t> preg;  // 1: phases non-negative and no int32 wrap (digest by segments)
 
     // progress
-    int64_t tick = 0, done = 0, usage_lo = 0;
+    int64_t tick = 0, done = 0;
     int err = KS_OK;
     std::string errmsg;
 
@@ -158,6 +175,9 @@ struct ks_engine {
     uint8_t* d_mask = nullptr;
     int64_t* d_score = nullptr;
     unsigned long long* d_usage = nullptr;
+    DVec<int32_t> d_blk;                  // usage query: candidate pod blocks
+    std::vector<int32_t> h_blk;
+    DVec<unsigned long long> d_digest;    // [6][T + 1] difference arrays, then the prefix sums
 };
 
 namespace {
@@ -317,6 +337,7 @@ void engine_free(ks_engine* e) {
     e->pods.release(); e->dur.release(); e->b_node.release(); e->b_status.release();
     e->phase_off.release(); e->cum_sec.release(); e->exp_pod.release(); e->exp_off.release();
     e->t0.release(); e->fin.release(); e->use.release(); e->expired.release(); e->exp_pos.release();
+    e->preg.release(); e->d_blk.release(); e->d_digest.release();
     if (e->node_mem) (void)hipFree(e->node_mem);
     if (e->lists) (void)hipFree(e->lists);
     if (e->cand) (void)hipFree(e->cand);
@@ -456,7 +477,7 @@ ks_status ks_load_nodes(ks_engine* e, int64_t n, const int64_t* alloc, const uin
 
 ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const int64_t* req, const uint8_t* keymask,
                          const uint64_t* tol, const uint64_t* sel, const int32_t* phase_off, const int32_t* phase_sec,
-                         const int64_t* phase_use, const uint8_t* flags) {
+                         const int64_t* phase_use, const uint8_t* flags, const int64_t* key_id) {
     if (!e) return KS_EINVAL;
     if (!e->nodes_loaded) return fail(e, KS_EINVAL, "ks_load_nodes must precede ks_submit_pods");
     if (m < 0) return fail(e, KS_EINVAL, "negative pod count");
@@ -478,6 +499,31 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
     }
     for (int64_t f = 0; f < nf * 3; f++)
         if (phase_use[f] < 0 || phase_use[f] >= kMaxValue) return fail(e, KS_EINVAL, "usage out of range");
+    // Pod keys: a Store over a same-key pod that is still running on the chosen node would drop
+    // that pod from the node's totals (kubesim/node/node.go:58).  Refuse the one case where that
+    // can happen — an earlier pod with the key may still run at this pod's bind tick — so every
+    // accepted trace schedules exactly as the reference (ks_engine.h, ks_submit_pods).
+    std::unordered_map<int64_t, int64_t> new_end;  // this call's keys -> latest run end
+    if (key_id) {
+        int64_t pb = e->P ? e->h_bind_tick[e->P - 1] : e->tick;
+        for (int64_t i = 0; i < m; i++) {
+            const int64_t bt = std::max<int64_t>(pb + 1, std::max<int64_t>(arrival[i], e->tick + 1));
+            pb = bt;
+            int64_t prev = std::numeric_limits<int64_t>::min();
+            auto it = new_end.find(key_id[i]);
+            if (it != new_end.end()) prev = it->second;
+            else if (auto jt = e->key_end.find(key_id[i]); jt != e->key_end.end()) prev = jt->second;
+            if (prev > bt)
+                return fail(e, KS_ERANGE, "pod %lld: key %lld reused at bind tick %lld while an earlier pod with it may run "
+                            "until tick %lld (Store would replace a running pod: outside the exact domain)",
+                            (long long)(e->P + i), (long long)key_id[i], (long long)bt, (long long)prev);
+            uint32_t acc = 0;
+            for (int32_t f = phase_off[i]; f < phase_off[i + 1]; f++) acc += (uint32_t)phase_sec[f];
+            const int32_t S = (int32_t)acc;
+            const int64_t d = S > 0 ? ((int64_t)S + e->cfg.tick_seconds - 1) / e->cfg.tick_seconds : 0;
+            new_end[key_id[i]] = std::max(prev, bt + d);
+        }
+    }
 
     {
         int64_t f[3] = {1, 1, 1};
@@ -501,6 +547,8 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
     std::vector<int32_t> dur(m), poff(m), cum(nf);
     std::vector<int64_t> t0(m), fin(m), eoff(m);
     std::vector<int32_t> tsec(m);
+    std::vector<int64_t> run_end(m);
+    std::vector<uint8_t> reg(m);
     std::vector<int32_t> epod;
     epod.reserve(m);
     const int64_t epod_base = e->exp_pod.n;
@@ -520,8 +568,12 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
         const int64_t bt = std::max<int64_t>(prev_bind + 1, arr);
         prev_bind = bt;
         uint32_t acc = 0;  // int32 wrapping, kubesim/pod/pod.go:155-162
+        int64_t acc64 = 0;
+        bool nonneg = true;
         for (int32_t f = phase_off[i]; f < phase_off[i + 1]; f++) {
             acc += (uint32_t)phase_sec[f];
+            acc64 += phase_sec[f];
+            nonneg &= phase_sec[f] >= 0;
             cum[f] = (int32_t)acc;
         }
         const int32_t S = (int32_t)acc;
@@ -530,6 +582,10 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
         dur[i] = (int32_t)d;
         t0[i] = bt;
         fin[i] = d > 0 ? bt + d : kNever;
+        run_end[i] = bt + d;
+        // the digest's segment form: cumulative seconds non-decreasing and (t - t0) * tick never
+        // wraps int32 while the pod runs (else the exact per-tick form)
+        reg[i] = nonneg && acc64 <= (int64_t)INT32_MAX - e->cfg.tick_seconds;
         poff[i] = (int32_t)(e->F + phase_off[i]);
         // expiries due before pod j binds: finish tick in (bind_tick[j-1], bind_tick[j]]
         while (!e->pending.empty() && e->pending.top().first <= bt) {
@@ -554,6 +610,7 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
     HIPCHK(e, e->b_status.append(neg.data(), m, st));
     std::vector<uint8_t> zero(m, 0);
     HIPCHK(e, e->expired.append(zero.data(), m, st));
+    HIPCHK(e, e->preg.append(reg.data(), m, st));
     // phase_off holds P+1 entries: overwrite the trailing sentinel
     if (e->phase_off.n) e->phase_off.n -= 1;
     HIPCHK(e, e->phase_off.append(poff.data(), m, st));
@@ -577,6 +634,19 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
     e->h_dur.insert(e->h_dur.end(), dur.begin(), dur.end());
     e->h_total_sec.insert(e->h_total_sec.end(), tsec.begin(), tsec.end());
     e->h_exp_off.insert(e->h_exp_off.end(), eoff.begin(), eoff.end());
+    for (int64_t i = 0; i < m; i++) e->h_key.push_back(key_id ? key_id[i] : e->P + i);
+    for (const auto& kv : new_end) e->key_end[kv.first] = kv.second;
+    e->h_node.resize(e->P + m, -1);
+    e->h_status.resize(e->P + m, -1);
+    // run-interval index (usage queries)
+    e->h_end.insert(e->h_end.end(), run_end.begin(), run_end.end());
+    for (int64_t q = e->P; q < e->P + m; q++) {
+        const int64_t b = q / kUBlk, s = b / kUSup;
+        if ((int64_t)e->blk_end.size() <= b) e->blk_end.push_back(std::numeric_limits<int64_t>::min());
+        if ((int64_t)e->sup_end.size() <= s) e->sup_end.push_back(std::numeric_limits<int64_t>::min());
+        e->blk_end[b] = std::max(e->blk_end[b], e->h_end[q]);
+        e->sup_end[s] = std::max(e->sup_end[s], e->h_end[q]);
+    }
     e->P += m;
     e->F += nf;
     e->last_arrival = last;
@@ -588,7 +658,8 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
 namespace {
 
 // ks_step, first half: the pods whose bind tick falls in (tick, tick + ticks] and the device
-// counters for them.  Returns false when there is nothing to schedule (the tick just advances).
+// counters for them.  Returns false when there is nothing to schedule (the caller just advances
+// the tick once the step as a whole has succeeded).
 bool step_prepare(ks_engine* e, int64_t ticks, int64_t* p_hi_out) {
     const int64_t t_end = e->tick + ticks;
     const int64_t p_hi = std::upper_bound(e->h_bind_tick.begin() + e->done, e->h_bind_tick.end(), t_end) -
@@ -601,11 +672,17 @@ bool step_prepare(ks_engine* e, int64_t ticks, int64_t* p_hi_out) {
     e->h_ctr[3] = -1;
     e->h_ctr[4] = 0;
     *e->h_args = make_args(e);
-    if (p_hi <= e->done) {
-        e->tick = t_end;
-        return false;
+    return p_hi > e->done;
+}
+
+// A device failure inside a step leaves the device counters and the binds of the step unknown:
+// the engine stops (sticky KS_EDEVICE) with its tick and binds at the last completed step.
+ks_status device_stop(ks_engine* e, ks_status r) {
+    if (r == KS_EDEVICE && e->err == KS_OK) {
+        e->err = KS_EDEVICE;
+        if (e->errmsg.empty()) e->errmsg = "device failure during a step";
     }
-    return true;
+    return r;
 }
 
 // ks_step, second half: the binds [done, new_done) (node / status copied back by the caller),
@@ -618,6 +695,10 @@ ks_status step_finish(ks_engine* e, int64_t t_end, int64_t new_done, const int32
         out[i].node = node[i];
         out[i].status = status[i];
         out[i].tick = e->h_bind_tick[e->done + i];
+    }
+    for (int64_t i = 0; i < nb; i++) {
+        e->h_node[e->done + i] = node[i];
+        e->h_status[e->done + i] = (int8_t)status[i];
     }
     *n_out = nb;
     e->done = new_done;
@@ -640,15 +721,24 @@ ks_status step_finish(ks_engine* e, int64_t t_end, int64_t new_done, const int32
 
 extern "C" {
 
+static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t cap, int64_t* n_out);
+
 ks_status ks_step(ks_engine* e, int64_t ticks, ks_bind* out, int64_t cap, int64_t* n_out) {
-    if (!e || !n_out || ticks < 0) return KS_EINVAL;
+    if (!e || !n_out || ticks < 0 || cap < 0 || (cap > 0 && !out)) return KS_EINVAL;
     *n_out = 0;
     if (e->err) return (ks_status)e->err;
     if (!e->nodes_loaded) return fail(e, KS_EINVAL, "no nodes loaded");
+    return device_stop(e, step_body(e, ticks, out, cap, n_out));
+}
+
+static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t cap, int64_t* n_out) {
     HIPCHK(e, hipSetDevice(e->device));
     const int64_t t_end = e->tick + ticks;
     int64_t p_hi = 0;
-    if (!step_prepare(e, ticks, &p_hi)) return KS_OK;
+    if (!step_prepare(e, ticks, &p_hi)) {
+        e->tick = t_end;
+        return KS_OK;
+    }
     hipStream_t st = e->st;
     HIPCHK(e, hipMemcpyAsync(e->d_ctr, e->h_ctr, 5 * sizeof(int64_t), hipMemcpyHostToDevice, st));
     HIPCHK(e, hipMemcpyAsync(e->d_args, e->h_args, sizeof(ks::EngineArgs), hipMemcpyHostToDevice, st));
@@ -838,7 +928,7 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
     if (S == 0) return KS_OK;
     if (hipSetDevice(g->device) != hipSuccess) return KS_EDEVICE;
     std::vector<int64_t> p_hi(S, 0), t_end(S, 0);
-    std::vector<char> live(S, 0);
+    std::vector<char> live(S, 0), part(S, 0);  // part: takes part in this step
     int mode = ks::kEvalMicro, blk_n = 0, B = 0;  // B: the largest member batch (grid size)
     bool k16 = true, small = true;
     for (ks_engine* e : g->engs) {
@@ -862,6 +952,7 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
             continue;
         }
         t_end[i] = e->tick + ticks;
+        part[i] = 1;
         live[i] = step_prepare(e, ticks, &p_hi[i]);
         // the widest evaluator any scenario needs (each is exact on every narrower domain)
         mode = std::min(mode, e->mode);
@@ -875,10 +966,23 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
     for (int i = 0; i < S; i++) g->h_args[i].PG = pg;
     hipStream_t st = g->st;
     auto dev = [&](hipError_t r) { return r == hipSuccess; };
+    // a device failure leaves every participating member's step unknown: sticky KS_EDEVICE, ticks
+    // and binds stay at the last completed step
+    auto dev_fail = [&](const char* what) {
+        g->errmsg = what;
+        for (int i = 0; i < S; i++)
+            if (part[i]) {
+                ks_engine* e = g->engs[i];
+                e->err = KS_EDEVICE;
+                e->errmsg = what;
+                status_out[i] = KS_EDEVICE;
+            }
+        return KS_EDEVICE;
+    };
     if (!dev(hipMemcpyAsync(g->d_ctr, g->h_ctr, sizeof(int64_t) * 32 * S, hipMemcpyHostToDevice, st)) ||
         !dev(hipMemcpyAsync(g->d_args, g->h_args, sizeof(ks::EngineArgs) * S, hipMemcpyHostToDevice, st)) ||
         !dev(hipEventRecord(g->ev[0], st)))
-        return KS_EDEVICE;
+        return dev_fail("group step: argument upload failed");
     std::vector<int64_t> start(S);
     for (int i = 0; i < S; i++) start[i] = g->engs[i]->done;
     int64_t launches = 0;
@@ -892,29 +996,27 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
                 !dev(ks::launch_scan(g->d_args, S, blk_n, B, pg, mode, k16, st)) ||
                 !dev(ks::launch_merge(g->d_args, S, B, nullptr, 0, 0, 0, nullptr, blk_n, st)) ||
                 !dev(ks::launch_resolve(g->d_args, S, mode, small, st)))
-                return KS_EDEVICE;
+                return dev_fail("group step: kernel launch failed");
             launches++;
         }
         if (!dev(hipMemcpyAsync(g->h_ctr, g->d_ctr, sizeof(int64_t) * 32 * S, hipMemcpyDeviceToHost, st)) ||
             !dev(hipStreamSynchronize(st)))
-            return KS_EDEVICE;
+            return dev_fail("group step: device synchronisation failed");
         for (int i = 0; i < S; i++) {
             if (!live[i]) continue;
             ks_engine* e = g->engs[i];
             const int64_t prev = start[i];
             start[i] = e->h_ctr[0];
             if (e->h_ctr[2] != 0 || start[i] >= p_hi[i]) live[i] = 0;
-            else if (start[i] <= prev) {  // every launch commits at least its first pod
-                g->errmsg = "scheduling made no progress";
-                return KS_EDEVICE;
-            }
+            else if (start[i] <= prev)  // every launch commits at least its first pod
+                return dev_fail("group step: scheduling made no progress");
         }
     }
     // binds back: one gather into a packed buffer, one copy
     int64_t total = 0, max_n = 0;
     for (int i = 0; i < S; i++) {
         ks_engine* e = g->engs[i];
-        const int64_t nb = status_out[i] == KS_OK && t_end[i] ? start[i] - e->done : 0;
+        const int64_t nb = status_out[i] == KS_OK && part[i] ? start[i] - e->done : 0;
         g->h_seg[i] = ks::BindSeg{e->b_node.p, e->b_status.p, e->done, std::max<int64_t>(nb, 0), total};
         total += std::max<int64_t>(nb, 0);
         max_n = std::max(max_n, nb);
@@ -927,16 +1029,17 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
         if (!dev(hipMalloc(&g->d_out, sizeof(int32_t) * 2 * g->out_cap)) ||
             !dev(hipHostMalloc(&g->h_out, sizeof(int32_t) * 2 * g->out_cap, hipHostMallocDefault))) {
             g->out_cap = 0;
-            return KS_EDEVICE;
+            return dev_fail("group step: bind buffer allocation failed");
         }
     }
     if (total) {
         if (!dev(hipMemcpyAsync(g->d_seg, g->h_seg, sizeof(ks::BindSeg) * S, hipMemcpyHostToDevice, st)) ||
             !dev(ks::launch_gather_binds(g->d_seg, S, max_n, g->d_out, g->d_out + total, st)) ||
             !dev(hipMemcpyAsync(g->h_out, g->d_out, sizeof(int32_t) * 2 * total, hipMemcpyDeviceToHost, st)))
-            return KS_EDEVICE;
+            return dev_fail("group step: bind copy failed");
     }
-    if (!dev(hipEventRecord(g->ev[1], st)) || !dev(hipStreamSynchronize(st))) return KS_EDEVICE;
+    if (!dev(hipEventRecord(g->ev[1], st)) || !dev(hipStreamSynchronize(st)))
+        return dev_fail("group step: device synchronisation failed");
     float ms = 0;
     (void)hipEventElapsedTime(&ms, g->ev[0], g->ev[1]);
     // unpack into the caller's ks_bind rows: members are independent, so large groups fill them
@@ -944,7 +1047,7 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
     auto finish = [&](int lo, int hi) {
         for (int i = lo; i < hi; i++) {
             ks_engine* e = g->engs[i];
-            if (status_out[i] != KS_OK || !t_end[i]) continue;
+            if (status_out[i] != KS_OK || !part[i]) continue;
             const ks::BindSeg& sg = g->h_seg[i];
             status_out[i] = step_finish(e, t_end[i], start[i], g->h_out + sg.off, g->h_out + total + sg.off,
                                         out ? out + (int64_t)i * cap : nullptr, out ? cap : 0, &n_out[i]);
@@ -1004,17 +1107,131 @@ ks_status ks_score(ks_engine* e, int64_t pod, int64_t* score_out) {
     return KS_OK;
 }
 
-ks_status ks_usage(ks_engine* e, int64_t* usage_out) {
+// Candidate pod blocks of a usage query over ticks >= t_lo: blocks of the pods [0, q_hi) (bind
+// ticks are FIFO-monotone, so q_hi bounds the start side) holding a pod whose run end is > t_lo;
+// super blocks whose every pod ended by t_lo are skipped whole.
+static int64_t usage_blocks(ks_engine* e, int64_t t_lo, int64_t q_hi) {
+    e->h_blk.clear();
+    const int64_t nblk = (q_hi + kUBlk - 1) / kUBlk;
+    for (int64_t s = 0; s * kUSup < nblk; s++) {
+        if (e->sup_end[s] <= t_lo) continue;
+        const int64_t b1 = std::min(nblk, (s + 1) * kUSup);
+        for (int64_t b = s * kUSup; b < b1; b++)
+            if (e->blk_end[b] > t_lo) e->h_blk.push_back((int32_t)b);
+    }
+    return (int64_t)e->h_blk.size();
+}
+
+// pods bound at ticks <= t (a FIFO prefix of the binds made so far)
+static int64_t bound_by(const ks_engine* e, int64_t t) {
+    return std::upper_bound(e->h_bind_tick.begin(), e->h_bind_tick.begin() + e->done, t) - e->h_bind_tick.begin();
+}
+
+static_assert(kUBlk == 256, "usage index block = the usage kernels' workgroup");
+
+ks_status ks_usage_at(ks_engine* e, int64_t t, int64_t* usage_out) {
     if (!e || !usage_out) return KS_EINVAL;
     if (!e->nodes_loaded) return fail(e, KS_EINVAL, "no nodes loaded");
+    if (t < 0 || t > e->tick) return fail(e, KS_EINVAL, "usage tick %lld outside [0, %lld]", (long long)t, (long long)e->tick);
     if (e->n == 0) return KS_OK;
     HIPCHK(e, hipSetDevice(e->device));
-    while (e->usage_lo < e->done && e->h_fin[e->usage_lo] <= e->tick) e->usage_lo++;
+    const int64_t q_hi = bound_by(e, t);
+    const int64_t nb = usage_blocks(e, t, q_hi);
     HIPCHK(e, hipMemsetAsync(e->d_usage, 0, sizeof(unsigned long long) * 3 * e->n, e->st));
-    HIPCHK(e, ks::launch_usage(e->usage_lo, e->done, e->tick, e->cfg.tick_seconds, e->b_node.p, e->b_status.p,
-                               e->t0.p, e->dur.p, e->phase_off.p, e->cum_sec.p, e->use.p, e->d_usage, e->st));
+    if (nb) {
+        HIPCHK(e, e->d_blk.reserve(nb, e->st));
+        HIPCHK(e, hipMemcpyAsync(e->d_blk.p, e->h_blk.data(), sizeof(int32_t) * nb, hipMemcpyHostToDevice, e->st));
+        HIPCHK(e, ks::launch_usage(e->d_blk.p, nb, q_hi, t, e->cfg.tick_seconds, e->b_node.p, e->b_status.p, e->t0.p,
+                                   e->dur.p, e->phase_off.p, e->cum_sec.p, e->use.p, e->d_usage, e->st));
+    }
     HIPCHK(e, hipMemcpyAsync(usage_out, e->d_usage, sizeof(int64_t) * 3 * e->n, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
+    return KS_OK;
+}
+
+ks_status ks_usage(ks_engine* e, int64_t* usage_out) {
+    if (!e) return KS_EINVAL;
+    return ks_usage_at(e, e->tick, usage_out);
+}
+
+ks_status ks_usage_digest(ks_engine* e, int64_t t_lo, int64_t t_hi, uint64_t* out) {
+    if (!e || !out) return KS_EINVAL;
+    if (!e->nodes_loaded) return fail(e, KS_EINVAL, "no nodes loaded");
+    if (t_lo < 0 || t_hi <= t_lo || t_hi - 1 > e->tick || t_hi - t_lo > kMaxDigestTicks)
+        return fail(e, KS_EINVAL, "digest window [%lld, %lld) outside [0, %lld] or longer than %lld ticks",
+                    (long long)t_lo, (long long)t_hi, (long long)e->tick + 1, (long long)kMaxDigestTicks);
+    HIPCHK(e, hipSetDevice(e->device));
+    const int64_t T = t_hi - t_lo;
+    const int64_t q_hi = bound_by(e, t_hi - 1);
+    const int64_t nb = usage_blocks(e, t_lo, q_hi);
+    HIPCHK(e, e->d_digest.reserve(6 * (T + 1) + 6 * T, e->st));
+    unsigned long long* diff = e->d_digest.p;
+    unsigned long long* res = diff + 6 * (T + 1);
+    HIPCHK(e, hipMemsetAsync(diff, 0, sizeof(unsigned long long) * 6 * (T + 1), e->st));
+    if (nb) {
+        HIPCHK(e, e->d_blk.reserve(nb, e->st));
+        HIPCHK(e, hipMemcpyAsync(e->d_blk.p, e->h_blk.data(), sizeof(int32_t) * nb, hipMemcpyHostToDevice, e->st));
+    }
+    HIPCHK(e, ks::launch_usage_digest(e->d_blk.p, nb, q_hi, t_lo, t_hi, e->cfg.tick_seconds, e->b_node.p, e->b_status.p,
+                                      e->t0.p, e->dur.p, e->preg.p, e->phase_off.p, e->cum_sec.p, e->use.p, diff, res,
+                                      e->st));
+    HIPCHK(e, hipMemcpyAsync(out, res, sizeof(uint64_t) * 6 * T, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    return KS_OK;
+}
+
+uint64_t ks_node_mix(int64_t node) {
+    uint64_t z = (uint64_t)(node + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// Name-keyed index: every pod bound per node in FIFO order, extended over the binds
+// [idx_upto, done) on each query; a key's stored pod is the last one bound there (Store
+// replaces, kubesim/node/node.go:58).
+static void index_binds(ks_engine* e) {
+    if ((int64_t)e->node_pods.size() < e->n) e->node_pods.resize(e->n);
+    for (int64_t q = e->idx_upto; q < e->done; q++) {
+        const int32_t nd = e->h_node[q];
+        if (nd < 0) continue;  // the pod an aborted run stopped at is never stored
+        e->node_pods[nd].push_back(q);
+    }
+    e->idx_upto = e->done;
+}
+
+ks_status ks_pod_lookup(ks_engine* e, int32_t node, int64_t key_id, int64_t* pod_out) {
+    if (!e || !pod_out) return KS_EINVAL;
+    *pod_out = -1;
+    if (node < 0 || node >= e->n) return fail(e, KS_EINVAL, "node %d out of range", node);
+    index_binds(e);
+    const std::vector<int64_t>& v = e->node_pods[node];
+    for (auto it = v.rbegin(); it != v.rend(); ++it)  // the last Store under the key wins
+        if (e->h_key[*it] == key_id) {
+            *pod_out = *it;
+            return KS_OK;
+        }
+    return fail(e, KS_ENOTFOUND, "pod with key %lld not found on node %d", (long long)key_id, node);
+}
+
+ks_status ks_node_pods(ks_engine* e, int32_t node, int64_t* pods_out, int64_t cap, int64_t* n_out) {
+    if (!e || !n_out || cap < 0 || (cap > 0 && !pods_out)) return KS_EINVAL;
+    *n_out = 0;
+    if (node < 0 || node >= e->n) return fail(e, KS_EINVAL, "node %d out of range", node);
+    index_binds(e);
+    const std::vector<int64_t>& v = e->node_pods[node];
+    // one pod per key: the last one bound here (a pod is listed iff no later pod on this node
+    // has its key)
+    std::unordered_map<int64_t, int64_t> last;
+    last.reserve(v.size());
+    for (int64_t q : v) last[e->h_key[q]] = q;
+    int64_t k = 0;
+    for (int64_t q : v)
+        if (last[e->h_key[q]] == q) {
+            if (k < cap) pods_out[k] = q;
+            k++;
+        }
+    *n_out = k;
     return KS_OK;
 }
 

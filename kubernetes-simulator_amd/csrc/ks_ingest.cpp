@@ -202,6 +202,7 @@ ks_status quantity_value_ceil(const char* s, int64_t* out) {
 struct YNode {
     enum Kind { kScalar, kMap, kSeq, kNull } kind = kNull;
     std::string scalar;
+    bool quoted = false;  // a quoted scalar is always a string (yaml.v2: no implicit resolution)
     std::vector<std::pair<std::string, std::unique_ptr<YNode>>> map;
     std::vector<std::unique_ptr<YNode>> seq;
     const YNode* get(const std::string& k, bool nocase = false) const {
@@ -318,6 +319,7 @@ std::unique_ptr<YNode> scalar_node(const std::string& v, int no) {
                        v.front() == '>' || v.front() == '!'))
         throw YamlError{"line " + std::to_string(no) + ": unsupported YAML construct '" + v + "'"};
     n->kind = YNode::kScalar;
+    n->quoted = !v.empty() && (v.front() == '"' || v.front() == '\'');
     n->scalar = unquote(v, no);
     return n;
 }
@@ -412,6 +414,131 @@ void set_err(char* err, int32_t len, const char* fmt, ...) {
     va_end(ap);
 }
 
+// strconv.ParseInt(s, 0, 64) of Go 1.11 (the reference's pinned toolchain, .travis.yml): optional
+// sign, then "0x"/"0X" hex, a leading "0" octal, else decimal.  Returns false on a syntax error;
+// *big = true when the magnitude does not fit int64 (ErrRange).
+bool go_parse_int(const std::string& s0, __int128* v, bool* big) {
+    *big = false;
+    if (s0.empty()) return false;
+    size_t i = 0;
+    bool neg = false;
+    if (s0[0] == '+' || s0[0] == '-') { neg = s0[0] == '-'; i = 1; }
+    std::string s = s0.substr(i);
+    if (s.empty()) return false;
+    int base = 10;
+    if (s[0] == '0' && s.size() > 1 && (s[1] == 'x' || s[1] == 'X')) {
+        if (s.size() < 3) return false;
+        base = 16;
+        s = s.substr(2);
+    } else if (s[0] == '0') {
+        base = 8;
+        s = s.substr(1);
+    }
+    unsigned __int128 n = 0;
+    for (char c : s) {
+        int d;
+        if (c >= '0' && c <= '9') d = c - '0';
+        else if (c >= 'a' && c <= 'z') d = c - 'a' + 10;
+        else if (c >= 'A' && c <= 'Z') d = c - 'A' + 10;
+        else return false;
+        if (d >= base) return false;
+        if (n <= ((unsigned __int128)1 << 70)) n = n * base + d;  // saturates far above 2^64
+    }
+    const unsigned __int128 lim = (unsigned __int128)1 << 63;
+    if (neg ? n > lim : n >= lim) *big = true;
+    *v = neg ? -(__int128)n : (__int128)n;
+    return true;
+}
+
+// An int32 struct field decoded by yaml.v2 v2.2.2 (vendor/gopkg.in/yaml.v2/resolve.go:86-196,
+// decode.go:443-465): null -> 0; a quoted scalar is a string (type error); a plain scalar
+// resolves by its first character: digits / sign -> underscores dropped, ParseInt(base 0), then
+// ParseUint (too big for int32 anyway), then a YAML-style float (truncated toward zero), then
+// 0b / -0b binary; '.' -> a float; the resolve map (bools, nulls, .inf, .nan) and anything else
+// -> not an int32.  The result must fit int32 (OverflowInt).
+bool yaml_int32(const YNode* n, int32_t* out) {
+    *out = 0;
+    if (!n || n->kind == YNode::kNull) return true;
+    if (n->kind != YNode::kScalar || n->quoted) return false;
+    const std::string& in = n->scalar;
+    static const char* kNulls[] = {"", "~", "null", "Null", "NULL"};
+    for (const char* z : kNulls)
+        if (in == z) return true;
+    if (in.empty()) return true;
+    auto fits = [&](__int128 v) {
+        if (v < INT32_MIN || v > INT32_MAX) return false;
+        *out = (int32_t)v;
+        return true;
+    };
+    auto from_float = [&](double f) {  // decode.go: resolved <= MaxInt64 && !OverflowInt(int64(f))
+        if (!(f <= 9223372036854775807.0) || f < -2147483649.0) return false;
+        return fits((__int128)(int64_t)f);
+    };
+    auto float_syntax = [](const std::string& t, size_t i) {  // ^[-+]?[0-9]*\.?[0-9]+([eE][-+][0-9]+)?$
+        if (i < t.size() && (t[i] == '+' || t[i] == '-')) i++;
+        size_t a = i;
+        while (i < t.size() && std::isdigit((unsigned char)t[i])) i++;
+        const size_t int_digits = i - a;
+        if (i < t.size() && t[i] == '.') {
+            i++;
+            size_t b = i;
+            while (i < t.size() && std::isdigit((unsigned char)t[i])) i++;
+            if (i == b) return false;
+        } else if (int_digits == 0) {
+            return false;
+        }
+        if (i < t.size() && (t[i] == 'e' || t[i] == 'E')) {
+            i++;
+            if (i >= t.size() || (t[i] != '+' && t[i] != '-')) return false;
+            i++;
+            size_t b = i;
+            while (i < t.size() && std::isdigit((unsigned char)t[i])) i++;
+            if (i == b) return false;
+        }
+        return i == t.size();
+    };
+    const char c0 = in[0];
+    if (c0 == '.') {  // ParseFloat(in): ".5", ".5e3", ".5E-2" (".inf" / ".nan" are map entries: no int)
+        size_t i = 1, b = 1;
+        while (i < in.size() && std::isdigit((unsigned char)in[i])) i++;
+        if (i == b) return false;
+        if (i < in.size() && (in[i] == 'e' || in[i] == 'E')) {
+            i++;
+            if (i < in.size() && (in[i] == '+' || in[i] == '-')) i++;
+            size_t e = i;
+            while (i < in.size() && std::isdigit((unsigned char)in[i])) i++;
+            if (i == e) return false;
+        }
+        if (i != in.size()) return false;
+        return from_float(std::strtod(in.c_str(), nullptr));
+    }
+    if (!(std::isdigit((unsigned char)c0) || c0 == '+' || c0 == '-')) return false;  // bools, words: strings
+    {  // a timestamp (four digits then '-') never decodes into an int
+        size_t i = 0;
+        while (i < in.size() && std::isdigit((unsigned char)in[i])) i++;
+        if (i == 4 && i < in.size() && in[i] == '-') return false;
+    }
+    std::string plain;
+    for (char c : in)
+        if (c != '_') plain += c;
+    __int128 v = 0;
+    bool big = false;
+    if (go_parse_int(plain, &v, &big)) return !big && fits(v);  // ParseUint only adds >= 2^63
+    if (float_syntax(plain, 0)) return from_float(std::strtod(plain.c_str(), nullptr));
+    if (plain.compare(0, 2, "0b") == 0 || plain.compare(0, 3, "-0b") == 0) {
+        const bool neg = plain[0] == '-';
+        const std::string d = plain.substr(neg ? 3 : 2);
+        if (d.empty()) return false;
+        unsigned __int128 n = 0;
+        for (char c : d) {
+            if (c != '0' && c != '1') return false;
+            if (n <= ((unsigned __int128)1 << 70)) n = n * 2 + (c - '0');
+        }
+        return fits(neg ? -(__int128)n : (__int128)n);
+    }
+    return false;
+}
+
 int resource_index(const std::string& name) {
     if (name == "cpu") return 0;
     if (name == "memory") return 1;
@@ -461,23 +588,20 @@ ks_status ks_parse_simspec(const char* yaml, int32_t max_phases, int32_t* n_phas
     int32_t n = 0;
     for (const auto& ph : doc->seq) {
         const YNode* ru = ph->kind == YNode::kMap ? ph->get("resourceUsage") : nullptr;
-        if (!ru || ru->kind == YNode::kNull || ru->kind == YNode::kScalar) {  // spec.go:48-50
+        if (ru && ru->kind != YNode::kNull && ru->kind != YNode::kMap) {  // yaml.v2: cannot unmarshal into a map
+            set_err(err, err_len, "resourceUsage is not a mapping");
+            return KS_EINVAL;
+        }
+        if (!ru || ru->kind == YNode::kNull) {  // spec.go:48-50
             set_err(err, err_len, "Invalid spec.resoruceUsage field");
             return KS_EINVAL;
         }
-        int64_t sec = 0;
-        if (const YNode* s = ph->get("seconds")) {
-            if (s->kind != YNode::kScalar) {
-                set_err(err, err_len, "seconds is not an integer");
-                return KS_EINVAL;
-            }
-            char* q = nullptr;
-            errno = 0;
-            sec = std::strtoll(s->scalar.c_str(), &q, 10);
-            if (s->scalar.empty() || *q != 0 || sec < INT32_MIN || sec > INT32_MAX) {
-                set_err(err, err_len, "seconds %s is not an int32", s->scalar.c_str());
-                return KS_EINVAL;
-            }
+        int32_t sec = 0;
+        if (!yaml_int32(ph->get("seconds"), &sec)) {  // yaml.v2 int32 field decoding
+            const YNode* s = ph->get("seconds");
+            set_err(err, err_len, "cannot unmarshal seconds %s%s%s into int32", s && s->quoted ? "\"" : "",
+                    s && s->kind == YNode::kScalar ? s->scalar.c_str() : "(non-scalar)", s && s->quoted ? "\"" : "");
+            return KS_EINVAL;
         }
         int64_t use[3] = {0, 0, 0};
         uint8_t mask = 0;

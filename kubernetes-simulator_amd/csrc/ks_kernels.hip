@@ -1013,27 +1013,115 @@ __global__ __launch_bounds__(256) void flush_kernel(NodeSoA s, const PodRec* pod
 }
 
 // Per-node usage at tick t: Σ over running pods of the current simSpec phase's usage
-// (kubesim/pod/pod.go:47-63; int32 passed seconds vs int32 cumulative phase seconds).
-__global__ __launch_bounds__(256) void usage_kernel(int64_t q_lo, int64_t q_hi, int64_t t, int32_t tick_s,
-                                                     const int32_t* b_node, const int32_t* b_status,
-                                                     const int64_t* t0, const int32_t* dur, const int32_t* phase_off,
-                                                     const int32_t* cum_sec, const int64_t* use,
-                                                     unsigned long long* usage) {
-    for (int64_t q = q_lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < q_hi;
-         q += (int64_t)gridDim.x * blockDim.x) {
-        if (b_status[q] != 0) continue;
-        const int64_t dt = t - t0[q];
-        if (dt < 0 || dt >= dur[q]) continue;
-        const int32_t passed = (int32_t)(dt * tick_s);
-        for (int32_t f = phase_off[q]; f < phase_off[q + 1]; ++f) {
-            if (passed < cum_sec[f]) {
-                const int32_t nd = b_node[q];
-                atomicAdd(&usage[nd * 3 + 0], (unsigned long long)use[(int64_t)f * 3 + 0]);
-                atomicAdd(&usage[nd * 3 + 1], (unsigned long long)use[(int64_t)f * 3 + 1]);
-                atomicAdd(&usage[nd * 3 + 2], (unsigned long long)use[(int64_t)f * 3 + 2]);
-                break;
+// (kubesim/pod/pod.go:47-63; int32 passed seconds vs int32 cumulative phase seconds), scattered
+// into the node rows with 64-bit atomic adds (exact).  Grid: the host's candidate blocks of
+// kUsageBlk pods (only blocks holding a pod that may still run at t), pods < q_hi (bound by t).
+constexpr int kUsageBlk = 256;
+__global__ __launch_bounds__(kUsageBlk) void usage_kernel(const int32_t* __restrict__ blocks, int64_t q_hi, int64_t t,
+                                                           int32_t tick_s, const int32_t* b_node, const int32_t* b_status,
+                                                           const int64_t* t0, const int32_t* dur,
+                                                           const int32_t* phase_off, const int32_t* cum_sec,
+                                                           const int64_t* use, unsigned long long* usage) {
+    const int64_t q = (int64_t)blocks[blockIdx.x] * kUsageBlk + threadIdx.x;
+    if (q >= q_hi || b_status[q] != 0) return;
+    const int64_t dt = t - t0[q];
+    if (dt < 0 || dt >= dur[q]) return;
+    const int32_t passed = (int32_t)(dt * tick_s);
+    for (int32_t f = phase_off[q]; f < phase_off[q + 1]; ++f) {
+        if (passed < cum_sec[f]) {
+            const int64_t nd = b_node[q];
+            atomicAdd(&usage[nd * 3 + 0], (unsigned long long)use[(int64_t)f * 3 + 0]);
+            atomicAdd(&usage[nd * 3 + 1], (unsigned long long)use[(int64_t)f * 3 + 1]);
+            atomicAdd(&usage[nd * 3 + 2], (unsigned long long)use[(int64_t)f * 3 + 2]);
+            break;
+        }
+    }
+}
+
+// Per-tick usage digest over ticks [t_lo, t_hi) (ks_usage_digest): each running pod's phases
+// are piecewise constant in t, so a phase active over ticks [a, b) adds +u at a and -u at b
+// of a difference array (six of them: Σ usage[k] and Σ mix(node) * usage[k], mod 2^64), and
+// one prefix sum gives every tick.  Regular pods (non-negative phases, no int32 wrap): phase f
+// is active iff c_{f-1} <= (t - t0) * tick < c_f, i.e. t - t0 in [ceil(c_{f-1}/tick),
+// ceil(c_f/tick)); others are evaluated tick by tick with the reference's int32 arithmetic.
+__device__ __forceinline__ uint64_t node_mix(int64_t node) {
+    uint64_t z = (uint64_t)(node + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ void digest_add(unsigned long long* diff, int64_t T1, int64_t lo, int64_t hi,
+                                           const int64_t* u, uint64_t w) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const uint64_t v = (uint64_t)u[k];
+        if (!v) continue;
+        atomicAdd(&diff[k * T1 + lo], (unsigned long long)v);
+        atomicAdd(&diff[k * T1 + hi], (unsigned long long)(0ull - v));
+        const uint64_t vw = v * w;
+        atomicAdd(&diff[(3 + k) * T1 + lo], (unsigned long long)vw);
+        atomicAdd(&diff[(3 + k) * T1 + hi], (unsigned long long)(0ull - vw));
+    }
+}
+__global__ __launch_bounds__(kUsageBlk) void usage_digest_kernel(
+    const int32_t* __restrict__ blocks, int64_t q_hi, int64_t t_lo, int64_t t_hi, int32_t tick_s,
+    const int32_t* b_node, const int32_t* b_status, const int64_t* t0, const int32_t* dur, const uint8_t* preg,
+    const int32_t* phase_off, const int32_t* cum_sec, const int64_t* use, unsigned long long* diff) {
+    const int64_t q = (int64_t)blocks[blockIdx.x] * kUsageBlk + threadIdx.x;
+    if (q >= q_hi || b_status[q] != 0) return;
+    const int64_t d = dur[q];
+    if (d <= 0) return;
+    const int64_t s = t0[q];
+    const int64_t a0 = max(s, t_lo), a1 = min(s + d, t_hi);
+    if (a0 >= a1) return;
+    const uint64_t w = node_mix(b_node[q]);
+    const int64_t T1 = t_hi - t_lo + 1;
+    const int32_t f0 = phase_off[q], f1 = phase_off[q + 1];
+    if (preg[q]) {
+        int64_t c_prev = 0;
+        for (int32_t f = f0; f < f1; ++f) {
+            const int64_t c = cum_sec[f];
+            if (c > c_prev) {
+                const int64_t lo = max(a0, s + (c_prev + tick_s - 1) / tick_s);
+                const int64_t hi = min(a1, s + (c + tick_s - 1) / tick_s);
+                if (lo < hi) digest_add(diff, T1, lo - t_lo, hi - t_lo, use + (int64_t)f * 3, w);
+                c_prev = c;
             }
         }
+    } else {
+        for (int64_t t = a0; t < a1; ++t) {
+            const int32_t passed = (int32_t)((t - s) * tick_s);
+            for (int32_t f = f0; f < f1; ++f)
+                if (passed < cum_sec[f]) {
+                    digest_add(diff, T1, t - t_lo, t - t_lo + 1, use + (int64_t)f * 3, w);
+                    break;
+                }
+        }
+    }
+}
+
+// Prefix sums of the six difference arrays ([6][T + 1]) into out[T][6]: one workgroup per
+// array, each thread a contiguous chunk, a workgroup scan of the chunk sums.
+__global__ __launch_bounds__(1024) void digest_scan_kernel(const unsigned long long* __restrict__ diff, int64_t T,
+                                                            unsigned long long* __restrict__ out) {
+    __shared__ unsigned long long part[1024];
+    const int k = blockIdx.x, tid = threadIdx.x;
+    const unsigned long long* d = diff + (int64_t)k * (T + 1);
+    const int64_t chunk = (T + 1023) / 1024, lo = min<int64_t>(T, tid * chunk), hi = min<int64_t>(T, lo + chunk);
+    unsigned long long s = 0;
+    for (int64_t i = lo; i < hi; ++i) s += d[i];
+    part[tid] = s;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const unsigned long long v = tid >= off ? part[tid - off] : 0ull;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    unsigned long long run = tid ? part[tid - 1] : 0ull;
+    for (int64_t i = lo; i < hi; ++i) {
+        run += d[i];
+        out[i * 6 + k] = run;
     }
 }
 
@@ -1181,13 +1269,27 @@ hipError_t launch_flush(const NodeSoA& s, const PodRec* pods, const int64_t* fin
     return hipGetLastError();
 }
 
-hipError_t launch_usage(int64_t q_lo, int64_t q_hi, int64_t t, int32_t tick_s, const int32_t* b_node,
-                        const int32_t* b_status, const int64_t* t0, const int32_t* dur, const int32_t* phase_off,
-                        const int32_t* cum_sec, const int64_t* use, unsigned long long* usage, hipStream_t st) {
-    if (q_hi <= q_lo) return hipSuccess;
-    const int64_t blocks = std::min<int64_t>((q_hi - q_lo + 255) / 256, 2048);
-    hipLaunchKernelGGL(usage_kernel, dim3((unsigned)blocks), dim3(256), 0, st, q_lo, q_hi, t, tick_s, b_node, b_status,
-                       t0, dur, phase_off, cum_sec, use, usage);
+int usage_block_pods() { return kUsageBlk; }
+
+hipError_t launch_usage(const int32_t* blocks, int64_t nblocks, int64_t q_hi, int64_t t, int32_t tick_s,
+                        const int32_t* b_node, const int32_t* b_status, const int64_t* t0, const int32_t* dur,
+                        const int32_t* phase_off, const int32_t* cum_sec, const int64_t* use,
+                        unsigned long long* usage, hipStream_t st) {
+    if (nblocks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(usage_kernel, dim3((unsigned)nblocks), dim3(kUsageBlk), 0, st, blocks, q_hi, t, tick_s, b_node,
+                       b_status, t0, dur, phase_off, cum_sec, use, usage);
+    return hipGetLastError();
+}
+
+hipError_t launch_usage_digest(const int32_t* blocks, int64_t nblocks, int64_t q_hi, int64_t t_lo, int64_t t_hi,
+                               int32_t tick_s, const int32_t* b_node, const int32_t* b_status, const int64_t* t0,
+                               const int32_t* dur, const uint8_t* preg, const int32_t* phase_off,
+                               const int32_t* cum_sec, const int64_t* use, unsigned long long* diff,
+                               unsigned long long* out, hipStream_t st) {
+    if (nblocks > 0)
+        hipLaunchKernelGGL(usage_digest_kernel, dim3((unsigned)nblocks), dim3(kUsageBlk), 0, st, blocks, q_hi, t_lo,
+                           t_hi, tick_s, b_node, b_status, t0, dur, preg, phase_off, cum_sec, use, diff);
+    hipLaunchKernelGGL(digest_scan_kernel, dim3(6), dim3(1024), 0, st, diff, t_hi - t_lo, out);
     return hipGetLastError();
 }
 }  // namespace ks

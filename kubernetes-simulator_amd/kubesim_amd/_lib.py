@@ -17,7 +17,7 @@ KS_FILTER_FIT, KS_FILTER_TAINT, KS_FILTER_SELECTOR = 1, 2, 4
 KS_SCORER_CONST, KS_SCORER_LEAST_REQUESTED, KS_SCORER_BALANCED = 0, 1, 2
 KS_POD_OK, KS_POD_OVER_CAPACITY = 0, 1
 KS_PODFLAG_BAD_KEY, KS_PODFLAG_BAD_SPEC = 1, 2
-KS_ABI_VERSION = 1
+KS_ABI_VERSION = 2
 KS_ENGINE_FORCE_WIDE = 1
 KS_ENGINE_NO_TINY = 2
 KS_ENGINE_NO_MICRO = 4
@@ -32,6 +32,7 @@ EXPORTED_SYMBOLS = ("ks_create", "ks_destroy", "ks_load_nodes", "ks_submit_pods"
                     "ks_last_error", "ks_last_step_stats", "ks_set_profiling", "ks_debug_counters", "ks_selftest",
                     "ks_comm_unique_id", "ks_shard", "ks_group_create", "ks_group_destroy",
                     "ks_group_add", "ks_group_size", "ks_group_step", "ks_pod_status",
+                    "ks_usage_at", "ks_usage_digest", "ks_node_mix", "ks_pod_lookup", "ks_node_pods",
                     # include/ks_ingest.h
                     "ks_parse_quantity", "ks_parse_simspec", "ks_cluster_parse", "ks_cluster_free",
                     "ks_cluster_nodes", "ks_cluster_tick", "ks_cluster_start_clock", "ks_cluster_arrays",
@@ -84,12 +85,19 @@ def load():
     L.ks_destroy.argtypes = [p]
     L.ks_destroy.restype = None
     L.ks_load_nodes.argtypes = [p, C.c_int64, p, p, p]
-    L.ks_submit_pods.argtypes = [p, C.c_int64] + [p] * 9
+    L.ks_submit_pods.argtypes = [p, C.c_int64] + [p] * 10
     L.ks_step.argtypes = [p, C.c_int64, p, C.c_int64, C.POINTER(C.c_int64)]
     L.ks_filter.argtypes = [p, C.c_int64, p]
     L.ks_score.argtypes = [p, C.c_int64, p]
     L.ks_usage.argtypes = [p, p]
-    for f in ("ks_load_nodes", "ks_submit_pods", "ks_step", "ks_filter", "ks_score", "ks_usage"):
+    L.ks_usage_at.argtypes = [p, C.c_int64, p]
+    L.ks_usage_digest.argtypes = [p, C.c_int64, C.c_int64, p]
+    L.ks_node_mix.argtypes = [C.c_int64]
+    L.ks_node_mix.restype = C.c_uint64
+    L.ks_pod_lookup.argtypes = [p, C.c_int32, C.c_int64, C.POINTER(C.c_int64)]
+    L.ks_node_pods.argtypes = [p, C.c_int32, p, C.c_int64, C.POINTER(C.c_int64)]
+    for f in ("ks_load_nodes", "ks_submit_pods", "ks_step", "ks_filter", "ks_score", "ks_usage", "ks_usage_at",
+              "ks_usage_digest", "ks_pod_lookup", "ks_node_pods"):
         getattr(L, f).restype = C.c_int
     L.ks_current_tick.argtypes = [p]
     L.ks_current_tick.restype = C.c_int64

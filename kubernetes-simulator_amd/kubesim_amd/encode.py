@@ -150,7 +150,8 @@ def encode_pods(pods: dict, taint_dict, label_dict):
                 keymask=keymask, tol=tolmask, sel=selmask,
                 phase_off=pods["phase_off"].astype(np.int32),
                 phase_sec=pods["phase_sec"].astype(np.int32),
-                phase_use=np.ascontiguousarray(use), flags=pods["flags"].astype(np.uint8))
+                phase_use=np.ascontiguousarray(use), flags=pods["flags"].astype(np.uint8),
+                key_id=np.asarray(pods["key_id"], dtype=np.int64) if "key_id" in pods else None)
 
 
 def encode_trace(trace: dict):

@@ -116,20 +116,43 @@ class Engine:
                                           _p(_c(label, np.uint64))))
 
     def submit(self, pods: dict):
-        """Append encoded pods (see kubesim_amd.encode.encode_pods)."""
-        m = pods["m"]
+        """Append encoded pods (see kubesim_amd.encode.encode_pods).  ``key_id`` (optional,
+        int64 per pod): interned namespace-name keys; absent/None = every pod its own key."""
+        m = int(pods["m"])
         arrs = [_c(pods["arrival"], np.int64), _c(pods["req"], np.int64).reshape(-1, 3),
                 _c(pods["keymask"], np.uint8), _c(pods["tol"], np.uint64), _c(pods["sel"], np.uint64),
                 _c(pods["phase_off"], np.int32), _c(pods["phase_sec"], np.int32),
                 _c(pods["phase_use"], np.int64).reshape(-1, 3), _c(pods["flags"], np.uint8)]
-        self._check(self._L.ks_submit_pods(self.h, m, *[_p(a) for a in arrs]))
+        keys = pods.get("key_id")
+        if keys is not None:
+            keys = _c(keys, np.int64)
+        # the C side reads these lengths blindly: check them here
+        per_pod = {"arrival": arrs[0], "req": arrs[1], "keymask": arrs[2], "tol": arrs[3], "sel": arrs[4],
+                   "flags": arrs[8]}
+        if keys is not None:
+            per_pod["key_id"] = keys
+        for name, a in per_pod.items():
+            if len(a) != m:
+                raise ValueError(f"pods[{name!r}] has {len(a)} rows, expected m = {m}")
+        off = arrs[5]
+        if len(off) != m + 1:
+            raise ValueError(f"pods['phase_off'] has {len(off)} entries, expected m + 1 = {m + 1}")
+        nf = int(off[-1]) if m else 0
+        if m and (off[0] != 0 or (np.diff(off) < 0).any()):
+            raise ValueError("pods['phase_off'] must start at 0 and be non-decreasing")
+        if len(arrs[6]) < nf or len(arrs[7]) < nf:
+            raise ValueError(f"phase arrays shorter than phase_off[-1] = {nf}")
+        ptrs = [_p(a) for a in arrs] + [_p(keys) if keys is not None else None]
+        self._check(self._L.ks_submit_pods(self.h, m, *ptrs))
         self._submitted += m
 
     # -- tick loop ---------------------------------------------------------------------------
     def step(self, ticks: int, cap: int | None = None):
         """Advance ``ticks`` ticks; returns binds as a structured numpy array
-        (pod, node, status, tick)."""
-        cap = ticks if cap is None else cap
+        (pod, node, status, tick).  ``cap`` defaults to the binds the step can make (at most one
+        per tick and one per queued pod)."""
+        if cap is None:
+            cap = max(0, min(ticks, self.queued))
         out = (KsBind * max(cap, 1))()
         n = C.c_int64(0)
         rc = self._L.ks_step(self.h, ticks, out, cap, C.byref(n))
@@ -153,6 +176,32 @@ class Engine:
         out = np.zeros((self.n, 3), np.int64)
         self._check(self._L.ks_usage(self.h, _p(out)))
         return out
+
+    def usage_at(self, t: int):
+        """Per-node usage [n][3] at any past tick 0 <= t <= the current tick."""
+        out = np.zeros((self.n, 3), np.int64)
+        self._check(self._L.ks_usage_at(self.h, t, _p(out)))
+        return out
+
+    def usage_digest(self, t_lo: int, t_hi: int):
+        """[t_hi - t_lo][6] uint64: per tick Σ_n usage[n][k] (k < 3) and Σ_n mix(n) usage[n][k-3]."""
+        out = np.zeros((max(t_hi - t_lo, 0), 6), np.uint64)
+        self._check(self._L.ks_usage_digest(self.h, t_lo, t_hi, _p(out)))
+        return out
+
+    def pod_lookup(self, node: int, key_id: int):
+        """Node.GetPod: FIFO index of the pod stored on ``node`` under ``key_id`` (KsError NotFound)."""
+        q = C.c_int64(-1)
+        self._check(self._L.ks_pod_lookup(self.h, node, key_id, C.byref(q)))
+        return q.value
+
+    def node_pods(self, node: int):
+        """Node.GetPodList: FIFO indices of the pods stored on ``node`` (one per key)."""
+        n = C.c_int64(0)
+        self._check(self._L.ks_node_pods(self.h, node, None, 0, C.byref(n)))
+        out = np.zeros(max(n.value, 1), np.int64)
+        self._check(self._L.ks_node_pods(self.h, node, _p(out), n.value, C.byref(n)))
+        return out[:n.value].copy()
 
     def pod_status(self, pod_lo: int = 0, n: int | None = None):
         """Pod.BuildStatus phases (kubesim/pod/pod.go:78-145) at the current tick: structured

@@ -17,6 +17,7 @@ TEST INFRASTRUCTURE ONLY (pins the units and ingest rules the traces use).
 """
 from __future__ import annotations
 
+import re
 from fractions import Fraction
 
 import yaml
@@ -120,17 +121,103 @@ def build_resource_list(d: dict) -> dict:
     return out
 
 
+_GO_FLOAT = re.compile(r"^[-+]?[0-9]*\.?[0-9]+([eE][-+][0-9]+)?$")   # resolve.go:84
+_NULLS = {"", "~", "null", "Null", "NULL"}
+
+
+def _go_parse_int(s: str):
+    """strconv.ParseInt(s, 0, 64) of Go 1.11: value, or None on a syntax error (a magnitude
+    >= 2^63 is returned as is: it can never decode into an int32)."""
+    neg = s[:1] == "-"
+    if s[:1] in "+-" and s:
+        s = s[1:]
+    if not s:
+        return None
+    if len(s) > 1 and s[0] == "0" and s[1] in "xX":
+        if len(s) < 3:
+            return None
+        base, digits = 16, s[2:]
+    elif s[0] == "0":
+        base, digits = 8, s[1:]
+    else:
+        base, digits = 10, s
+    v = 0
+    for c in digits:
+        d = int(c, 36) if c.isascii() and c.isalnum() else 99
+        if d >= base:
+            return None
+        v = v * base + d
+    return -v if neg else v
+
+
+def yaml_int32(node):
+    """An int32 field as yaml.v2 v2.2.2 decodes it (resolve.go:86-196, decode.go:443-465);
+    ``node`` is a PyYAML composed node or None.  Raises QuantityError when it is no int32."""
+    if node is None or (isinstance(node, yaml.ScalarNode) and node.tag == "tag:yaml.org,2002:null"
+                        and node.style is None and node.value in _NULLS):
+        return 0
+    if not isinstance(node, yaml.ScalarNode):
+        raise QuantityError("seconds is not a scalar")
+    if node.style is not None:   # quoted: a !!str, which no int field accepts
+        raise QuantityError(f"cannot unmarshal !!str `{node.value}` into int32")
+    s = node.value
+    if s in _NULLS:
+        return 0
+
+    def fits(v):
+        if not -(1 << 31) <= v < (1 << 31):
+            raise QuantityError(f"seconds {s} overflows int32")
+        return v
+
+    def from_float(f):
+        if not f <= 9223372036854775807.0 or f < -(1 << 63):
+            raise QuantityError(f"seconds {s} overflows int32")
+        return fits(int(f))   # Go's int64(float64) truncates toward zero
+
+    if s[0] == ".":
+        if not re.fullmatch(r"\.[0-9]+([eE][-+]?[0-9]+)?", s):
+            raise QuantityError(f"seconds {s} is not a number")
+        return from_float(float(s))
+    if not (s[0].isdigit() or s[0] in "+-"):
+        raise QuantityError(f"seconds {s} is not an int")   # bools, words, .inf ...
+    if re.match(r"^[0-9]{4}-", s):
+        raise QuantityError(f"seconds {s} is a timestamp")
+    plain = s.replace("_", "")
+    v = _go_parse_int(plain)
+    if v is not None:
+        return fits(v)
+    if _GO_FLOAT.match(plain):
+        return from_float(float(plain))
+    for pre, sign in (("0b", 1), ("-0b", -1)):
+        if plain.startswith(pre) and plain[len(pre):] and set(plain[len(pre):]) <= {"0", "1"}:
+            return fits(sign * int(plain[len(pre):], 2))
+    raise QuantityError(f"seconds {s} is not an int")
+
+
+def _plain(node):
+    """literal text of the scalars of a composed node (decode.go:420-428: scalars decode into
+    strings as their text), or the node itself when not a mapping/sequence/scalar"""
+    if isinstance(node, yaml.MappingNode):
+        return {k.value: _plain(v) for k, v in node.value}
+    if isinstance(node, yaml.SequenceNode):
+        return [_plain(v) for v in node.value]
+    return None if (node.style is None and node.value in _NULLS) else node.value
+
+
 def parse_simspec(text: str):
-    doc = yaml.load(text, Loader=yaml.BaseLoader)
-    if doc is None:
+    root = yaml.compose(text, Loader=yaml.BaseLoader)
+    if root is None:
         return []
+    if not isinstance(root, yaml.SequenceNode):
+        raise QuantityError("simSpec is not a YAML list")
     phases = []
-    for item in doc:
-        ru = item.get("resourceUsage") if isinstance(item, dict) else None
-        if ru is None or not isinstance(ru, dict):
+    for item in root.value:
+        fields = {k.value: v for k, v in item.value} if isinstance(item, yaml.MappingNode) else {}
+        ru = fields.get("resourceUsage")
+        if ru is not None and isinstance(ru, yaml.SequenceNode):
+            raise QuantityError("resourceUsage is not a mapping")   # yaml.v2 type error
+        if ru is None or not isinstance(ru, yaml.MappingNode):
             raise InvalidResourceUsageField("Invalid spec.resoruceUsage field")
-        sec = int(item.get("seconds", "0"))
-        if not -(1 << 31) <= sec < (1 << 31):
-            raise QuantityError("seconds out of int32 range")
-        phases.append((sec, build_resource_list(ru)))
+        sec = yaml_int32(fields.get("seconds"))
+        phases.append((sec, build_resource_list({k: ("" if v is None else v) for k, v in _plain(ru).items()})))
     return phases

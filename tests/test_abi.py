@@ -56,3 +56,13 @@ def test_engine_refuses_without_library(monkeypatch, tmp_path):
     with pytest.raises(ImportError):
         _lib.load()
     importlib.reload(_lib)
+
+
+def test_node_mix_matches_documented_formula():
+    """ks_node_mix is a pure function (no device): the digest's node weight as the header
+    spells it out."""
+    from kubesim_amd import _lib
+    from usage_digest import node_mix
+    L = _lib.load()
+    for nd in (0, 1, 2, 63, 50_000, (1 << 24) - 1):
+        assert L.ks_node_mix(nd) == node_mix(nd)

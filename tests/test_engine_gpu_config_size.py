@@ -1,0 +1,176 @@
+"""GPU parity at the BASELINE.json configurations' full sizes (C3, C4).
+
+C3 (50k nodes, 1M-pod trace, Filter fit+taint+selector -> LR+BA):
+  * the first 40,000 pods bind-for-bind against the OpenMP oracle, with usage checked at sampled
+    ticks of the run through ks_usage_at (the oracle stepped to each sample tick);
+  * the WHOLE 1M-pod trace: the engine at the default batch and at a batch of 97 pods give
+    identical binds (an exact resolver's results cannot depend on how the FIFO is cut into
+    batches), plus invariants that hold for any exact implementation of the reference's loop —
+    FIFO order, one bind per tick, every bind Ok under the fit filter (admission is exactly that
+    predicate, kubesim/node/node.go:44-47), chosen nodes satisfy the pod's taint / selector
+    filters, and the running pods' requests recomputed on the host from the binds never exceed
+    any node's capacity; the per-tick usage digest agrees with ks_usage_at at sampled ticks.
+C4 (1024 what-if scenarios x 2,000 nodes x 10,000 pods, one group, the default batch — so the
+  half-size RSmall resolver and the group-wide pods-per-workgroup are the ones exercised):
+  16 scenarios spread over the group bind-for-bind and usage-for-usage against the oracle over
+  their whole traces, every scenario checked with the invariants above.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from harness import assert_same_binds, encoded, make_engine, make_oracle
+from kubesim_amd import tracegen
+
+pytestmark = pytest.mark.gpu
+MODE = "feeds_all_lrba"
+SCORERS = ((1, 1, 0), (2, 1, 0))
+
+
+def _threads():
+    return int(os.environ.get("OMP_NUM_THREADS") or 0) or min(os.cpu_count() or 1, 16)
+
+
+def _check_invariants(binds, first_pod, n_nodes, enc, last_tick=0):
+    p = enc["pods"]
+    tol = p["tol"].astype(np.uint64)
+    sel = p["sel"].astype(np.uint64)
+    taint = enc["taint"].astype(np.uint64)
+    label = enc["label"].astype(np.uint64)
+    np.testing.assert_array_equal(binds["pod"], np.arange(first_pod, first_pod + len(binds)))
+    if len(binds):
+        assert (np.diff(binds["tick"]) > 0).all() and binds["tick"][0] > last_tick
+    assert (binds["status"] == 0).all()
+    nd, q = binds["node"], binds["pod"]
+    assert ((nd >= 0) & (nd < n_nodes)).all()
+    assert ((taint[nd] & ~tol[q]) == 0).all()
+    assert ((label[nd] & sel[q]) == sel[q]).all()
+
+
+def _dur_ticks(enc, tick_seconds):
+    p = enc["pods"]
+    S = np.add.reduceat(p["phase_sec"].astype(np.int64), p["phase_off"][:-1]) if len(p["phase_sec"]) else 0
+    S = np.where(np.diff(p["phase_off"]) > 0, S, 0)
+    return np.where(S > 0, -(-S // tick_seconds), 0)
+
+
+def _check_capacity(binds, enc, dur, t, n_nodes):
+    """Requests of the pods running at tick t (bound Ok, t0 <= t < t0 + dur), per node, recomputed
+    on the host: never above capacity, running count never above the pods capacity."""
+    q, t0 = binds["pod"], binds["tick"]
+    run = (t0 <= t) & (t < t0 + dur[q]) & (binds["status"] == 0)
+    req = enc["pods"]["req"].reshape(-1, 3)
+    alloc = enc["alloc"]
+    tot = np.zeros((n_nodes, 3), np.int64)
+    np.add.at(tot, binds["node"][run], req[q[run]])
+    nr = np.bincount(binds["node"][run], minlength=n_nodes)
+    for k in range(3):
+        has = alloc[:, k] >= 0
+        assert (tot[has, k] <= alloc[has, k]).all(), f"resource {k} over capacity at tick {t}"
+    assert (nr <= alloc[:, 3]).all()
+
+
+@pytest.fixture(scope="module")
+def c3():
+    tr = tracegen.c3_trace(n_nodes=50_000, n_pods=1_000_000)
+    return tr, encoded(tr)
+
+
+def test_c3_40k_pods_bit_exact_with_usage_samples(c3):
+    tr, enc = c3
+    P = 40_000
+    eng = make_engine(tr, enc, MODE)
+    eng.submit(enc["pods"])
+    ora = make_oracle(tr, MODE)
+    ora.set_threads(_threads())
+    ora.submit(tracegen.slice_pods(tr, 0, P))
+    eb = eng.step(P)
+    samples = (1, 977, 5000, 12_345, 25_000, P)
+    obs, t = [], 0
+    for s in samples:
+        b, rc = ora.step(s - t, cap=s - t)
+        assert rc == 0
+        obs.append(b)
+        t = s
+        np.testing.assert_array_equal(eng.usage_at(s), ora.usage(), err_msg=f"usage at tick {s}")
+    ob = {k: np.concatenate([x[k] for x in obs]) for k in obs[0]}
+    assert_same_binds(eb, ob)
+
+
+def test_c3_full_trace_batch_independent_and_invariants(c3):
+    tr, enc = c3
+    m, n = tr["pods"]["m"], tr["nodes"]["n"]
+    a = make_engine(tr, enc, MODE)             # default batch (256)
+    a.submit(enc["pods"])
+    b = make_engine(tr, enc, MODE, batch_pods=97)
+    b.submit(enc["pods"])
+    dur = _dur_ticks(enc, tr["tick_seconds"])
+    done, last_tick, allb = 0, 0, []
+    for chunk in (200_000,) * 5:
+        ea = a.step(chunk)
+        eb = b.step(chunk)
+        np.testing.assert_array_equal(ea, eb)
+        _check_invariants(ea, done, n, enc, last_tick)
+        allb.append(ea)
+        done += len(ea)
+        last_tick = int(ea["tick"][-1])
+        sofar = np.concatenate(allb)
+        _check_capacity(sofar, enc, dur, last_tick, n)
+        _check_capacity(sofar, enc, dur, last_tick - 4321, n)
+    assert done == m
+    # the per-tick usage digest against ks_usage_at at sampled ticks of the last 100k ticks
+    lo = last_tick - 100_000
+    dg = a.usage_digest(lo, last_tick + 1)
+    for t in (lo, lo + 1, lo + 31_337, last_tick - 1, last_tick):
+        u = a.usage_at(t)
+        np.testing.assert_array_equal(dg[t - lo, :3], u.sum(axis=0).astype(np.uint64))
+
+
+def _group_step_all(g, ticks, chunk):
+    out = None
+    left = ticks
+    while left > 0:
+        k = min(chunk, left)
+        binds, cnt, st, _ = g.step(k)
+        parts = g.split(binds, cnt)
+        out = parts if out is None else [np.concatenate([x, y]) for x, y in zip(out, parts)]
+        left -= k
+        if (st != 0).all():
+            break
+    return out, st
+
+
+def test_c4_1024_scenarios_config_size():
+    from kubesim_amd.engine import Group
+    S, N, P = 1024, 2000, 10_000
+    g = Group(S)
+    traces, encs = [], []
+    for s in range(S):
+        tr = tracegen.c4_scenario(s, n_nodes=N, n_pods=P)
+        enc = encoded(tr)
+        e = g.add(tick_seconds=tr["tick_seconds"], filter_mode=1, filters=7, scorers=SCORERS)
+        e.load_nodes(enc["alloc"], enc["taint"], enc["label"])
+        e.submit(enc["pods"])
+        traces.append(tr)
+        encs.append(enc)
+    per, st = _group_step_all(g, P, 2500)
+    sample = list(range(0, S, S // 16))
+    ok_runs = 0
+    for s in range(S):
+        b = per[s]
+        if st[s] == 0:
+            assert len(b) == P
+            ok_runs += 1
+        _check_invariants(b, 0, N, encs[s])
+    assert ok_runs >= S // 2
+    for s in sample:
+        ora = make_oracle(traces[s], MODE)
+        ora.set_threads(_threads())
+        ora.submit(traces[s])
+        ob, rc = ora.step(P, cap=P)
+        assert rc == int(st[s]), (s, rc, st[s])
+        assert_same_binds(per[s], ob)
+        if rc == 0:
+            np.testing.assert_array_equal(g.members[s].usage(), ora.usage(), err_msg=f"scenario {s}")
+    g.close()

@@ -79,6 +79,50 @@ def test_simspec_edge_cases():
     assert e.value.code == _lib.KS_ERANGE
 
 
+# simSpec `seconds` (an int32 struct field) decoded the way yaml.v2 v2.2.2 does it under Go 1.11,
+# hand-derived from vendor/gopkg.in/yaml.v2/resolve.go:86-196 and decode.go:443-465
+# (None = Unmarshal fails: the pod's bind aborts the run with InvalidArgument).
+SECONDS_KATS = [
+    ("60", 60), ("+60", 60), ("-60", -60), ("0", 0), ("010", 8), ("-010", -8),   # leading 0: octal
+    ("08", 8), ("0999", 999),          # not octal: ParseInt fails, the YAML float rule accepts it
+    ("0x3c", 60), ("0X3C", 60), ("-0x10", -16), ("0x", None),
+    ("1_000", 1000), ("1__0", 10), ("_1", None),           # underscores dropped (hint: first char)
+    ("90.5", 90), ("-90.9", -90), ("1e+3", 1000), ("1E-1", 0), ("1e3", None), ("1.", None),
+    (".5", 0), (".5e3", 500), ("-.5", 0), (".", None),
+    ("0b101", 5), ("-0b101", -5), ("+0b101", None), ("0b", None), ("0o17", None),
+    ("2147483647", 2147483647), ("2147483648", None), ("-2147483648", -2147483648),
+    ("-2147483649", None), ("2147483647.9", 2147483647), ("9223372036854775808", None),
+    ("1e+30", None), ("~", 0), ("null", 0), ("", 0), ("true", None), ("yes", None),
+    (".inf", None), (".nan", None), ("2001-01-01", None), ("ten", None),
+    ('"60"', None), ("'60'", None),                          # quoted: a !!str, not an int
+]
+
+
+@pytest.mark.parametrize("text,want", SECONDS_KATS)
+def test_simspec_seconds_follow_yaml_v2(text, want):
+    doc = f"- seconds: {text}\n  resourceUsage:\n    cpu: 1\n" if text else "- seconds:\n  resourceUsage:\n    cpu: 1\n"
+    if want is None:
+        with pytest.raises(KsError) as e:
+            parse_simspec(doc)
+        assert e.value.code == _lib.KS_EINVAL
+        with pytest.raises(ValueError):
+            Q.parse_simspec(doc)
+    else:
+        assert parse_simspec(doc) == [(want, {"cpu": 1000})]
+        assert [x[0] for x in Q.parse_simspec(doc)] == [want]
+
+
+def test_simspec_resource_usage_must_be_a_mapping():
+    for doc in ("- seconds: 1\n  resourceUsage: []\n", "- seconds: 1\n  resourceUsage:\n  - cpu\n",
+                "- seconds: 1\n  resourceUsage: 5\n", "- seconds: 1\n  resourceUsage: ~\n"):
+        with pytest.raises(KsError) as e:
+            parse_simspec(doc)
+        assert e.value.code == _lib.KS_EINVAL, doc
+        with pytest.raises(ValueError):
+            Q.parse_simspec(doc)
+    assert parse_simspec("- seconds: 1\n  resourceUsage: {}\n") == [(1, {})]
+
+
 CONFIG = """# cluster config in the reference's schema (kubesim/config/config.go:15-41)
 logLevel: debug
 tick: 10
