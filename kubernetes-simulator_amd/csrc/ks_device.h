@@ -65,6 +65,14 @@ struct NodeV {
     uint64_t taint, label;
 };
 
+// The same state in 32-bit fields, for the narrow / tiny / micro domains (every scaled capacity
+// < 2^29, so requested totals of running pods too; the pods capacity clamped to 2^31 - 1, above
+// any running count): half the registers and 32-bit arithmetic in the resolver's owner lanes.
+struct NodeW {
+    int32_t ac, am, ag, ap, rc, rm, rg, nr;
+    uint64_t taint, label;
+};
+
 __device__ __forceinline__ NodeV load_node(const NodeSoA& s, int64_t i) {
     NodeV v;
     v.ac = s.ac[i]; v.am = s.am[i]; v.ag = s.ag[i]; v.ap = s.ap[i];
@@ -206,7 +214,8 @@ __host__ __device__ __forceinline__ int32_t ba_score_n(int32_t Ac, int32_t Am, i
     return q;
 }
 
-__host__ __device__ __forceinline__ uint32_t eval_total1_narrow(const Cfg& c, const PodRec& p, const NodeV& n) {
+template <class NS>
+__host__ __device__ __forceinline__ uint32_t eval_total1_narrow(const Cfg& c, const PodRec& p, const NS& n) {
     if (!c.has_scorers) return 0;
     const int32_t ac = (int32_t)n.ac, am = (int32_t)n.am, ag = (int32_t)n.ag;
     const int32_t rc = (int32_t)n.rc, rm = (int32_t)n.rm, rg = (int32_t)n.rg;
@@ -252,7 +261,8 @@ __host__ __device__ __forceinline__ int32_t div10_tiny(int32_t y, int32_t A, flo
     return q;
 }
 
-__host__ __device__ __forceinline__ uint32_t eval_total1_tiny(const Cfg& c, const PodRec& p, const NodeV& n) {
+template <class NS>
+__host__ __device__ __forceinline__ uint32_t eval_total1_tiny(const Cfg& c, const PodRec& p, const NS& n) {
     // Branch-free: every floor is computed on safe inputs and selected, so the LR / LR / BA
     // chains interleave even when a single lane evaluates (the resolver's bind wave).
     const int32_t ac = (int32_t)n.ac, am = (int32_t)n.am, ag = (int32_t)n.ag;
@@ -321,7 +331,8 @@ __host__ __device__ __forceinline__ int32_t lr10_micro(int32_t x, float r) {
     return (int32_t)fmaf((float)x, r, kMicroBias);
 }
 
-__host__ __device__ __forceinline__ uint32_t eval_total1_micro(const Cfg& c, const PodRec& p, const NodeV& n) {
+template <class NS>
+__host__ __device__ __forceinline__ uint32_t eval_total1_micro(const Cfg& c, const PodRec& p, const NS& n) {
     const int32_t ac = (int32_t)n.ac, am = (int32_t)n.am, ag = (int32_t)n.ag;
     const int32_t rc = (int32_t)n.rc, rm = (int32_t)n.rm, rg = (int32_t)n.rg;
     const int32_t qc = clamp_micro(p.req[0]), qm = clamp_micro(p.req[1]), qg = clamp_micro(p.req[2]);
@@ -359,8 +370,8 @@ __host__ __device__ __forceinline__ uint32_t eval_total1_micro(const Cfg& c, con
 // A larger value is a narrower domain; each evaluator is exact on every narrower domain.
 enum : int { kEvalWide = 0, kEvalNarrow = 1, kEvalTiny = 2, kEvalMicro = 3 };
 
-template <int kMode>
-__host__ __device__ __forceinline__ uint32_t eval_t(const Cfg& c, const PodRec& p, const NodeV& n) {
+template <int kMode, class NS>
+__host__ __device__ __forceinline__ uint32_t eval_t(const Cfg& c, const PodRec& p, const NS& n) {
     if constexpr (kMode == kEvalMicro) return eval_total1_micro(c, p, n);
     else if constexpr (kMode == kEvalTiny) return eval_total1_tiny(c, p, n);
     else if constexpr (kMode == kEvalNarrow) return eval_total1_narrow(c, p, n);
@@ -493,6 +504,8 @@ hipError_t launch_merge(const EngineArgs* d, int S, int B, const uint64_t* lists
 // small: the RSmall resolver (batches <= small_resolver_max_batch() pods, clusters <=
 // small_resolver_max_nodes() nodes; half the LDS, two resolvers per CU)
 hipError_t launch_resolve(const EngineArgs* d, int S, int mode, bool small, hipStream_t st);
+// the speculative resolver (ks_resolve.hip): same contract, same size classes
+hipError_t launch_resolve2(const EngineArgs* d, int S, int mode, bool small, hipStream_t st);
 int small_resolver_max_batch();
 int small_resolver_max_nodes();
 struct BindSeg {
