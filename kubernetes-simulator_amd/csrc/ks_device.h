@@ -65,14 +65,6 @@ struct NodeV {
     uint64_t taint, label;
 };
 
-// The same state in 32-bit fields, for the narrow / tiny / micro domains (every scaled capacity
-// < 2^29, so requested totals of running pods too; the pods capacity clamped to 2^31 - 1, above
-// any running count): half the registers and 32-bit arithmetic in the resolver's owner lanes.
-struct NodeW {
-    int32_t ac, am, ag, ap, rc, rm, rg, nr;
-    uint64_t taint, label;
-};
-
 __device__ __forceinline__ NodeV load_node(const NodeSoA& s, int64_t i) {
     NodeV v;
     v.ac = s.ac[i]; v.am = s.am[i]; v.ag = s.ag[i]; v.ap = s.ap[i];
@@ -504,8 +496,6 @@ hipError_t launch_merge(const EngineArgs* d, int S, int B, const uint64_t* lists
 // small: the RSmall resolver (batches <= small_resolver_max_batch() pods, clusters <=
 // small_resolver_max_nodes() nodes; half the LDS, two resolvers per CU)
 hipError_t launch_resolve(const EngineArgs* d, int S, int mode, bool small, hipStream_t st);
-// the speculative resolver (ks_resolve.hip): same contract, same size classes
-hipError_t launch_resolve2(const EngineArgs* d, int S, int mode, bool small, hipStream_t st);
 int small_resolver_max_batch();
 int small_resolver_max_nodes();
 struct BindSeg {
