@@ -135,6 +135,12 @@ int32_t ks_group_size(const ks_group* g);
  * the communicator id with ks_comm_unique_id and the host broadcasts it (any channel).
  * vshards > 1 splits each rank's range further (same merge path; lets one GPU test it).
  * id may be NULL when world == 1 (no communicator). */
+/* The layout ks_load_nodes and ks_step use for n_nodes over world ranks x vshards parts:
+ * part_lo_out[world * vshards + 1] = first 256-node scan block of each part (the last entry = the
+ * block count); rank r scans parts [r * vshards, (r + 1) * vshards).  Exchange: part p's per-pod
+ * top-L keys fill cand_all[p][B][L]; rank r's parts are one contiguous all-gather slice; the
+ * second merge reads cand_all[p][b][*] for every part p.  Pure host function (no device). */
+ks_status ks_shard_layout(int64_t n_nodes, int32_t world, int32_t vshards, int32_t* part_lo_out);
 #define KS_COMM_ID_BYTES 128
 ks_status ks_comm_unique_id(uint8_t* id_out /* [KS_COMM_ID_BYTES] */);
 ks_status ks_shard(ks_engine* eng, int32_t world, int32_t rank, const uint8_t* id, int32_t vshards);

@@ -399,6 +399,16 @@ ks_status ks_shard(ks_engine* e, int32_t world, int32_t rank, const uint8_t* id,
     return KS_OK;
 }
 
+ks_status ks_shard_layout(int64_t n_nodes, int32_t world, int32_t vshards, int32_t* part_lo_out) {
+    if (!part_lo_out || n_nodes < 0 || n_nodes > kMaxNodes || world < 1 || vshards < 1 || (int64_t)world * vshards > 4096)
+        return KS_EINVAL;
+    const int64_t n_pad = std::max<int64_t>(64, (n_nodes + 63) / 64 * 64);
+    const int64_t nblk = (n_pad + ks::block_nodes() - 1) / ks::block_nodes();
+    const int G = world * vshards;
+    for (int p = 0; p <= G; p++) part_lo_out[p] = (int32_t)((int64_t)p * nblk / G);
+    return KS_OK;
+}
+
 ks_status ks_load_nodes(ks_engine* e, int64_t n, const int64_t* alloc, const uint64_t* taint, const uint64_t* label) {
     if (!e) return KS_EINVAL;
     if (e->nodes_loaded) return fail(e, KS_EINVAL, "nodes already loaded");
@@ -449,7 +459,7 @@ ks_status ks_load_nodes(ks_engine* e, int64_t n, const int64_t* alloc, const uin
     e->nblk = (int)((e->n_pad + ks::block_nodes() - 1) / ks::block_nodes());
     const int G = e->world * e->vsh;
     e->part_lo.assign(G + 1, 0);
-    for (int p = 0; p <= G; p++) e->part_lo[p] = (int)((int64_t)p * e->nblk / G);
+    (void)ks_shard_layout(n, e->world, e->vsh, e->part_lo.data());
     e->blk_lo = e->part_lo[e->rank * e->vsh];
     e->blk_n = e->part_lo[(e->rank + 1) * e->vsh] - e->blk_lo;
     // default batch: small clusters exhaust a pod's top-L list after fewer binds, so a batch of

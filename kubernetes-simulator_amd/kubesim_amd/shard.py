@@ -14,6 +14,17 @@ BLOCK_NODES = 256
 TOP_L = 8
 
 
+def engine_part_blocks(n_nodes: int, world: int, vshards: int = 1) -> np.ndarray:
+    """The engine's own layout (include/ks_engine.h ks_shard_layout, used by ks_load_nodes)."""
+    import ctypes as C
+    from . import _lib
+    out = np.zeros(world * vshards + 1, np.int32)
+    rc = _lib.load().ks_shard_layout(n_nodes, world, vshards, out.ctypes.data_as(C.c_void_p))
+    if rc != _lib.KS_OK:
+        raise ValueError(f"ks_shard_layout({n_nodes}, {world}, {vshards}) = {rc}")
+    return out.astype(np.int64)
+
+
 def part_blocks(n_nodes: int, world: int, vshards: int = 1) -> np.ndarray:
     """Block boundaries of the world*vshards parts (ks_load_nodes: p * nblk / G)."""
     n_pad = max(64, (n_nodes + 63) // 64 * 64)

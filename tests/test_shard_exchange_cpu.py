@@ -62,6 +62,65 @@ def _rank_main(rank, world, port, n_nodes, q):
         dist.destroy_process_group()
 
 
+def _rank_main_layout(rank, world, vsh, port, n_nodes, q):
+    """The exchange in the engine's own layout (ks_shard_layout + ks_step): this rank's vsh parts'
+    per-pod top-L lists as its contiguous slice of cand_all[G][B][L], one all-gather, then the
+    second merge over the G parts of each pod."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        G = world * vsh
+        pb = shard.engine_part_blocks(n_nodes, world, vsh)   # the engine's geometry, not a restatement
+        tr = small_trace(37, n_nodes=n_nodes, n_pods=300, selectors=False)
+        ora = make_oracle(tr, MODE)
+        ora.submit(tr)
+        b, rc = ora.step(100)
+        assert rc == 0, rc
+        pods = list(range(100, 120))
+        B = len(pods)
+        mine = np.zeros((vsh, B, shard.TOP_L), np.uint64)   # cand_all[rank*vsh : (rank+1)*vsh]
+        full = []
+        for i, p in enumerate(pods):
+            feas, score = ora.eval(p)
+            cand = (feas != 0) & (score >= 0)
+            full.append(shard.top_l(shard.packed_keys(score, cand)))
+            for v in range(vsh):
+                part = rank * vsh + v
+                lo = min(int(pb[part]) * shard.BLOCK_NODES, n_nodes)
+                hi = min(int(pb[part + 1]) * shard.BLOCK_NODES, n_nodes)
+                if hi > lo:
+                    mine[v, i] = shard.top_l(shard.packed_keys(score[lo:hi], cand[lo:hi], lo))
+        t = torch.from_numpy(mine.reshape(-1).view(np.int64).copy())
+        out = torch.zeros(world * t.numel(), dtype=torch.int64)
+        dist.all_gather_into_tensor(out, t)
+        cand_all = out.numpy().view(np.uint64).reshape(G, B, shard.TOP_L)
+        merged = shard.merge_lists(cand_all)
+        ok = np.array_equal(merged, np.stack(full)) and np.array_equal(pb, shard.part_blocks(n_nodes, world, vsh))
+        q.put((rank, bool(ok), 0))
+    except BaseException as e:
+        q.put((rank, False, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_nodes,vsh", [(1500, 2), (4100, 3), (700, 2)])
+def test_shard_exchange_engine_layout_gloo_world2(n_nodes, vsh):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main_layout, args=(r, world, vsh, port, n_nodes, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok, err in res:
+        assert ok, f"rank {rank}: {err or 'merged lists differ from the global top-L'}"
+
+
 @pytest.mark.parametrize("n_nodes", [300, 1024, 1500])
 def test_shard_exchange_gloo_world2(n_nodes):
     world = 2
@@ -80,6 +139,11 @@ def test_shard_exchange_gloo_world2(n_nodes):
     for rank, ok, rc, bind_node, head_node, lo, hi in res:
         assert ok, f"rank {rank}: merged shard lists differ from the global top-L"
         assert rc == 0 and bind_node == head_node
+
+
+def test_engine_layout_matches_restatement():
+    for n, w, v in ((50_000, 8, 1), (1 << 20, 8, 1), (1000, 4, 1), (100, 4, 1), (4100, 2, 3), (0, 1, 1)):
+        np.testing.assert_array_equal(shard.engine_part_blocks(n, w, v), shard.part_blocks(n, w, v))
 
 
 def test_part_blocks_match_engine_geometry():
