@@ -323,6 +323,16 @@ __host__ __device__ __forceinline__ int32_t lr10_micro(int32_t x, float r) {
     return (int32_t)fmaf((float)x, r, kMicroBias);
 }
 
+// Per-node invariants of the micro evaluator — 1/Ac, 1/Am (v_rcp) and Ac*Am — computed per call,
+// unless the state type carries them (the resolver's register entries: found by overload, same
+// values, so the results are bit-identical).
+template <class NS>
+__host__ __device__ __forceinline__ float micro_ic(const NS&, int32_t acs) { return rcp_est((float)acs); }
+template <class NS>
+__host__ __device__ __forceinline__ float micro_im(const NS&, int32_t ams) { return rcp_est((float)ams); }
+template <class NS>
+__host__ __device__ __forceinline__ int32_t micro_d(const NS&, int32_t acs, int32_t ams) { return mul24(acs, ams); }
+
 template <class NS>
 __host__ __device__ __forceinline__ uint32_t eval_total1_micro(const Cfg& c, const PodRec& p, const NS& n) {
     const int32_t ac = (int32_t)n.ac, am = (int32_t)n.am, ag = (int32_t)n.ag;
@@ -340,13 +350,13 @@ __host__ __device__ __forceinline__ uint32_t eval_total1_micro(const Cfg& c, con
     ok &= !sel_on | ((n.label & p.sel) == p.sel);
     const bool lc_on = ac > 0 && uc <= ac, lm_on = am > 0 && um <= am;
     const int32_t acs = ac > 0 ? ac : 1, ams = am > 0 ? am : 1;
-    const float iac = rcp_est((float)acs), iam = rcp_est((float)ams);  // node-invariant: hoisted
+    const float iac = micro_ic(n, acs), iam = micro_im(n, ams);  // node-invariant: hoisted
     const float rc10 = 10.f * iac, rm10 = 10.f * iam;
     const int32_t lc = lc_on ? lr10_micro(ac - uc, rc10) : 0;
     const int32_t lm = lm_on ? lr10_micro(am - um, rm10) : 0;
     const bool ba_on = ac > 0 && am > 0 && uc < ac && um < am;
     const int32_t ucs = ba_on ? uc : 0, ums = ba_on ? um : 0;
-    const int32_t D = mul24(acs, ams), a = mul24(ucs, ams), b = mul24(ums, acs);
+    const int32_t D = micro_d(n, acs, ams), a = mul24(ucs, ams), b = mul24(ums, acs);
     const int32_t X = a > b ? a - b : b - a;
     const int32_t N = mul24(D - X, 10);
     int32_t q = (int32_t)(10.f - 10.f * fabsf((float)ucs * iac - (float)ums * iam));
@@ -385,12 +395,13 @@ struct PruneF {
     float bc, ic, bm, im;
     int32_t live;  // 0: no pod can make this node a candidate
 };
-__host__ __device__ __forceinline__ PruneF prune_prep(const Cfg& c, const NodeV& n) {
+template <class NS>
+__host__ __device__ __forceinline__ PruneF prune_prep(const Cfg& c, const NS& n) {
     PruneF f;
     f.ic = n.ac > 0 ? rcp_est((float)n.ac) : 0.f;
-    f.bc = n.ac > 0 ? (float)(n.ac - n.rc) * f.ic : -1.f;
+    f.bc = n.ac > 0 ? (float)(int64_t)(n.ac - n.rc) * f.ic : -1.f;
     f.im = n.am > 0 ? rcp_est((float)n.am) : 0.f;
-    f.bm = n.am > 0 ? (float)(n.am - n.rm) * f.im : -1.f;
+    f.bm = n.am > 0 ? (float)(int64_t)(n.am - n.rm) * f.im : -1.f;
     f.live = c.has_scorers && !(c.filter_feeds && (c.filters & kFilterFit) && n.nr >= n.ap);
     return f;
 }
@@ -455,6 +466,11 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
     return ((uint64_t)mh << 32) | ml;
 }
 
+// ctr[] slots of a batch (EngineArgs::ctr), pod flags the resolvers stop on, error codes
+enum : int64_t { kCtrStart = 0, kCtrEnd = 1, kCtrErr = 2, kCtrErrPod = 3, kCtrEarly = 4 };
+enum : uint32_t { kFlagBadKey = 1, kFlagBadSpec = 2 };
+enum : int64_t { kErrEinval = 1, kErrNotFound = 2 };
+
 // Arguments of the batch kernels (expire_head / scan / resolve).
 struct EngineArgs {
     Cfg c;
@@ -496,6 +512,8 @@ hipError_t launch_merge(const EngineArgs* d, int S, int B, const uint64_t* lists
 // small: the RSmall resolver (batches <= small_resolver_max_batch() pods, clusters <=
 // small_resolver_max_nodes() nodes; half the LDS, two resolvers per CU)
 hipError_t launch_resolve(const EngineArgs* d, int S, int mode, bool small, hipStream_t st);
+// the register-table resolver (ks_resolve.hip): same batches, same results, 4-wave workgroups
+hipError_t launch_resolve4(const EngineArgs* d, int S, int mode, bool small, hipStream_t st);
 int small_resolver_max_batch();
 int small_resolver_max_nodes();
 struct BindSeg {

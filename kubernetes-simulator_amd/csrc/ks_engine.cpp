@@ -32,6 +32,7 @@
 #include <numeric>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <queue>
@@ -129,6 +130,7 @@ struct ks_engine {
     int64_t scale[3] = {1, 1, 1};   // device unit of cpu / memory / gpu, in milli-units
     int64_t max_alloc[3] = {0, 0, 0};  // largest capacity per resource, milli-units
     int mode = ks::kEvalWide;  // evaluator variant (ks_device.h)
+    int resolver = 4;          // 4: register-table resolver (ks_resolve.hip), 1: resolve_kernel
     uint32_t flags = 0;        // KS_ENGINE_*
     std::vector<int64_t> h_exp_pos;  // global exp_pod index holding pod q's own expiry, or -1
     // pod keys (Node.CreatePod's pods.Store(key, pod), kubesim/node/node.go:58)
@@ -297,6 +299,7 @@ ks_status engine_init(const ks_config* cfg, ks_engine** out) {
     e->dc.w_ba = (int32_t)w_ba;
     e->dc.const_total = (int32_t)const_total;
     e->dc.tick_seconds = cfg->tick_seconds;
+    if (const char* v = std::getenv("KS_RESOLVER")) e->resolver = std::atoi(v) == 1 ? 1 : 4;  // A/B switch
     *out = e;
     return KS_OK;
 }
@@ -795,7 +798,8 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
                 HIPCHK(e, ks::launch_merge(d, 1, e->B, e->cand_all, L, G, BL, e->cand, G, st));
             }
             if (ev[3]) HIPCHK(e, hipEventRecord(ev[3], st));
-            HIPCHK(e, ks::launch_resolve(d, 1, e->mode, small_resolver(e), st));
+            HIPCHK(e, e->resolver == 1 ? ks::launch_resolve(d, 1, e->mode, small_resolver(e), st)
+                                        : ks::launch_resolve4(d, 1, e->mode, small_resolver(e), st));
             if (ev[4]) HIPCHK(e, hipEventRecord(ev[4], st));
             launches++;
         }
@@ -1005,7 +1009,8 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
             if (!dev(ks::launch_expire_head(g->d_args, S, st)) ||
                 !dev(ks::launch_scan(g->d_args, S, blk_n, B, pg, mode, k16, st)) ||
                 !dev(ks::launch_merge(g->d_args, S, B, nullptr, 0, 0, 0, nullptr, blk_n, st)) ||
-                !dev(ks::launch_resolve(g->d_args, S, mode, small, st)))
+                !dev(g->engs[0]->resolver == 1 ? ks::launch_resolve(g->d_args, S, mode, small, st)
+                                               : ks::launch_resolve4(g->d_args, S, mode, small, st)))
                 return dev_fail("group step: kernel launch failed");
             launches++;
         }

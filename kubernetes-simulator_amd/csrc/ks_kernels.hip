@@ -70,9 +70,6 @@ using RSmall = RCfg<512, 256, 10, 128, 13>;
 constexpr int kMaxBatchR = RBig::kMaxBatchR;
 constexpr int kSmallMaxNodes = RSmall::kFilterBits;
 
-enum : int64_t { kCtrStart = 0, kCtrEnd = 1, kCtrErr = 2, kCtrErrPod = 3, kCtrEarly = 4 };
-enum : uint32_t { kFlagBadKey = 1, kFlagBadSpec = 2 };
-enum : int64_t { kErrEinval = 1, kErrNotFound = 2 };
 
 // owner slot of a resolve wave, or -1
 __device__ __forceinline__ int owner_slot(int wave) {

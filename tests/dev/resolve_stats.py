@@ -91,7 +91,21 @@ def main():
             fin.setdefault(t + dur[j], []).append(j)
 
     st = dict(T=[], ge=[], win_list=0, win_touched_batch=0, win_touched_exp=0, exhausted=0, pods=0,
-              lk_rank=[], pre=[])
+              lk_rank=[], pre=[], Tact=[], bnd=[], grp=[], grp_pass=[], grp_act=[], grp_act_pass=[])
+
+    def tbound(n_idx, p):
+        """prune_tmax's float upper bound of total (ks_device.h), vectorised, filters ignored"""
+        qc, qm, _ = p["req"]
+        a_c, a_m = ac[n_idx].astype(np.float32), am[n_idx].astype(np.float32)
+        ic = np.where(a_c > 0, 1 / np.maximum(a_c, 1), 0).astype(np.float32)
+        im = np.where(a_m > 0, 1 / np.maximum(a_m, 1), 0).astype(np.float32)
+        fc = np.where(a_c > 0, (a_c - rc[n_idx]) * ic, -1) - qc * ic
+        fm = np.where(a_m > 0, (a_m - rm[n_idx]) * im, -1) - qm * im
+        lc = np.where(fc > -1.5e-5, np.floor(10 * fc + 1.5e-5), 0)
+        lm = np.where(fm > -1.5e-5, np.floor(10 * fm + 1.5e-5), 0)
+        tot = (lc + lm) // 2
+        tot = tot + np.where((fc > -1.5e-5) & (fm > -1.5e-5), np.floor(10 - 10 * np.abs(fc - fm) + 3e-5), 0)
+        return tot.astype(np.int64)
     j = 0
     # warm-up: sequential
     while j < a.skip:
@@ -117,11 +131,17 @@ def main():
                 pre.add(int(node_of[q]))
         st["pre"].append(len(pre))
         touched = set(pre)
+        modified = set()
+        order = list(pre)  # entry numbering: pre-inserted, then in-batch winners
+        act_order = []     # entry numbering by activation (first bind or expiry in the batch)
         for i in range(a.batch):
             jj = s + i
             tt = jj + 1
             if i > 0:
-                expire(tt)
+                for n_ in expire(tt):
+                    if n_ not in modified:
+                        modified.add(n_)
+                        act_order.append(n_)
             k = keys(scores(ac, am, ag, apd, rc, rm, rg, nr, taint, label, pod(jj)), nid)
             lst = lists[i]
             unt = [(kk, x) for kk, x in lst if x not in touched]
@@ -135,6 +155,22 @@ def main():
             T = np.fromiter(touched, np.int64) if touched else np.zeros(0, np.int64)
             st["T"].append(len(T))
             st["ge"].append(int((k[T] >= lk).sum()) if len(T) else 0)
+            st["Tact"].append(len(modified))
+            if len(order):
+                E = np.array(order, np.int64)
+                bk = keys(tbound(E, pod(jj)) + 1, E)
+                ok_ = bk >= lk
+                st["bnd"].append(int(ok_.sum()))
+                g = np.arange(len(E)) // 64
+                st["grp"].append(int(g.max()) + 1)
+                st["grp_pass"].append(len(set(g[ok_])))
+            if act_order:
+                E = np.array(act_order, np.int64)
+                bk = keys(tbound(E, pod(jj)) + 1, E)
+                ok_ = bk >= lk
+                g = np.arange(len(E)) // 64
+                st["grp_act"].append(int(g.max()) + 1)
+                st["grp_act_pass"].append(len(set(g[ok_])))
             w = int(np.argmax(k))
             if w in touched:
                 if w in pre:
@@ -144,6 +180,11 @@ def main():
             else:
                 st["win_list"] += 1
                 assert k[w] == lk, (k[w], lk)
+            if w not in touched:
+                order.append(w)
+            if w not in modified:
+                modified.add(w)
+                act_order.append(w)
             touched.add(w)
             bind(jj, w, tt)
             st["pods"] += 1
@@ -154,6 +195,10 @@ def main():
     print(f"touched entries with exact key >= list cand: mean {ge.mean():.2f}  p90 {np.percentile(ge, 90):.0f}  max {ge.max()}")
     print(f"winner: list {st['win_list']}  touched(batch) {st['win_touched_batch']}  touched(expiry) {st['win_touched_exp']}")
     print(f"list cand rank histogram: {np.bincount(st['lk_rank'])}")
+    print(f"modified (active) entries: mean {np.mean(st['Tact']):.0f}  max {np.max(st['Tact'])}")
+    print(f"entries passing the float bound: mean {np.mean(st['bnd']):.2f}  p90 {np.percentile(st['bnd'], 90):.0f}")
+    print(f"64-entry groups: mean {np.mean(st['grp']):.2f}, with a bound pass {np.mean(st['grp_pass']):.2f}")
+    print(f"activation-ordered groups: mean {np.mean(st['grp_act']):.2f}, with a bound pass {np.mean(st['grp_act_pass']):.2f}")
 
 
 if __name__ == "__main__":
