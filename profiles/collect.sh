@@ -8,18 +8,20 @@
 set -euo pipefail
 OUT=${1:-gpurun_out/prof}
 ROOT=$(pwd)
-mkdir -p "$OUT"
+DB=/tmp/ks_prof   # result databases (large): scratch, summaries go to OUT
+mkdir -p "$OUT" "$DB"
 export TMPDIR=/tmp
-B="$ROOT/bench.py --steps 4 --warmup 1 --no-cpu-baseline"
+B="$ROOT/bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-c5"
 cd /tmp
-timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/c3" -o run -- python3 $B > "$ROOT/$OUT/c3_bench.json"
-timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/c4" -o run -- python3 "$ROOT/bench.py" --config c4 --steps 2 --warmup 1 > "$ROOT/$OUT/c4_bench.json"
-timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE -d "$ROOT/$OUT/fetch" -o run -- python3 $B --steps 2 > /dev/null
-timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE -d "$ROOT/$OUT/write" -o run -- python3 $B --steps 2 > /dev/null
-timeout -k 10 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$ROOT/$OUT/sq" -o run -- python3 $B --steps 2 > /dev/null
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$DB/c3" -o run -- python3 $B > "$ROOT/$OUT/c3_bench.json"
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$DB/c4" -o run -- python3 "$ROOT/bench.py" --config c4 --steps 2 --warmup 1 > "$ROOT/$OUT/c4_bench.json"
+timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE -d "$DB/fetch" -o run -- python3 $B --steps 2 > /dev/null
+timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE -d "$DB/write" -o run -- python3 $B --steps 2 > /dev/null
+timeout -k 10 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$DB/sq" -o run -- python3 $B --steps 2 > /dev/null
 cd "$ROOT"
-python3 profiles/db_summary.py stats "$OUT/c3/run_results.db" "$OUT/c3_kernel_stats.csv"
-python3 profiles/db_summary.py stats "$OUT/c4/run_results.db" "$OUT/c4_kernel_stats.csv"
-python3 profiles/db_summary.py pmc "$OUT/fetch/run_results.db" "$OUT/write/run_results.db" "$OUT/sq/run_results.db" \
+python3 profiles/db_summary.py stats "$DB/c3/run_results.db" "$OUT/c3_kernel_stats.csv"
+python3 profiles/db_summary.py stats "$DB/c4/run_results.db" "$OUT/c4_kernel_stats.csv"
+python3 profiles/db_summary.py pmc "$DB/fetch/run_results.db" "$DB/write/run_results.db" "$DB/sq/run_results.db" \
     "$OUT/pmc_summary.json" "rocprofv3 --pmc passes over bench.py --steps 2 --warmup 1 (C3), MI355X"
+rm -rf "$DB"
 echo "profiles collected in $OUT"

@@ -17,7 +17,8 @@ import sys
 
 
 def short(name):
-    return name.split("(")[0].replace("void ", "").split("<")[0]
+    name = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    return name.split("(")[0].split("<")[0]
 
 
 def stats(db, out):
