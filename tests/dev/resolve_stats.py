@@ -51,6 +51,8 @@ def main():
     ap.add_argument("--batches", type=int, default=10)
     ap.add_argument("--skip", type=int, default=8000, help="pods bound sequentially before measuring")
     ap.add_argument("--L", type=int, default=8)
+    ap.add_argument("--overlap", action="store_true",
+                    help="lists from the snapshot before the previous batch; its modified nodes touched")
     a = ap.parse_args()
     tr = tracegen.c3_trace(n_nodes=a.nodes, n_pods=a.pods)
     enc = encode.encode_trace(tr)
@@ -114,14 +116,20 @@ def main():
         k = scores(ac, am, ag, apd, rc, rm, rg, nr, taint, label, pod(j))
         bind(j, int(np.argmax(keys(k, nid))), t)
         j += 1
+    snap = (rc.copy(), rm.copy(), rg.copy(), nr.copy())
+    prev_mod = set()
     for b in range(a.batches):
         s = j
         t = s + 1
+        head = set(int(node_of[q]) for q in fin.get(t, []))
         expire(t)
-        # snapshot lists
+        # snapshot lists (overlap: the state before the previous batch, as a scan running beside
+        # the previous resolve would see it)
+        src = snap if a.overlap else (rc, rm, rg, nr)
+        snap = (rc.copy(), rm.copy(), rg.copy(), nr.copy())
         lists = []
         for i in range(a.batch):
-            k = keys(scores(ac, am, ag, apd, rc, rm, rg, nr, taint, label, pod(s + i)), nid)
+            k = keys(scores(ac, am, ag, apd, src[0], src[1], src[2], src[3], taint, label, pod(s + i)), nid)
             top = np.argsort(-k)[:a.L]
             lists.append([(int(k[x]), int(x)) for x in top if k[x] > 0])
         # pre-inserted expiry nodes of the window
@@ -129,6 +137,8 @@ def main():
         for i in range(1, a.batch):
             for q in fin.get(s + i + 1, []):
                 pre.add(int(node_of[q]))
+        if a.overlap:
+            pre |= prev_mod | head
         st["pre"].append(len(pre))
         touched = set(pre)
         modified = set()
@@ -189,6 +199,7 @@ def main():
             bind(jj, w, tt)
             st["pods"] += 1
             j = jj + 1
+        prev_mod = set(modified) | head
     T = np.array(st["T"]); ge = np.array(st["ge"])
     print(f"pods {st['pods']}  exhausted stops {st['exhausted']}  pre-inserted/batch {np.mean(st['pre']):.0f}")
     print(f"touched T: mean {T.mean():.0f} max {T.max()}")
