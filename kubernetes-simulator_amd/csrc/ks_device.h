@@ -509,11 +509,11 @@ hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int
 // nl_max: the largest nl of the launch (<= 64 / L candidates per pod: one wave per pod)
 hipError_t launch_merge(const EngineArgs* d, int S, int B, const uint64_t* lists, int64_t pod_stride, int32_t nl,
                         int64_t list_stride, uint64_t* out, int nl_max, hipStream_t st);
-// small: the RSmall resolver (batches <= small_resolver_max_batch() pods, clusters <=
-// small_resolver_max_nodes() nodes; half the LDS, two resolvers per CU)
-hipError_t launch_resolve(const EngineArgs* d, int S, int mode, bool small, hipStream_t st);
-// the register-table resolver (ks_resolve.hip): same batches, same results, 4-wave workgroups
-hipError_t launch_resolve4(const EngineArgs* d, int S, int mode, bool small, hipStream_t st);
+// the role-split resolver (ks_kernels.hip): batches of up to max_batch_pods() pods, any cluster
+hipError_t launch_resolve(const EngineArgs* d, int S, int mode, hipStream_t st);
+// the register-table resolver (ks_resolve.hip): batches of <= small_resolver_max_batch() pods of
+// clusters of <= small_resolver_max_nodes() nodes, four per CU
+hipError_t launch_resolve_small(const EngineArgs* d, int S, int mode, hipStream_t st);
 int small_resolver_max_batch();
 int small_resolver_max_nodes();
 struct BindSeg {

@@ -130,10 +130,6 @@ struct ks_engine {
     int64_t scale[3] = {1, 1, 1};   // device unit of cpu / memory / gpu, in milli-units
     int64_t max_alloc[3] = {0, 0, 0};  // largest capacity per resource, milli-units
     int mode = ks::kEvalWide;  // evaluator variant (ks_device.h)
-    // resolver: 0 = by size class (the role-split resolve_kernel for big batches — lowest latency
-    // per pod; the 4-wave register-table resolver for small ones — several per CU, what-if groups),
-    // 1 / 4 = always one of them (KS_RESOLVER, A/B)
-    int resolver = 0;
     uint32_t flags = 0;        // KS_ENGINE_*
     std::vector<int64_t> h_exp_pos;  // global exp_pod index holding pod q's own expiry, or -1
     // pod keys (Node.CreatePod's pods.Store(key, pod), kubesim/node/node.go:58)
@@ -234,21 +230,18 @@ bool key16(const ks_engine* e) {
     return (int64_t)e->dc.const_total + 10 * ((int64_t)e->dc.w_lr + e->dc.w_ba) + 1 < (1 << 16);
 }
 
-// the half-size resolver holds this engine's batches (ks_kernels.hip, RSmall)
+// the small (register-table) resolver holds this engine's batches
 bool small_resolver(const ks_engine* e) {
     return e->B <= ks::small_resolver_max_batch() && e->dc.n_nodes <= ks::small_resolver_max_nodes();
 }
 
-// Both resolvers give the same binds (tested); they differ in shape.  The role-split resolve_kernel
-// (16 waves, ks_kernels.hip) has the shorter per-pod chain: C3 245 us per 234-pod batch against
-// 375 us for the register-table one.  The register-table resolver (4 waves, ks_resolve.hip) is
-// lighter: its small size class fits four workgroups per CU, so a what-if group's resolvers run
-// side by side — C4 2.30e11 against 2.16e11 evals/s.
-hipError_t launch_resolver(int which, const ks::EngineArgs* d, int S, int mode, bool small, hipStream_t st) {
-    const bool r4 = which == 4 || (which == 0 && small);
-    return r4 ? ks::launch_resolve4(d, S, mode, small, st) : ks::launch_resolve(d, S, mode, small, st);
+// Two resolvers, the same binds: the role-split resolve_kernel (16 waves, ks_kernels.hip) has the
+// shortest per-pod chain and takes big batches; the register-table resolver (4 waves,
+// ks_resolve.hip) is lighter — four per CU, so a what-if group's resolvers run side by side (C4
+// 2.29e11 against 2.16e11 evals/s with the role-split kernel's half-size class).
+hipError_t launch_resolver(const ks::EngineArgs* d, int S, int mode, bool small, hipStream_t st) {
+    return small ? ks::launch_resolve_small(d, S, mode, st) : ks::launch_resolve(d, S, mode, st);
 }
-
 void update_mode(ks_engine* e) {
     int64_t m[3];
     for (int k = 0; k < 3; k++) m[k] = e->max_alloc[k] / e->scale[k];
@@ -312,7 +305,6 @@ ks_status engine_init(const ks_config* cfg, ks_engine** out) {
     e->dc.w_ba = (int32_t)w_ba;
     e->dc.const_total = (int32_t)const_total;
     e->dc.tick_seconds = cfg->tick_seconds;
-    if (const char* v = std::getenv("KS_RESOLVER")) e->resolver = std::atoi(v) == 1 ? 1 : (std::atoi(v) == 4 ? 4 : 0);
     *out = e;
     return KS_OK;
 }
@@ -811,7 +803,7 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
                 HIPCHK(e, ks::launch_merge(d, 1, e->B, e->cand_all, L, G, BL, e->cand, G, st));
             }
             if (ev[3]) HIPCHK(e, hipEventRecord(ev[3], st));
-            HIPCHK(e, launch_resolver(e->resolver, d, 1, e->mode, small_resolver(e), st));
+            HIPCHK(e, launch_resolver(d, 1, e->mode, small_resolver(e), st));
             if (ev[4]) HIPCHK(e, hipEventRecord(ev[4], st));
             launches++;
         }
@@ -1021,7 +1013,7 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
             if (!dev(ks::launch_expire_head(g->d_args, S, st)) ||
                 !dev(ks::launch_scan(g->d_args, S, blk_n, B, pg, mode, k16, st)) ||
                 !dev(ks::launch_merge(g->d_args, S, B, nullptr, 0, 0, 0, nullptr, blk_n, st)) ||
-                !dev(launch_resolver(g->engs[0]->resolver, g->d_args, S, mode, small, st)))
+                !dev(launch_resolver(g->d_args, S, mode, small, st)))
                 return dev_fail("group step: kernel launch failed");
             launches++;
         }

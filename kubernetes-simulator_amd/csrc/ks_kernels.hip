@@ -46,12 +46,11 @@ constexpr int kOwnerWave0 = 3;           // waves 3..15 own the touched entries,
 #define KS_PRIO 0
 #endif
 constexpr int kWriterWave = KS_WRITER_WAVE;  // the bind's bookkeeping writer (off the critical path)
-// Resolver size classes (the LDS footprint): touched-node table entries, open-addressing node ->
-// entry map slots (log2), pods per launch, touched filter bits (log2; the filter is exact — no
-// hash confirmation — for clusters of at most that many nodes).  RBig: any cluster, 256-pod
-// batches, 1024 threads, ~150 KB of LDS (one workgroup per CU).  RSmall: batches of <= 128 pods
-// of clusters of <= 8,192 nodes (what-if scenarios), 512 threads (4 owner waves), ~56 KB, so two
-// resolvers share a CU (registers: 2 x 8 waves of <= 128 VGPRs).
+// Resolver size (the LDS footprint): touched-node table entries, open-addressing node -> entry
+// map slots (log2), pods per launch, touched filter bits (log2; the filter is exact — no hash
+// confirmation — for clusters of at most that many nodes).  RBig: any cluster, 256-pod batches,
+// 1024 threads, ~150 KB of LDS (one workgroup per CU).  Small batches of small clusters (what-if
+// scenarios) go to the register-table resolver instead (ks_resolve.hip).
 template <int THREADS, int TMAX, int HASH_LOG2, int MAXB, int FBITS_LOG2>
 struct RCfg {
     static constexpr int kThreads = THREADS;
@@ -66,9 +65,7 @@ struct RCfg {
     static_assert(TMAX - MAXB <= THREADS, "one thread per pre-inserted expiry");
 };
 using RBig = RCfg<kResolveThreads, 768, 11, 256, 16>;
-using RSmall = RCfg<512, 256, 10, 128, 13>;
 constexpr int kMaxBatchR = RBig::kMaxBatchR;
-constexpr int kSmallMaxNodes = RSmall::kFilterBits;
 
 
 // owner slot of a resolve wave, or -1
@@ -130,6 +127,10 @@ __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict_
     const int pg0 = blockIdx.y * a.PG;
     if (pg0 >= nb) return;
     const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
+#ifdef KS_SCAN_STAMPS  // diagnostic: evaluation / extraction cycles of wave 0, ctr[20] / ctr[21]
+    uint64_t st0;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st0)::"memory");
+#endif
     const int blk = a.blk_lo + blockIdx.x;
     const uint32_t blk_base = (uint32_t)blk * kBlockNodes;
     const int64_t node = (int64_t)blk_base + threadIdx.x;
@@ -157,6 +158,10 @@ __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict_
         kv[b * kBlockNodes + threadIdx.x] = (KT)(valid ? t : 0u);
     }
     __syncthreads();
+#ifdef KS_SCAN_STAMPS
+    uint64_t st1;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st1)::"memory");
+#endif
     for (int b = wave; b < np; b += kScanWaves) {
         uint32_t v[kScanWaves];
 #pragma unroll
@@ -184,6 +189,14 @@ __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict_
         }
         if (lane >= cnt && lane < kL) out[lane] = 0ull;
     }
+#ifdef KS_SCAN_STAMPS
+    uint64_t st2;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st2)::"memory");
+    if (threadIdx.x == 0) {
+        atomicAdd((unsigned long long*)a.ctr + 20, (unsigned long long)(st1 - st0));
+        atomicAdd((unsigned long long*)a.ctr + 21, (unsigned long long)(st2 - st1));
+    }
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1143,8 +1156,6 @@ __global__ __launch_bounds__(256) void rescale_kernel(NodeSoA s, int64_t n_pad, 
 // Launchers, called by ks_engine.cpp.
 // ---------------------------------------------------------------------------------------------
 int max_batch_pods() { return kMaxBatchR; }
-int small_resolver_max_batch() { return RSmall::kMaxBatchR; }
-int small_resolver_max_nodes() { return kSmallMaxNodes; }
 int max_pods_per_scan_wg() { return kMaxPG; }
 int block_nodes() { return kBlockNodes; }
 
@@ -1195,11 +1206,8 @@ static void launch_resolve_t(const EngineArgs* d, int S, int mode, hipStream_t s
     }
 }
 
-hipError_t launch_resolve(const EngineArgs* d, int S, int mode, bool small, hipStream_t st) {
-    if (small)
-        launch_resolve_t<RSmall>(d, S, mode, st);
-    else
-        launch_resolve_t<RBig>(d, S, mode, st);
+hipError_t launch_resolve(const EngineArgs* d, int S, int mode, hipStream_t st) {
+    launch_resolve_t<RBig>(d, S, mode, st);
     return hipGetLastError();
 }
 

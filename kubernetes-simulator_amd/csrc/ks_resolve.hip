@@ -48,15 +48,10 @@ struct Cfg4 {
     static_assert(kMaxExp < kHash, "the hash never fills");
     static_assert(MAXB <= kThreads, "one thread per pod in the window search");
 };
-// RBig: any cluster, 256-pod batches, 768 entries.  RSmall: batches of <= 128 pods of clusters of
-// <= 8,192 nodes (what-if scenarios), 256 entries, ~40 KB of LDS, so several share a CU.
-#ifndef KS_R4_PRUNE
-#define KS_R4_PRUNE 1  // skip entries whose float upper bound is below the pod's list candidate
-#endif
-#ifndef KS_R4_WAVES
-#define KS_R4_WAVES 4
-#endif
-using RBig = Cfg4<KS_R4_WAVES, 768 / (KS_R4_WAVES * kWave) + (768 % (KS_R4_WAVES * kWave) != 0), 768, 256, 11, 16>;
+// The small class: batches of <= 128 pods of clusters of <= 8,192 nodes (what-if scenarios),
+// 256 entries, ~34 KB of LDS and <= 88 VGPRs, so four resolvers share a CU.  (A 768-entry class
+// of the same kernel — 3 register slots — was exact but slower than the role-split resolver on
+// 256-pod batches: DESIGN.md §4.)
 using RSmall = Cfg4<4, 1, 256, 128, 10, 13>;
 
 // Entry state in registers: 32-bit fields for the narrow evaluators (every capacity < 2^29 and
@@ -338,12 +333,9 @@ __global__ __launch_bounds__(C::kThreads) void resolve_kernel(const EngineArgs* 
         for (int s = 0; s < S; ++s) {
             const int e = (s * W + wave) * kWave + lane;
             if ((s * W + wave) * kWave < T) {
-                bool want = e < T;
-                if (KS_R4_PRUNE) {
-                    want &= opf[s].live != 0;
-                    if (lbk != 0 && want)
-                        want = make_key(prune_tmax(a.c, opf[s], qfc, qfm) + 1u, (uint32_t)onode[s]) >= lbk;
-                }
+                bool want = e < T && opf[s].live != 0;
+                if (lbk != 0 && want)
+                    want = make_key(prune_tmax(a.c, opf[s], qfc, qfm) + 1u, (uint32_t)onode[s]) >= lbk;
                 if (__ballot(want)) {
                     const uint64_t k = make_key(eval_t<kMode>(a.c, p, own[s]), (uint32_t)onode[s]);
                     const uint64_t v = (want && k) ? ikey(k, e) : 0ull;
@@ -544,12 +536,12 @@ void launch_t(const EngineArgs* d, int S, int mode, hipStream_t st) {
 
 }  // namespace
 
-hipError_t launch_resolve4(const EngineArgs* d, int S, int mode, bool small, hipStream_t st) {
-    if (small)
-        launch_t<RSmall>(d, S, mode, st);
-    else
-        launch_t<RBig>(d, S, mode, st);
+hipError_t launch_resolve_small(const EngineArgs* d, int S, int mode, hipStream_t st) {
+    launch_t<RSmall>(d, S, mode, st);
     return hipGetLastError();
 }
+
+int small_resolver_max_batch() { return RSmall::kMaxB; }
+int small_resolver_max_nodes() { return RSmall::kFilterBits; }
 
 }  // namespace ks

@@ -1,6 +1,7 @@
 """Diagnostic: phase breakdown of the register-table resolver (ks_resolve.hip built with
--DKS_R4_STAMPS: make -C kubernetes-simulator_amd/csrc variant NAME=st DEFS=-DKS_R4_STAMPS) on C3.
-Stamps wait for LDS (s_waitcnt lgkmcnt(0)), so phases are serialised a little."""
+-DKS_R4_STAMPS: make -C kubernetes-simulator_amd/csrc variant NAME=st DEFS=-DKS_R4_STAMPS) on one
+C4 what-if scenario (2,000 nodes, 128-pod batches: the small class it serves).  Stamps wait for
+LDS (s_waitcnt lgkmcnt(0)), so phases are serialised a little."""
 import os
 import sys
 import time
@@ -14,22 +15,22 @@ _lib.LIB_PATH = os.path.join(ROOT, "kubernetes-simulator_amd", "kubesim_amd",
 from kubesim_amd import encode, tracegen  # noqa: E402
 from kubesim_amd.engine import Engine  # noqa: E402
 
-tr = tracegen.c3_trace(n_pods=60_000)
+tr = tracegen.c4_scenario(0, n_nodes=2000, n_pods=40_000)
 enc = encode.encode_trace(tr)
 eng = Engine(tick_seconds=tr["tick_seconds"], filter_mode=1, filters=7, scorers=((1, 1, 0), (2, 1, 0)))
 eng.load_nodes(enc["alloc"], enc["taint"], enc["label"])
 eng.submit(enc["pods"])
-eng.step(16384)
+eng.step(4096)
 c0 = eng.debug_counters().copy()
 eng.set_profiling(True)
 t = time.perf_counter()
-eng.step(16384)
+eng.step(8192)
 dt = time.perf_counter() - t
 st = eng.last_step_stats()
 d = eng.debug_counters() - c0
 it, L = max(int(d[5]), 1), max(int(d[6]), 1)
 names = ("decide", "bind", "expiries", "mask", "eval", "barrier")
-print(f"{16384 / dt:.0f} pods/s; resolve {st['resolve_ms'] * 1e6 / max(st['pods'], 1):.0f} ns/pod; "
+print(f"{8192 / dt:.0f} pods/s; resolve {st['resolve_ms'] * 1e6 / max(st['pods'], 1):.0f} ns/pod; "
       f"{it / L:.1f} pods/launch")
 for w in range(4):
     row = [d[8 + 6 * w + k] / it for k in range(6)]
