@@ -1,4 +1,4 @@
-# Full GPU suite, the default bench line, and the C4 A/B of the register-table resolver's pruning.
+# Full GPU suite, the default bench line and the C4 line.
 set -o pipefail
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
@@ -13,7 +13,6 @@ rc=$?
 echo "bench rc=$rc"
 cat gpurun_out/b_r2c.json
 if [ $rc -ne 0 ]; then exit $rc; fi
-for v in libks_engine.so libks_engine_np.so; do
-  echo "C4 $v"
-  timeout -k 10 200 python -u tests/dev/ab_c4.py $v 2>/dev/null | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['kernels'])" || exit 1
-done
+timeout -k 10 300 python -u bench.py --config c4 --steps 3 --warmup 1 > gpurun_out/c4_r2c.json 2> gpurun_out/c4_r2c.log
+echo "c4 rc=$?"
+cat gpurun_out/c4_r2c.json
