@@ -141,6 +141,10 @@ int32_t ks_group_size(const ks_group* g);
  * top-L keys fill cand_all[p][B][L]; rank r's parts are one contiguous all-gather slice; the
  * second merge reads cand_all[p][b][*] for every part p.  Pure host function (no device). */
 ks_status ks_shard_layout(int64_t n_nodes, int32_t world, int32_t vshards, int32_t* part_lo_out);
+/* The second merge on the host: out[B][L] = exact top-L over parts of cand_all[parts][B][L]
+ * (each list sorted descending, 0-padded) — the device merge's per-list step (topl_insert,
+ * ks_device.h), for checking an exchange without a GPU.  Pure host function. */
+ks_status ks_merge_candidates(const uint64_t* cand_all, int32_t parts, int32_t B, uint64_t* out);
 #define KS_COMM_ID_BYTES 128
 ks_status ks_comm_unique_id(uint8_t* id_out /* [KS_COMM_ID_BYTES] */);
 ks_status ks_shard(ks_engine* eng, int32_t world, int32_t rank, const uint8_t* id, int32_t vshards);

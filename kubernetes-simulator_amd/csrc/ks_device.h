@@ -445,6 +445,24 @@ __host__ __device__ __forceinline__ uint64_t make_key(uint32_t total1, uint32_t 
     return total1 ? (((uint64_t)total1 << 32) | (uint64_t)(0xFFFFFFFFu - node)) : 0ull;
 }
 
+// Insert one sorted (descending, 0-padded) list of L keys into a sorted top-L: the per-thread step
+// of the merge kernel, also the host's ks_merge_candidates.  Keys are distinct (node in the low
+// bits), so the result is the exact top-L of the union.
+__host__ __device__ __forceinline__ void topl_insert(uint64_t (&top)[kTopL], const uint64_t (&lv)[kTopL]) {
+#pragma unroll
+    for (int k = 0; k < kTopL; ++k) {
+        uint64_t v = lv[k];
+        if (v <= top[kTopL - 1]) break;  // lists are sorted: nothing further can enter
+#pragma unroll
+        for (int s = 0; s < kTopL; ++s) {
+            const uint64_t t = top[s];
+            const bool gt = v > t;
+            top[s] = gt ? v : t;
+            v = gt ? t : v;
+        }
+    }
+}
+
 // Wave-wide unsigned max in VALU DPP moves (no LDS crossbar): Hillis-Steele row_shr 1/2/4/8
 // leaves each 16-lane row's max in its lane 15, row_bcast 15/31 folds the rows into lane 63.
 __device__ __forceinline__ uint32_t dpp_max_step(uint32_t v, uint32_t w) { return v > w ? v : w; }

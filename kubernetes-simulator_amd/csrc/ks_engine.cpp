@@ -407,6 +407,21 @@ ks_status ks_shard(ks_engine* e, int32_t world, int32_t rank, const uint8_t* id,
     return KS_OK;
 }
 
+ks_status ks_merge_candidates(const uint64_t* cand_all, int32_t parts, int32_t B, uint64_t* out) {
+    if (!cand_all || !out || parts < 1 || B < 0) return KS_EINVAL;
+    constexpr int L = ks::kTopL;
+    for (int64_t b = 0; b < B; b++) {
+        uint64_t top[L] = {};
+        for (int64_t p = 0; p < parts; p++) {
+            uint64_t lv[L];
+            std::memcpy(lv, cand_all + (p * B + b) * L, sizeof(lv));
+            ks::topl_insert(top, lv);
+        }
+        std::memcpy(out + b * L, top, sizeof(top));
+    }
+    return KS_OK;
+}
+
 ks_status ks_shard_layout(int64_t n_nodes, int32_t world, int32_t vshards, int32_t* part_lo_out) {
     if (!part_lo_out || n_nodes < 0 || n_nodes > kMaxNodes || world < 1 || vshards < 1 || (int64_t)world * vshards > 4096)
         return KS_EINVAL;

@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict_
         uint32_t v[kScanWaves];
 #pragma unroll
         for (int u = 0; u < kScanWaves; ++u) v[u] = (uint32_t)kv[b * kBlockNodes + u * kWave + lane];  // node u*64 + lane
-        uint64_t* out = a.lists + ((int64_t)(pg0 + b) * a.nblk + blk) * kL;
+        auto out = gptr(a.lists) + ((int64_t)(pg0 + b) * a.nblk + blk) * kL;  // global_: not in lgkmcnt
         int cnt = 0;
         for (int r = 0; r < kL && cnt < kL; ++r) {
             uint32_t lm = v[0];
@@ -237,18 +237,7 @@ __global__ __launch_bounds__(1024) void merge_kernel(const EngineArgs* __restric
             lv[2 * k] = w.x;
             lv[2 * k + 1] = w.y;
         }
-#pragma unroll
-        for (int k = 0; k < kL; ++k) {
-            uint64_t v = lv[k];
-            if (v <= top[kL - 1]) break;  // block lists are sorted: nothing further can enter
-#pragma unroll
-            for (int s = 0; s < kL; ++s) {
-                const uint64_t t = top[s];
-                const bool gt = v > t;
-                top[s] = gt ? v : t;
-                v = gt ? t : v;
-            }
-        }
+        topl_insert(top, lv);
     }
     // each wave: L rounds of its max thread head (the owner advances), no barrier; then wave 0
     // merges the wave lists (<= 128 candidates, two per lane) the same way

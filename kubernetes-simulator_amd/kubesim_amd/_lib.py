@@ -33,7 +33,7 @@ EXPORTED_SYMBOLS = ("ks_create", "ks_destroy", "ks_load_nodes", "ks_submit_pods"
                     "ks_comm_unique_id", "ks_shard", "ks_group_create", "ks_group_destroy",
                     "ks_group_add", "ks_group_size", "ks_group_step", "ks_pod_status",
                     "ks_usage_at", "ks_usage_digest", "ks_node_mix", "ks_pod_lookup", "ks_node_pods",
-                    "ks_shard_layout",
+                    "ks_shard_layout", "ks_merge_candidates",
                     # include/ks_ingest.h
                     "ks_parse_quantity", "ks_parse_simspec", "ks_cluster_parse", "ks_cluster_free",
                     "ks_cluster_nodes", "ks_cluster_tick", "ks_cluster_start_clock", "ks_cluster_arrays",
@@ -99,6 +99,8 @@ def load():
     L.ks_node_pods.argtypes = [p, C.c_int32, p, C.c_int64, C.POINTER(C.c_int64)]
     L.ks_shard_layout.argtypes = [C.c_int64, C.c_int32, C.c_int32, p]
     L.ks_shard_layout.restype = C.c_int
+    L.ks_merge_candidates.argtypes = [p, C.c_int32, C.c_int32, p]
+    L.ks_merge_candidates.restype = C.c_int
     for f in ("ks_load_nodes", "ks_submit_pods", "ks_step", "ks_filter", "ks_score", "ks_usage", "ks_usage_at",
               "ks_usage_digest", "ks_pod_lookup", "ks_node_pods"):
         getattr(L, f).restype = C.c_int

@@ -25,6 +25,21 @@ def engine_part_blocks(n_nodes: int, world: int, vshards: int = 1) -> np.ndarray
     return out.astype(np.int64)
 
 
+def engine_merge(cand_all: np.ndarray) -> np.ndarray:
+    """The engine's second merge on the host (ks_merge_candidates: the device merge's per-list
+    step): cand_all[G][B][L] -> [B][L]."""
+    import ctypes as C
+    from . import _lib
+    src = np.ascontiguousarray(cand_all, dtype=np.uint64)
+    G, B, L = src.shape
+    assert L == TOP_L
+    out = np.zeros((B, L), np.uint64)
+    rc = _lib.load().ks_merge_candidates(src.ctypes.data_as(C.c_void_p), G, B, out.ctypes.data_as(C.c_void_p))
+    if rc != _lib.KS_OK:
+        raise ValueError(f"ks_merge_candidates = {rc}")
+    return out
+
+
 def part_blocks(n_nodes: int, world: int, vshards: int = 1) -> np.ndarray:
     """Block boundaries of the world*vshards parts (ks_load_nodes: p * nblk / G)."""
     n_pad = max(64, (n_nodes + 63) // 64 * 64)

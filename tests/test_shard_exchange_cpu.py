@@ -65,7 +65,8 @@ def _rank_main(rank, world, port, n_nodes, q):
 def _rank_main_layout(rank, world, vsh, port, n_nodes, q):
     """The exchange in the engine's own layout (ks_shard_layout + ks_step): this rank's vsh parts'
     per-pod top-L lists as its contiguous slice of cand_all[G][B][L], one all-gather, then the
-    second merge over the G parts of each pod."""
+    engine's second merge (ks_merge_candidates, the device merge's per-list step) over the G parts
+    of each pod, equal to the global top-L."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -94,8 +95,9 @@ def _rank_main_layout(rank, world, vsh, port, n_nodes, q):
         out = torch.zeros(world * t.numel(), dtype=torch.int64)
         dist.all_gather_into_tensor(out, t)
         cand_all = out.numpy().view(np.uint64).reshape(G, B, shard.TOP_L)
-        merged = shard.merge_lists(cand_all)
-        ok = np.array_equal(merged, np.stack(full)) and np.array_equal(pb, shard.part_blocks(n_nodes, world, vsh))
+        merged = shard.engine_merge(cand_all)  # the engine's own second-merge step
+        ok = (np.array_equal(merged, np.stack(full)) and np.array_equal(merged, shard.merge_lists(cand_all))
+              and np.array_equal(pb, shard.part_blocks(n_nodes, world, vsh)))
         q.put((rank, bool(ok), 0))
     except BaseException as e:
         q.put((rank, False, repr(e)))
