@@ -4,8 +4,9 @@ The 8-GPU layout (8 ranks x 131,072 nodes, candidate lists all-gathered over RCC
 one box, so its data path is exercised here with virtual shards: one engine splits the node range
 into 8 parts, scans and merges each part to an exact per-pod top-L list, then runs the same second
 merge the all-gather feeds (ks_engine.cpp, ks_shard).  Checked:
-  * an exact prefix bind-for-bind against the CPU oracle (kubesim/kubesim.go:90-225) at 1M nodes
-    (the oracle needs ~65 ms per pod here, so the prefix is 200 pods);
+  * an exact prefix bind-for-bind and usage-for-usage against the CPU oracle
+    (kubesim/kubesim.go:90-225) at 1M nodes: 2,000 pods (the OpenMP oracle needs a few ms per pod
+    here on the box's 16 threads);
   * the sharded engine equals the unsharded engine over the whole 100k-pod trace (integer work,
     so any difference is a bug in the exchange);
   * the invariants of test_engine_gpu_large.py on the full run: FIFO one bind per tick, every
@@ -13,6 +14,8 @@ merge the all-gather feeds (ks_engine.cpp, ks_shard).  Checked:
 At 1M nodes the resolver's touched-node filter is the hashed one (nodes > the exact-bitmap range),
 so this is also the full-size parity test of that path.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -22,6 +25,10 @@ from kubesim_amd import tracegen
 pytestmark = pytest.mark.gpu
 MODE = "feeds_all_lrba"
 N_PODS = 100_000
+
+
+def _threads():
+    return int(os.environ.get("OMP_NUM_THREADS") or 0) or min(os.cpu_count() or 1, 16)
 
 
 @pytest.fixture(scope="module")
@@ -34,13 +41,15 @@ def test_c5_sharded_prefix_matches_oracle(c5):
     tr, enc = c5
     eng = make_engine(tr, enc, MODE, shard=(1, 0, None, 8))
     eng.submit(enc["pods"])
-    n = 200
+    n = 2000
     ora = make_oracle(tr, MODE)
+    ora.set_threads(_threads())
     ora.submit(tracegen.slice_pods(tr, 0, n))
     eb = eng.step(n)
     ob, orc = oracle_run(ora, n)
     assert orc == 0
     assert_same_binds(eb, ob)
+    np.testing.assert_array_equal(eng.usage(), ora.usage())
 
 
 def test_c5_sharded_equals_unsharded_full_run(c5):
