@@ -21,8 +21,10 @@ of the per-pod candidate lists per batch), total work fixed as N grows (strong s
 north star's scaling target.  Skipped (with the reason) when ranks share a GPU.
 
 roofline: "frac" is the whole path's fraction of the 80-B-per-evaluation model at 8 TB/s
-(SURVEY.md §8(d)): evals/s x 80 B / 8 TB/s.  The scan kernel's measured HBM traffic (PMC,
-profiles/pmc_scan.json) and the resolver's per-pod latency are reported under it.
+(SURVEY.md §8(d)): evals/s x 80 B / 8 TB/s; "stream_copy_gbs" is the HBM ceiling measured on the
+box (a 2 GiB device copy) and "frac_of_stream_copy" the same model against it.  The scan
+kernel's measured HBM traffic (PMC, profiles/pmc_scan.json) and the resolver's per-pod latency
+are reported under it.
 """
 from __future__ import annotations
 
@@ -93,6 +95,34 @@ def cpu_baseline(trace, scorers, sample_pods, budget_s):
                 pods_per_s=d_mt / t_mt,
                 single_thread={"value": d_st * n / t_st, "pods_per_s": d_st / t_st, "cores": 1,
                                "sample": f"first {d_st} pods, one thread ({t_st:.1f} s)"})
+
+
+def stream_copy_gbs(device: int, mib: int = 2048, reps: int = 10):
+    """Measured HBM ceiling on this box: a device-to-device copy of `mib` MiB,
+    read + write bytes over the time of `reps` copies (torch's copy kernel, HIP events)."""
+    try:
+        import torch
+        if not torch.cuda.is_available():
+            return None
+        n = mib * (1 << 20) // 4
+        a = torch.empty(n, dtype=torch.float32, device=f"cuda:{device}")
+        b = torch.empty_like(a)
+        a.fill_(1.0)
+        b.copy_(a)
+        torch.cuda.synchronize(device)
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0.record()
+        for _ in range(reps):
+            b.copy_(a)
+        t1.record()
+        t1.synchronize()
+        gbs = 2 * a.numel() * 4 * reps / (t0.elapsed_time(t1) * 1e-3) / 1e9
+        del a, b
+        torch.cuda.empty_cache()
+        return round(gbs, 1)
+    except Exception as ex:  # the measurement is informative only
+        log(f"stream copy skipped: {ex}")
+        return None
 
 
 def load_traffic():
@@ -257,6 +287,8 @@ def main():
             "pods_per_s": pods_per_s,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
+                         "stream_copy_gbs": (sc := stream_copy_gbs(local)),
+                         "frac_of_stream_copy": achieved / sc if sc else None,
                          "traffic": traffic["bytes"] if traffic else None,
                          "kernel": "whole path per batch (expire_head + scan + merge + resolve)",
                          "model": "80 B per (pod, node) evaluation (SURVEY.md 8(d)) x evals/s over the timed "
