@@ -1086,7 +1086,12 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
                                         out ? out + (int64_t)i * cap : nullptr, out ? cap : 0, &n_out[i]);
         }
     };
-    const int nth = total >= (1 << 18) ? std::min<int>(S, std::clamp<int>((int)std::thread::hardware_concurrency(), 1, 8)) : 1;
+    // the host's CPU share: OMP_NUM_THREADS when the job sets it (the GPU box does: 16), else the
+    // hardware threads, at most 32
+    int hw = (int)std::thread::hardware_concurrency();
+    if (const char* v = std::getenv("OMP_NUM_THREADS"))
+        if (std::atoi(v) > 0) hw = std::atoi(v);
+    const int nth = total >= (1 << 18) ? std::min<int>(S, std::clamp<int>(hw, 1, 32)) : 1;
     if (nth <= 1) {
         finish(0, S);
     } else {
