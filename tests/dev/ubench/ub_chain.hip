@@ -9,8 +9,18 @@
 
 using namespace ks;
 
+// the micro evaluator's per-node invariants carried by the state (as the register-table
+// resolver's NodeM does): found by overload, so eval_total1_micro skips 2 v_rcp + a multiply
+struct NodeC : NodeV {
+    float ic, im;
+    int32_t d;
+};
+__device__ __forceinline__ float micro_ic(const NodeC& n, int32_t) { return n.ic; }
+__device__ __forceinline__ float micro_im(const NodeC& n, int32_t) { return n.im; }
+__device__ __forceinline__ int32_t micro_d(const NodeC& n, int32_t, int32_t) { return n.d; }
+
 // kVar: 0 the whole chain; 1 without the evaluator (key from the state); 2 the evaluator alone
-// (state kept in registers, no LDS round trip)
+// (state kept in registers, no LDS round trip); 3 as 2 with the invariants cached (NodeC)
 template <int kThreads, int kVar>
 __global__ __launch_bounds__(kThreads) void chain(int iters, Cfg c, const PodRec* gp, const NodeV* gn,
                                                   unsigned long long* out, int* stop) {
@@ -45,12 +55,23 @@ __global__ __launch_bounds__(kThreads) void chain(int iters, Cfg c, const PodRec
     r.ac = tab[0][0]; r.am = tab[1][0]; r.ag = tab[2][0]; r.ap = tab[3][0];
     r.rc = tab[4][0]; r.rm = tab[5][0]; r.rg = tab[6][0]; r.nr = tab[7][0];
     r.taint = tu[0][0]; r.label = tu[1][0];
+    const float ic0 = rcp_est((float)(r.ac > 0 ? r.ac : 1)), im0 = rcp_est((float)(r.am > 0 ? r.am : 1));
     for (int it = 0; it < iters; ++it) {
         const int t = (int)(key & 255u) ^ (it & 255);
         const PodRec p = pods[it & 255], pn = pods[(it + 1) & 255];
         if (kVar == 2) {
             r.rc = (r.rc + (int64_t)(key & 7)) & 1023;  // a dependence on the previous key
             key = make_key(eval_t<kEvalMicro>(c, pn, r), (uint32_t)t);
+            continue;
+        }
+        if (kVar == 3) {
+            NodeC rc;
+            static_cast<NodeV&>(rc) = r;
+            rc.rc = (r.rc + (int64_t)(key & 7)) & 1023;
+            r.rc = rc.rc;
+            const int32_t acs = rc.ac > 0 ? (int32_t)rc.ac : 1, ams = rc.am > 0 ? (int32_t)rc.am : 1;
+            rc.ic = ic0; rc.im = im0; rc.d = mul24(acs, ams);
+            key = make_key(eval_t<kEvalMicro>(c, pn, rc), (uint32_t)t);
             continue;
         }
         NodeV n;
@@ -106,5 +127,6 @@ int main() {
     run<1024>("1 wave + 15 busy waves (3 share its SIMD)", c, p, n, d, stop);
     run<64, 1>("1 wave: LDS state + admission, no evaluator", c, p, n, d, stop);
     run<64, 2>("1 wave: evaluator alone (registers)", c, p, n, d, stop);
+    run<64, 3>("1 wave: evaluator alone, invariants cached", c, p, n, d, stop);
     return 0;
 }
