@@ -20,7 +20,8 @@ __device__ __forceinline__ float micro_im(const NodeC& n, int32_t) { return n.im
 __device__ __forceinline__ int32_t micro_d(const NodeC& n, int32_t, int32_t) { return n.d; }
 
 // kVar: 0 the whole chain; 1 without the evaluator (key from the state); 2 the evaluator alone
-// (state kept in registers, no LDS round trip); 3 as 2 with the invariants cached (NodeC)
+// (state kept in registers, no LDS round trip); 3 as 2 with the invariants cached (NodeC);
+// 4 as 2 with a different state in every lane (vector code, as the resolver's waves run it)
 template <int kThreads, int kVar>
 __global__ __launch_bounds__(kThreads) void chain(int iters, Cfg c, const PodRec* gp, const NodeV* gn,
                                                   unsigned long long* out, int* stop) {
@@ -62,6 +63,12 @@ __global__ __launch_bounds__(kThreads) void chain(int iters, Cfg c, const PodRec
         if (kVar == 2) {
             r.rc = (r.rc + (int64_t)(key & 7)) & 1023;  // a dependence on the previous key
             key = make_key(eval_t<kEvalMicro>(c, pn, r), (uint32_t)t);
+            continue;
+        }
+        if (kVar == 4) {
+            r.rc = (r.rc + (int64_t)(key & 7) + lane) & 1023;  // per-lane state: no scalarization
+            key = make_key(eval_t<kEvalMicro>(c, pn, r), (uint32_t)t);
+            key = (uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)key) | (key & 0xFFFFFFFF00000000ull);
             continue;
         }
         if (kVar == 3) {
@@ -128,5 +135,6 @@ int main() {
     run<64, 1>("1 wave: LDS state + admission, no evaluator", c, p, n, d, stop);
     run<64, 2>("1 wave: evaluator alone (registers)", c, p, n, d, stop);
     run<64, 3>("1 wave: evaluator alone, invariants cached", c, p, n, d, stop);
+    run<64, 4>("1 wave: evaluator alone, per-lane state", c, p, n, d, stop);
     return 0;
 }
