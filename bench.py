@@ -264,7 +264,7 @@ def main():
         scan_model = BYTES_PER_EVAL * pods_per_launch * nodes
         res_ns_pod = st["resolve_ms"] * 1e6 / max(st["pods"], 1)
         cpu = None
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N=1 figure
             cpu = cpu_baseline(trace, scorers, args.cpu_sample_pods, args.cpu_budget_s)
         line = {
             "metric": "pod-node Filter+Score evals/sec and pods bound/sec at 50k nodes, 1-8 GPUs",
