@@ -154,3 +154,24 @@ def test_part_blocks_match_engine_geometry():
     assert pb[0] == 0 and pb[-1] == (50_048 + 255) // 256 and np.all(np.diff(pb) >= 24)
     assert shard.rank_nodes(1000, 4, 3) == (768, 1000)
     assert shard.rank_nodes(100, 4, 0) == (0, 0)  # one block: parts 0..2 empty
+
+
+def test_engine_merge_candidates_random():
+    """ks_merge_candidates (the device merge's per-list step on the host) against a sort of the
+    union, on random sorted 0-padded lists with distinct keys, including empty parts."""
+    rng = np.random.default_rng(7)
+    for G, B in ((1, 5), (3, 17), (8, 64), (16, 3)):
+        keys = np.unique(rng.integers(1, 1 << 40, size=2 * G * B * shard.TOP_L, dtype=np.uint64))
+        keys = rng.permutation(keys)[:G * B * shard.TOP_L]
+        cand = np.sort(keys.reshape(G, B, shard.TOP_L), axis=2)[:, :, ::-1].copy()
+        # ragged: some lists shorter (zero tails), some parts empty for a pod
+        cut = rng.integers(0, shard.TOP_L + 1, size=(G, B))
+        for g in range(G):
+            for b in range(B):
+                cand[g, b, cut[g, b]:] = 0
+        want = np.zeros((B, shard.TOP_L), np.uint64)
+        for b in range(B):
+            u = np.sort(cand[:, b, :].ravel())[::-1]
+            want[b] = u[:shard.TOP_L]
+        np.testing.assert_array_equal(shard.engine_merge(cand), want)
+
