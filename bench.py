@@ -439,7 +439,7 @@ def _c5_leg_body(args, rank, world, local, dist, steps=None, warmup=1, line=None
             n_dev = torch.cuda.device_count()
         except ImportError:
             n_dev = 0
-        if n_dev < world:
+        if n_dev < world and not os.environ.get("KS_BENCH_SHARED_GPU"):  # rehearsal override
             return {"skipped": f"{world} ranks share {n_dev} GPU(s): RCCL needs one GPU per rank"}
     box = {"line": line} if line is not None else {}
     timer = None
@@ -541,6 +541,10 @@ def main_c5(args):
     args.c5_timeout = 0
     line = c5_leg(args, rank, world, local, dist, steps=args.steps, warmup=args.warmup)
     if rank == 0:
+        if "metric" not in line:  # the leg was skipped or failed: say so in a well-formed line
+            line = {"metric": "pod-node Filter+Score evals/sec and pods bound/sec (C5 1M-node sharded cluster)",
+                    "value": None, "unit": "evals/s", "n_gpus": world, "steps": args.steps,
+                    "warmup": args.warmup, "scaling": "strong", **line}
         line.update({"higher_is_better": True, "vs_baseline": None, "dtype": "int64"})
         print(json.dumps(line), flush=True)
     if dist is not None:
