@@ -20,8 +20,8 @@
 //     expiries are applied by the lanes owning their entries; every lane then evaluates pod i+1
 //     on its entries and the wave maximum goes to LDS for the next barrier.
 //   * An untouched winner becomes a new entry: its snapshot record is staged in LDS, gathered
-//     one iteration ahead (plain loads into registers, written to LDS the next iteration, so the
-//     HBM latency hides behind a whole iteration).
+//     one iteration ahead (plain loads into registers at the end of an iteration, written to LDS
+//     at the end of the next, so the HBM latency hides behind a whole iteration).
 //   * No global store inside the loop: binds, statuses and expiry marks are kept in LDS and
 //     written out after it, with the touched nodes' state.
 #include "ks_device.h"
@@ -362,13 +362,6 @@ __global__ __launch_bounds__(C::kThreads) void resolve_kernel(const EngineArgs* 
     for (; i < nb; ++i) {
         R4_STAMP(s0);
         const bool has_next = i + 1 < nb;
-        // staging: pod i+1's records (loaded during the previous iteration) into LDS, then the
-        // loads of pod i+2's
-        if (has_next && st_lane) sh.stage[(i + 1) & 1][st_r * kRecDw + st_d] = st_v;
-        if (i + 2 < nb && st_lane) {
-            const uint64_t key = sh.cand[i + 2][st_r];
-            st_v = key ? rec_dword(a.s, st_d, key_node(key)) : 0u;
-        }
         // every wave: pod i's decision
         uint64_t bw = 0;
 #pragma unroll
@@ -475,6 +468,13 @@ __global__ __launch_bounds__(C::kThreads) void resolve_kernel(const EngineArgs* 
         ck = cn;
         pc = pn;
         pcc = pcn;
+        // staging, off the decision's path: pod i+1's records (loaded during the previous
+        // iteration) into LDS for its bind, then the loads of pod i+2's
+        if (st_lane) sh.stage[(i + 1) & 1][st_r * kRecDw + st_d] = st_v;
+        if (i + 2 < nb && st_lane) {
+            const uint64_t key = sh.cand[i + 2][st_r];
+            st_v = key ? rec_dword(a.s, st_d, key_node(key)) : 0u;
+        }
         R4_STAMP(s5);
         R4_ACC(4, s5 - s4);
         __syncthreads();
