@@ -42,10 +42,10 @@ for k, name in ((0, "w0 work"), (1, "w0 wait"), (2, "w1 work"), (3, "w2 work"), 
                 (5, "w3 top"), (6, "w3 load"), (7, "w3 excl"), (8, "w3 eval"),
                 (11, "w1 fetch+fit"), (12, "w1 expiries"), (14, "w1 eval")):
     print(f"  {name:12s} {D[k]/max(pods,1):9.0f} cycles/pod")
-for k, name in ((5, "w0 insert"), (6, "w0 commit"), (7, "walker")):
+for k, name in ((5, "w0 insert"), (6, "w0 commit"), (7, "w0 issue")):
     print(f"  {name:12s} {d[k]/max(pods,1):9.0f} cycles/pod")
-print(f"  {'owner lanes':12s} {D[9]/max(pods,1):9.2f} per pod")
-print(f"  {'speculation':12s} {D[10]/max(pods,1):9.0f} cycles/pod")
+for k, name in ((9, "owner lanes"), (10, "owner waves")):
+    print(f"  {name:12s} {D[k]/max(pods,1):9.2f} per pod")
 L = max(d[14] or st["launches"], 1)
 print(f"  launches {d[14]}  pods/launch {pods / L:.1f}  expiries/launch {d[15] / L:.1f}")
 for k, name in ((8, "init+search"), (9, "loads"), (10, "pre-insert"), (11, "table loads"), (12, "prologue"), (13, "writeback")):
