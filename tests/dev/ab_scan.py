@@ -20,8 +20,10 @@ eng.load_nodes(enc["alloc"], enc["taint"], enc["label"])
 eng.submit(enc["pods"])
 eng.step(2048)
 eng.set_profiling(True)
-eng.step(8192)
+b = eng.step(8192)
+import zlib  # noqa: E402
+crc = zlib.crc32(b["node"].tobytes() + b["status"].tobytes())
 st = eng.last_step_stats()
 n = max(st["launches"], 1)
 print(f"{sys.argv[1]} {cfg}: scan {st['scan_ms'] / n * 1e3:.1f} us  resolve {st['resolve_ms'] / n * 1e3:.1f} us  "
-      f"other {st['other_ms'] / n * 1e3:.1f} us  launches {n}", flush=True)
+      f"other {st['other_ms'] / n * 1e3:.1f} us  launches {n}  binds {len(b)} crc {crc:08x}", flush=True)
