@@ -307,7 +307,12 @@ constexpr int64_t kMicroProd = 1LL << 24;
 constexpr int64_t kMicroReq = 1LL << 17;
 constexpr float kMicroBias = 1.0f / 131072.0f;  // 2^-17
 
-__host__ __device__ __forceinline__ int32_t clamp_micro(int64_t q) { return (int32_t)(q < kMicroReq ? q : kMicroReq); }
+// requests are >= 0: q < 2^17 tested on the two 32-bit halves, which the scalar unit can do for a
+// uniform pod (it has no 64-bit less-than, so a 64-bit compare would go to the VALU)
+__host__ __device__ __forceinline__ int32_t clamp_micro(int64_t q) {
+    const uint32_t lo = (uint32_t)q, hi = (uint32_t)((uint64_t)q >> 32);
+    return (int32_t)((hi | (lo >> 17)) ? (uint32_t)kMicroReq : lo);
+}
 
 // a * b for 0 <= a, b < 2^24 (full-rate 24-bit multiply on the device)
 __host__ __device__ __forceinline__ int32_t mul24(int32_t a, int32_t b) {
@@ -317,6 +322,27 @@ __host__ __device__ __forceinline__ int32_t mul24(int32_t a, int32_t b) {
     return a * b;
 #endif
 }
+// a * b + c for 0 <= a, b < 2^24 (v_mad_u32_u24); only the low 32 bits are kept.  Inline asm:
+// with a uniform operand the compiler would otherwise emit a quarter-rate v_mul_lo_u32.
+__host__ __device__ __forceinline__ uint32_t umad24(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+#else
+    return (uint32_t)((uint64_t)a * b) + c;
+#endif
+}
+// |a - b| (v_sad_u32)
+__host__ __device__ __forceinline__ uint32_t usad(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __usad(a, b, 0u);
+#else
+    return a > b ? a - b : b - a;
+#endif
+}
+// largest weight the micro evaluator multiplies with a 24-bit multiply (the host's mode choice)
+constexpr int64_t kMicroWeight = 1LL << 24;
 
 // floor(10 x / A) for 0 <= x <= A < 2^16 given r = 10 * rcp_est(A) (exactness: above)
 __host__ __device__ __forceinline__ int32_t lr10_micro(int32_t x, float r) {
@@ -333,39 +359,51 @@ __host__ __device__ __forceinline__ float micro_im(const NS&, int32_t ams) { ret
 template <class NS>
 __host__ __device__ __forceinline__ int32_t micro_d(const NS&, int32_t acs, int32_t ams) { return mul24(acs, ams); }
 
+// Written for a short dependent chain (the resolver evaluates a just-bound node on its critical
+// path): every term is computed unconditionally from the free amounts f = A - u and selected at
+// the end, so LeastRequested, both BalancedAllocation paths and the filters run side by side.
+//   * LeastRequested: max(trunc(fma(f, r, 2^-17)), 0) — the exact floor for 0 <= f <= A; for
+//     f < 0 (does not fit) or A <= 0 (then f <= 0) the fma is < 1, so the clamp gives the
+//     reference's 0.
+//   * BalancedAllocation is non-zero only when both free amounts are > 0 (which implies A > 0);
+//     otherwise its products are computed on out-of-domain values (unsigned, no overflow trap)
+//     and discarded.
+//   * weights < kMicroWeight (the host's mode choice): the weighted sum is two 24-bit mads.
 template <class NS>
 __host__ __device__ __forceinline__ uint32_t eval_total1_micro(const Cfg& c, const PodRec& p, const NS& n) {
     const int32_t ac = (int32_t)n.ac, am = (int32_t)n.am, ag = (int32_t)n.ag;
-    const int32_t rc = (int32_t)n.rc, rm = (int32_t)n.rm, rg = (int32_t)n.rg;
     const int32_t qc = clamp_micro(p.req[0]), qm = clamp_micro(p.req[1]), qg = clamp_micro(p.req[2]);
-    const int32_t uc = rc + qc, um = rm + qm;
+    // free after placing: (A - r) is per node (hoisted out of the scan's pod loop)
+    const int32_t fc = (ac - (int32_t)n.rc) - qc, fm = (am - (int32_t)n.rm) - qm, fg = (ag - (int32_t)n.rg) - qg;
     const bool fit_on = c.filter_feeds && (c.filters & kFilterFit);
     const bool taint_on = c.filter_feeds && (c.filters & kFilterTaint);
     const bool sel_on = c.filter_feeds && (c.filters & kFilterSelector);
     const uint32_t km = p.keymask;
     bool ok = c.has_scorers != 0;
-    ok &= !fit_on | ((n.nr < n.ap) & (!(km & 1) | (uc <= ac)) & (!(km & 2) | (um <= am)) &
-                     (!(km & 4) | (rg + qg <= ag)));
+    ok &= !fit_on | ((n.nr < n.ap) & (!(km & 1) | (fc >= 0)) & (!(km & 2) | (fm >= 0)) & (!(km & 4) | (fg >= 0)));
     ok &= !taint_on | ((n.taint & ~p.tol) == 0);
     ok &= !sel_on | ((n.label & p.sel) == p.sel);
-    const bool lc_on = ac > 0 && uc <= ac, lm_on = am > 0 && um <= am;
     const int32_t acs = ac > 0 ? ac : 1, ams = am > 0 ? am : 1;
     const float iac = micro_ic(n, acs), iam = micro_im(n, ams);  // node-invariant: hoisted
     const float rc10 = 10.f * iac, rm10 = 10.f * iam;
-    const int32_t lc = lc_on ? lr10_micro(ac - uc, rc10) : 0;
-    const int32_t lm = lm_on ? lr10_micro(am - um, rm10) : 0;
-    const bool ba_on = ac > 0 && am > 0 && uc < ac && um < am;
-    const int32_t ucs = ba_on ? uc : 0, ums = ba_on ? um : 0;
-    const int32_t D = micro_d(n, acs, ams), a = mul24(ucs, ams), b = mul24(ums, acs);
-    const int32_t X = a > b ? a - b : b - a;
-    const int32_t N = mul24(D - X, 10);
-    int32_t q = (int32_t)(10.f - 10.f * fabsf((float)ucs * iac - (float)ums * iam));
+    const float fcf = (float)fc, fmf = (float)fm;  // exact: |f| < 2^24
+    const int32_t lc0 = (int32_t)fmaf(fcf, rc10, kMicroBias), lm0 = (int32_t)fmaf(fmf, rm10, kMicroBias);
+    const uint32_t lrs = (uint32_t)((lc0 > 0 ? lc0 : 0) + (lm0 > 0 ? lm0 : 0)) >> 1;
+    const bool ba_on = (fc < fm ? fc : fm) > 0;
+    const uint32_t D = (uint32_t)micro_d(n, acs, ams);
+    // X = |uc Am - um Ac| = |fm Ac - fc Am| (u = A - f)
+    const uint32_t a = umad24((uint32_t)fm, (uint32_t)acs, 0u), b = umad24((uint32_t)fc, (uint32_t)ams, 0u);
+    const uint32_t X = usad(a, b);
+    const uint32_t N = umad24(D - X, 10u, 0u);
+    // estimate of 10 (D - X) / D = 10 - 10 |fm/Am - fc/Ac| (within 1e-5; the step below is exact)
+    int32_t q = (int32_t)(10.f - fabsf(fmaf(fmf, rm10, -fcf * rc10)));
     q = q < 0 ? 0 : (q > 10 ? 10 : q);
-    const int32_t t = mul24(q, D);
+    const uint32_t t = umad24((uint32_t)q, D, 0u);
     q += (N >= t + D) ? 1 : 0;
     q -= (N < t) ? 1 : 0;
-    const int32_t total = c.const_total + c.w_lr * ((lc + lm) >> 1) + c.w_ba * (ba_on ? q : 0);
-    return ok ? (uint32_t)total + 1u : 0u;
+    const uint32_t base = umad24((uint32_t)c.w_lr, lrs, (uint32_t)c.const_total + 1u);
+    const uint32_t total1 = umad24((uint32_t)c.w_ba, ba_on ? (uint32_t)q : 0u, base);
+    return ok ? total1 : 0u;
 }
 
 // Evaluator variants: 0 wide (64/128-bit), 1 narrow (capacities < 2^29), 2 tiny, 3 micro (above).

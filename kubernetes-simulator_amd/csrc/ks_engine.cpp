@@ -248,7 +248,8 @@ void update_mode(ks_engine* e) {
     const bool narrow = m[0] < ks::kNarrowCap && m[1] < ks::kNarrowCap && m[2] < ks::kNarrowCap;
     const bool tiny = m[0] < ks::kTinyCap && m[1] < ks::kTinyCap && m[2] < ks::kTinyCap && m[0] * m[1] < ks::kTinyCap;
     const bool micro = m[0] < ks::kMicroCap && m[1] < ks::kMicroCap && m[2] < ks::kMicroCap &&
-                       m[0] * m[1] < ks::kMicroProd;
+                       m[0] * m[1] < ks::kMicroProd && e->dc.w_lr < ks::kMicroWeight &&
+                       e->dc.w_ba < ks::kMicroWeight;
     const bool no_tiny = (e->flags & KS_ENGINE_NO_TINY) != 0;
     e->mode = (e->flags & KS_ENGINE_FORCE_WIDE) ? ks::kEvalWide
             : (micro && !no_tiny && !(e->flags & KS_ENGINE_NO_MICRO)) ? ks::kEvalMicro

@@ -50,3 +50,22 @@ extern "C" void ks_host_prune_batch(const ks::Cfg* c, int64_t n, const int64_t* 
         tmax[i] = ks::prune_tmax(*c, ks::prune_prep(*c, v), (float)p.req[0], (float)p.req[1]);
     }
 }
+// per case: the micro evaluator (capacities < 2^16, Ac*Am < 2^24) of pod req[i] on node i;
+// tol/sel/taint/label exercise the filter masks
+extern "C" void ks_host_micro_batch(const ks::Cfg* c, int64_t n, const int64_t* alloc /*[n][4]*/,
+                                    const int64_t* run /*[n][4]: rc rm rg nr*/, const int64_t* req /*[n][3]*/,
+                                    const uint32_t* keymask, const uint64_t* masks /*[n][4]: taint label tol sel*/,
+                                    uint32_t* total1, uint32_t* total1_m) {
+    for (int64_t i = 0; i < n; i++) {
+        ks::NodeV v{};
+        v.ac = alloc[i * 4 + 0]; v.am = alloc[i * 4 + 1]; v.ag = alloc[i * 4 + 2]; v.ap = alloc[i * 4 + 3];
+        v.rc = run[i * 4 + 0]; v.rm = run[i * 4 + 1]; v.rg = run[i * 4 + 2]; v.nr = run[i * 4 + 3];
+        v.taint = masks[i * 4 + 0]; v.label = masks[i * 4 + 1];
+        ks::PodRec p{};
+        p.req[0] = req[i * 3 + 0]; p.req[1] = req[i * 3 + 1]; p.req[2] = req[i * 3 + 2];
+        p.keymask = keymask[i];
+        p.tol = masks[i * 4 + 2]; p.sel = masks[i * 4 + 3];
+        total1[i] = ks::eval_total1(*c, p, v);
+        total1_m[i] = ks::eval_total1_micro(*c, p, v);
+    }
+}

@@ -173,3 +173,44 @@ def test_tiny_eval_exact(lib, feeds, const, w_lr, w_ba, cap_bits):
     t1t = np.zeros(n, np.uint32)
     lib.ks_host_prune_batch(C.byref(c), n, _p(alloc), _p(run), _p(req), _p(t1), _p(t1n), _p(tm), _p(t1t))
     np.testing.assert_array_equal(t1t, t1)
+
+
+@pytest.mark.parametrize("feeds,filters,const,w_lr,w_ba", [(1, 7, 0, 1, 1), (0, 0, 0, 1, 1), (1, 1, 5, 2, 0),
+                                                           (0, 0, 3, 0, 3), (1, 7, 0, 7, 13),
+                                                           (1, 3, 1000, (1 << 24) - 1, 50)])
+@pytest.mark.parametrize("cap_bits", [4, 11, 12])
+def test_micro_eval_exact(lib, feeds, filters, const, w_lr, w_ba, cap_bits):
+    """eval_total1_micro == the wide evaluator on the micro domain (capacities < 2^16, Ac*Am < 2^24,
+    weights < 2^24): fit boundaries (free amount 0 / -1), absent (-1) and zero capacities, absent
+    request keys, clamped requests, the pods capacity and the taint / selector masks."""
+    rng = np.random.default_rng(5000 + cap_bits * 11 + w_lr % 97 * 3 + w_ba + const + filters)
+    n = 100_000
+    alloc, run3, req = _nodes(rng, n, cap_bits)
+    alloc[:, 3] = rng.integers(0, 4, n)
+    run = np.zeros((n, 4), np.int64)
+    run[:, :3] = run3
+    run[:, 3] = rng.integers(0, 4, n)
+    # exact-fit and one-over boundaries, C3-like unit multiples, clamp path
+    for k in range(3):
+        cap = np.maximum(alloc[:, k], 0)
+        edge = rng.random(n) < 0.15
+        req[edge, k] = np.maximum(cap[edge] - run[edge, k] + rng.integers(-1, 2, edge.sum()), 0)
+    req[rng.random(n) < 0.03, 0] = 1 << 40
+    req[rng.random(n) < 0.03, 1] = (1 << 17) + 5
+    req[rng.random(n) < 0.03, 2] = (1 << 17) - 1
+    assert (np.maximum(alloc[:, 0], 0) * np.maximum(alloc[:, 1], 0) < (1 << 24)).all()
+    keymask = rng.integers(0, 8, n).astype(np.uint32)
+    masks = np.zeros((n, 4), np.uint64)
+    bits = lambda p: np.where(rng.random(n) < p, np.uint64(1) << rng.integers(0, 64, n).astype(np.uint64), np.uint64(0))
+    masks[:, 0] = bits(0.3) | bits(0.2)  # node taints
+    masks[:, 1] = bits(0.5) | bits(0.5)  # node labels
+    masks[:, 2] = masks[:, 0] | bits(0.3)  # tolerations: usually all
+    masks[rng.random(n) < 0.2, 2] = 0
+    masks[:, 3] = np.where(rng.random(n) < 0.5, masks[:, 1] & bits(1.0), bits(0.2))  # selectors
+    c = Cfg(n_nodes=n, nwb=0, filter_feeds=feeds, filters=filters, has_scorers=1, w_lr=w_lr,
+            w_ba=w_ba, const_total=const, tick_seconds=1)
+    t1 = np.zeros(n, np.uint32); t1m = np.zeros(n, np.uint32)
+    lib.ks_host_micro_batch.argtypes = [C.POINTER(Cfg), C.c_int64] + [C.c_void_p] * 7
+    lib.ks_host_micro_batch(C.byref(c), n, _p(alloc), _p(run), _p(req), _p(keymask), _p(masks), _p(t1), _p(t1m))
+    assert (t1 > 0).sum() > n // 10
+    np.testing.assert_array_equal(t1m, t1)
