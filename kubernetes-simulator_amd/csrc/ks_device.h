@@ -443,6 +443,23 @@ __host__ __device__ __forceinline__ PruneF prune_prep(const Cfg& c, const NS& n)
     f.live = c.has_scorers && !(c.filter_feeds && (c.filters & kFilterFit) && n.nr >= n.ap);
     return f;
 }
+// The same for capacities < 2^29 (every evaluator but the wide one): A - r fits int32, so each
+// conversion is one v_cvt instead of an int64-to-float sequence (identical values).
+template <int kMode, class NS>
+__host__ __device__ __forceinline__ PruneF prune_prep_t(const Cfg& c, const NS& n) {
+    if constexpr (kMode >= kEvalNarrow) {
+        const int32_t ac = (int32_t)n.ac, am = (int32_t)n.am;
+        PruneF f;
+        f.ic = ac > 0 ? rcp_est((float)ac) : 0.f;
+        f.bc = ac > 0 ? (float)(ac - (int32_t)n.rc) * f.ic : -1.f;
+        f.im = am > 0 ? rcp_est((float)am) : 0.f;
+        f.bm = am > 0 ? (float)(am - (int32_t)n.rm) * f.im : -1.f;
+        f.live = c.has_scorers && !(c.filter_feeds && (c.filters & kFilterFit) && n.nr >= n.ap);
+        return f;
+    } else {
+        return prune_prep(c, n);
+    }
+}
 __host__ __device__ __forceinline__ uint32_t prune_tmax(const Cfg& c, const PruneF& f, float qc, float qm) {
     const float fc = fmaf(-qc, f.ic, f.bc), fm = fmaf(-qm, f.im, f.bm);
     int32_t total = c.const_total;
