@@ -27,9 +27,6 @@
 // highest total, ties to the lowest node index.
 #include "ks_device.h"
 
-#include <cstdlib>
-#include <cstring>
-
 namespace ks {
 
 constexpr int kScanWaves = 4;            // 256-thread scan workgroups, one 256-node block each
@@ -731,7 +728,7 @@ __global__ __launch_bounds__(C::kThreads) void resolve_kernel(const EngineArgs* 
     } else if (oslot >= 0 && r < sh.n_t) {
         own = t_node(sh, r);
         own_node = sh.tnode[r];
-        own_pf = prune_prep(a.c, own);
+        own_pf = prune_prep_t<kMode>(a.c, own);
         loaded = true;
         const uint64_t k = make_key(eval_t<kMode>(a.c, sh.pod[0], own), (uint32_t)own_node);
         if (k != 0 && k >= sh.cand[0][kL - 1]) fold_best(&sh.ctl[0].best, ikey(k, r));
@@ -798,11 +795,11 @@ __global__ __launch_bounds__(C::kThreads) void resolve_kernel(const EngineArgs* 
                     if (!loaded) {
                         own = t_node(sh, r);
                         own_node = sh.tnode[r];
-                        own_pf = prune_prep(a.c, own);
+                        own_pf = prune_prep_t<kMode>(a.c, own);
                         loaded = true;
                     } else if (dr == i) {
                         own.rc = sh.ts[4][r]; own.rm = sh.ts[5][r]; own.rg = sh.ts[6][r]; own.nr = sh.ts[7][r];
-                        own_pf = prune_prep(a.c, own);
+                        own_pf = prune_prep_t<kMode>(a.c, own);
                     }
                 }
                 bool want = r < nt && own_pf.live && r != went;
@@ -977,440 +974,6 @@ __global__ __launch_bounds__(C::kThreads) void resolve_kernel(const EngineArgs* 
         atomicAdd(&d[15], (unsigned long long)e_cnt);  // expiries in windows
     }
 #endif
-}
-
-// ------------------------------------------------------------------------------------------
-// resolve, owner-binds form: the same exact walk with one role per wave, no hand-off of node state
-// between waves and few LDS instructions per pod (the LDS pipe is shared by every wave of the CU:
-// ~16 LDS wave-instructions per wave per pod, as the first version of this kernel issued, made
-// the pipe, not the chain, set the pace).
-//
-//   wave 0       the list walker: commits pod i+1's best untouched list node (chosen among three
-//                prefetched candidates: the ones still untouched when pod i+1's list was walked,
-//                two iterations earlier, minus pod i-1's and pod i's winners), stages its record,
-//                walks pod i+3's list, issues its three candidates' record loads (two iterations
-//                of HBM latency hidden) and fills pod i+3's control slot
-//   waves 1..12  owners: lane r keeps table entry r — node state, prune bound, and the next
-//                expiry due on it — in registers for the whole launch.  The owner of pod i's
-//                winner binds it itself (admission, outputs, table insert of a new node) and
-//                evaluates pod i+1 on the new state at once; every owner applies the expiries
-//                due on its entry before pod i+1 (a per-entry list, checked against a register)
-//                and evaluates pod i+1 unless the prune bound excludes it.  Keys are folded into
-//                the pod's decision word with LDS atomic max.  Pod records come from HBM (vector
-//                loads one iteration ahead), not from LDS.
-// Per pod every wave reads its control slot (two 16-byte LDS loads) and nothing else in the
-// common case.  One barrier per pod; the chain is the bound lane's: decision read, admission,
-// bind, evaluation, fold.  States go back to HBM straight from the owner registers.
-// ------------------------------------------------------------------------------------------
-template <int THREADS, int TMAX, int HASH_LOG2, int MAXB, int FBITS_LOG2>
-struct OCfg {
-    static constexpr int kThreads = THREADS;
-    static constexpr int kTMax = TMAX;
-    static constexpr int kHashLog2 = HASH_LOG2;
-    static constexpr int kHash = 1 << HASH_LOG2;
-    static constexpr int kMaxBatchR = MAXB;
-    static constexpr int kMaxExp = TMAX - MAXB;
-    static constexpr int kFilterBits = 1 << FBITS_LOG2;
-    static_assert(TMAX == (THREADS / kWave - 1) * kWave, "one table entry per owner thread");
-    static_assert(TMAX - MAXB <= THREADS, "one thread per pre-inserted expiry");
-};
-using OBig = OCfg<832, 768, 11, 256, 16>;
-static_assert(OBig::kMaxBatchR == RBig::kMaxBatchR, "both resolvers take the same batches");
-
-// Pod p's control slot (ctl[p & 3]), 32 bytes read by every wave as two 16-byte loads.
-enum : uint32_t { kCtlDur = 1u << 8 };  // bits: pod flags | kCtlDur when the pod runs if bound Ok
-struct alignas(16) OCtl {
-    uint64_t best;      // pod p's winner (ikey), folded during the previous iteration
-    uint64_t lbk_next;  // lower bound of pod p+1's winner key
-    int32_t kfull;      // every untouched entry of a full list is gone: the batch must stop
-    uint32_t bits;
-    int32_t exp_slot;   // window slot of pod p's own expiry, or -1
-    int32_t e1;         // end of pod p+1's expiry window: slots < e1 are due before pod p+1 binds
-};
-
-template <class C>
-struct OwnerShared {
-    using Cfg = C;
-    static constexpr int kTMax = C::kTMax, kHash = C::kHash, kMaxBatchR = C::kMaxBatchR, kMaxExp = C::kMaxExp,
-                         kFilterBits = C::kFilterBits;
-    int32_t tnode[kTMax];
-    int32_t ehead[kTMax];       // first window slot of the entry's expiry list, -1: none
-    int32_t hkey[kHash];
-    int32_t hval[kHash];
-    uint32_t tfilt[kFilterBits / 32];
-    PodCtl pctl[kMaxBatchR + 3];  // exp_slot: window slot of the pod's own expiry, or -1
-    uint64_t cand[kMaxBatchR + 3][kL];
-    int32_t ex_q[kMaxExp];
-    int32_t ex_next[kMaxExp];   // next slot of the same entry's expiry list
-    int32_t ex_entry[kMaxExp];
-    int32_t ex_ok[kMaxExp];
-    int32_t ex_node[kMaxExp];
-    int64_t ex_req[kMaxExp][3];
-    OCtl ctl[4];
-    int64_t stage[2][10];       // pod p's best untouched list node's record, slot p & 1
-    int32_t n_t, committed, err_code, err_pod, nb, e_cnt;
-};
-
-// Walker state for one pod: its first three list entries untouched at walk time (0 = none), whether
-// the list is full, and their records (lanes 0..29: field lane % 10 of candidate lane / 10).
-struct Prefetch3 {
-    int64_t val;
-    uint64_t k[3];
-    bool full;
-};
-
-// Walk pod p's list (touched: the table filter, which holds every winner up to the previous
-// iteration, plus `excl`, this iteration's winner), fill pod p's control slot (reset: its decision
-// word too — the slot last held pod p - 4) and pod p-1's lower bound of pod p's winner, issue the
-// record loads.  Two more winners may join before pod p is decided, so the first untouched entry
-// then is one of the three, and the third bounds the winner from below.
-template <class SH>
-__device__ __forceinline__ void walk3(const EngineArgs& a, SH& sh, int p, int lane, bool exact, int32_t excl,
-                                      bool reset, Prefetch3& pf) {
-    const uint64_t c = lane < kL ? sh.cand[p][lane] : 0ull;
-    const bool ok = c != 0 && key_node(c) != excl && !is_touched(sh, key_node(c), exact);
-    uint64_t m = __ballot(ok);
-    pf.full = __popcll(__ballot(c != 0)) == kL;
-#pragma unroll
-    for (int s = 0; s < 3; ++s) {
-        const int pa = m ? __ffsll((unsigned long long)m) - 1 : -1;
-        m &= m - 1;
-        pf.k[s] = pa >= 0 ? readlane64(c, pa) : 0ull;
-    }
-    if (lane == 0) {
-        const PodCtl pc = sh.pctl[p], pn = sh.pctl[p + 1];
-        const uint64_t last = pf.k[1] ? pf.k[1] : pf.k[0];
-        sh.ctl[(p - 1) & 3].lbk_next = pf.k[2] ? pf.k[2] : (pf.full ? last : 0ull);
-        OCtl& o = sh.ctl[p & 3];
-        if (reset) { o.best = 0; o.kfull = 0; }
-        o.bits = pc.flags | (pc.dur > 0 ? kCtlDur : 0u);
-        o.exp_slot = pc.exp_slot;
-        o.e1 = pn.ex_hi;
-    }
-    const int slot = lane / 10;
-    const uint64_t ks = slot == 0 ? pf.k[0] : (slot == 1 ? pf.k[1] : pf.k[2]);
-    if (lane < 30 && ks != 0) pf.val = node_field(a.s, lane % 10, key_node(ks));
-}
-
-// Pod p's best untouched list node given the two winners decided since its walk (-1: none):
-// stage its record, fold its key, set kfull.
-template <class SH>
-__device__ __forceinline__ void commit3(SH& sh, int p, int lane, const Prefetch3& pf, int32_t w1, int32_t w2,
-                                        bool allow_stop) {
-    int slot = -1;
-#pragma unroll
-    for (int s = 2; s >= 0; --s) {
-        const int32_t nd = key_node(pf.k[s]);
-        if (pf.k[s] != 0 && nd != w1 && nd != w2) slot = s;
-    }
-    const uint64_t key = slot == 0 ? pf.k[0] : (slot == 1 ? pf.k[1] : (slot == 2 ? pf.k[2] : 0ull));
-    if (slot >= 0 && lane < 30 && lane / 10 == slot) sh.stage[p & 1][lane % 10] = pf.val;
-    if (lane == 0) {
-        if (slot >= 0) fold_best(&sh.ctl[p & 3].best, ikey(key, kEntUntouched));
-        if (allow_stop && slot < 0 && pf.full) sh.ctl[p & 3].kfull = 1;
-    }
-}
-
-// smallest slot > `above` in entry r's expiry list (INT32_MAX: none)
-template <class SH>
-__device__ __forceinline__ int32_t exp_min_above(const SH& sh, int r, int32_t above) {
-    int32_t best = INT32_MAX;
-    for (int32_t x = sh.ehead[r]; x >= 0; x = sh.ex_next[x])
-        if (x > above && x < best) best = x;
-    return best;
-}
-
-// a 16-byte-aligned record of 10 int64 fields in LDS as five 16-byte loads
-__device__ __forceinline__ NodeV stage_node5(const int64_t* s) {
-    const ulonglong2* w = reinterpret_cast<const ulonglong2*>(s);
-    const ulonglong2 a = w[0], b = w[1], c = w[2], d = w[3], e = w[4];
-    NodeV v;
-    v.ac = (int64_t)a.x; v.am = (int64_t)a.y; v.ag = (int64_t)b.x; v.ap = (int64_t)b.y;
-    v.rc = (int64_t)c.x; v.rm = (int64_t)c.y; v.rg = (int64_t)d.x; v.nr = (int64_t)d.y;
-    v.taint = e.x; v.label = e.y;
-    return v;
-}
-
-// a pod record from HBM with vector loads (every lane the same address; vmcnt only, so neither an
-// LDS wait nor the barrier waits for it)
-__device__ __forceinline__ void pod_issue(const PodRec* src, uint4 (&w)[3]) {
-    typedef const __attribute__((address_space(1))) uint32_t* gp;
-    const gp g = (gp)src;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        w[k].x = g[4 * k]; w[k].y = g[4 * k + 1]; w[k].z = g[4 * k + 2]; w[k].w = g[4 * k + 3];
-    }
-}
-__device__ __forceinline__ PodRec pod_from(const uint4 (&w)[3]) {
-    PodRec p;
-    __builtin_memcpy(&p, &w[0], 16);
-    __builtin_memcpy(reinterpret_cast<char*>(&p) + 16, &w[1], 16);
-    __builtin_memcpy(reinterpret_cast<char*>(&p) + 32, &w[2], 16);
-    return p;
-}
-
-template <int kMode, class C>
-__global__ __launch_bounds__(C::kThreads) void resolve_owner_kernel(const EngineArgs* __restrict__ A) {
-    constexpr int kTMax = C::kTMax, kHash = C::kHash, kMaxBatchR = C::kMaxBatchR, kMaxExp = C::kMaxExp,
-                  kFilterBits = C::kFilterBits, kThreads = C::kThreads;
-    __shared__ OwnerShared<C> sh;
-    const EngineArgs a = A[blockIdx.x];
-    const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid >> 6;
-    const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
-    if (a.ctr[kCtrErr] != 0) return;
-    const bool exact = a.c.n_nodes <= kFilterBits;
-    int nb = (int)min<int64_t>(min<int64_t>(a.B, kMaxBatchR), end - start);
-    if (nb <= 0) return;
-
-    // expiry window of pods start+1 .. start+nb-1, batch shrunk to fit it (as resolve_kernel)
-    const int64_t e_base = a.exp_off[start + 1];
-    const int64_t off_mid = tid < nb ? a.exp_off[start + tid + 1] : 0;
-    const bool fits_win = tid < nb && off_mid - e_base <= kMaxExp;
-    if (tid == 0) {
-        sh.n_t = 0; sh.err_code = 0; sh.err_pod = -1;
-        for (int b = 0; b < 4; ++b) sh.ctl[b] = OCtl{0, 0, 0, 0, -1, 0};
-    }
-    for (int h = tid; h < kHash; h += kThreads) sh.hkey[h] = -1;
-    for (int w = tid; w < kFilterBits / 32; w += kThreads) sh.tfilt[w] = 0;
-    for (int e = tid; e < kTMax; e += kThreads) sh.ehead[e] = -1;
-    nb = __syncthreads_count(fits_win);
-    if (tid == nb - 1) { sh.nb = nb; sh.committed = nb; sh.e_cnt = nb > 1 ? (int32_t)(off_mid - e_base) : 0; }
-    __syncthreads();
-    const int64_t e_cnt = sh.e_cnt;
-
-    for (int i = tid; i < nb; i += kThreads) {
-        PodCtl pc;
-        pc.flags = a.pods[start + i].flags;
-        pc.ex_lo = i <= 1 ? 0 : (int32_t)(a.exp_off[start + i] - e_base);
-        pc.ex_hi = i + 1 <= 1 ? 0 : (int32_t)(a.exp_off[start + i + 1] - e_base);
-        pc.dur = a.dur[start + i];
-        const int64_t pos = a.exp_pos[start + i];
-        pc.exp_slot = (pos >= e_base && pos - e_base < e_cnt) ? (int32_t)(pos - e_base) : -1;
-        pc.pad[0] = pc.pad[1] = pc.pad[2] = 0;
-        sh.pctl[i] = pc;
-    }
-    for (int i = tid; i < nb * kL; i += kThreads) sh.cand[i / kL][i % kL] = a.cand[i];
-    for (int i = tid; i < 3 * kL; i += kThreads) sh.cand[nb + i / kL][i % kL] = 0;
-    if (tid < 3) sh.pctl[nb + tid] = PodCtl{0, 0, 0, 0, -1, {0, 0, 0}};
-    for (int e = tid; e < e_cnt; e += kThreads) {
-        const int32_t q = a.exp_pod[e_base + e];
-        const PodRec& pq = a.pods[q];
-        sh.ex_q[e] = q;
-        sh.ex_entry[e] = -1;
-        sh.ex_req[e][0] = pq.req[0]; sh.ex_req[e][1] = pq.req[1]; sh.ex_req[e][2] = pq.req[2];
-        if (q < start) {
-            sh.ex_node[e] = a.b_node[q];
-            sh.ex_ok[e] = (a.b_status[q] == 0) && !a.expired[q];
-        } else {
-            sh.ex_node[e] = -1;
-            sh.ex_ok[e] = 0;  // an in-batch pod's expiry joins its entry's list when it binds
-        }
-    }
-    __syncthreads();
-    // pre-insert every node an expiry of this batch lands on (see resolve_kernel)
-    const bool pre_want = tid < e_cnt && sh.ex_ok[tid];
-    int pre_slot = -1;
-    bool pre_claim = false;
-    if (pre_want) {
-        const int32_t nd = sh.ex_node[tid];
-        uint32_t hs = hslot<OwnerShared<C>>(nd);
-        for (;;) {
-            const int32_t prev = atomicCAS(&sh.hkey[hs], -1, nd);
-            if (prev == -1 || prev == nd) { pre_slot = (int)hs; pre_claim = prev == -1; break; }
-            hs = (hs + 1) & (kHash - 1);
-        }
-    }
-    __syncthreads();
-    if (pre_claim) {
-        const int32_t nd = sh.ex_node[tid];
-        const int idx = atomicAdd(&sh.n_t, 1);
-        sh.hval[pre_slot] = idx;
-        sh.tnode[idx] = nd;
-        const uint32_t f = (uint32_t)nd & (kFilterBits - 1);
-        atomicOr(&sh.tfilt[f >> 5], 1u << (f & 31));
-    }
-    __syncthreads();
-    if (pre_want) {  // the slot joins its entry's expiry list (list order is immaterial)
-        const int ent = sh.hval[pre_slot];
-        sh.ex_next[tid] = atomicExch(&sh.ehead[ent], (int32_t)tid);
-    }
-    __syncthreads();
-
-    // ---- prologue: owners load their entries and fold pod 0; the walker commits pod 0 and walks
-    // pods 1 and 2
-    const int n_t0 = sh.n_t;
-    const bool owner = wave >= 1;
-    const int r = owner ? (wave - 1) * kWave + lane : kTMax;
-    const int wr0 = (wave - 1) * kWave;  // first entry of this owner wave
-    const PodRec* gpods = a.pods + start;
-    NodeV own{};
-    int32_t own_node = -1;
-    PruneF own_pf{};
-    int32_t next_x = INT32_MAX;  // the earliest window slot due on this entry
-    Prefetch3 pfa{}, pfb{};      // walker: pods i+1, i+2
-    uint4 pw1[3] = {};           // owners: pod i+1 (raw, loaded one iteration ahead)
-    if (owner) {
-        if (wr0 >= n_t0 + nb) return;  // can never own an entry (see resolve_kernel)
-        if (nb > 1) pod_issue(gpods + 1, pw1);
-        if (r < n_t0) {
-            own_node = sh.tnode[r];
-            own = load_node(a.s, own_node);
-            own_pf = prune_prep_t<kMode>(a.c, own);
-            next_x = exp_min_above(sh, r, -1);
-            const uint64_t k = make_key(eval_t<kMode>(a.c, gpods[0], own), (uint32_t)own_node);
-            if (k != 0 && k >= sh.cand[0][kL - 1]) fold_best(&sh.ctl[0].best, ikey(k, r));
-        }
-    } else {
-        // (the owners fold pod 0 concurrently: the slots were zeroed above and are not reset here)
-        Prefetch3 p0{};
-        walk3(a, sh, 0, lane, exact, -1, false, p0);
-        if (nb > 1) walk3(a, sh, 1, lane, exact, -1, false, pfa);
-        if (nb > 2) walk3(a, sh, 2, lane, exact, -1, false, pfb);
-        commit3(sh, 0, lane, p0, -1, -1, false);  // pod 0 never stops on an exhausted list
-    }
-    __syncthreads();
-
-    int nt = n_t0;        // table size before the current pod
-    int32_t w_prev = -1;  // winner node of the previous pod
-    PodRec p = gpods[0];  // pod i (the binder's request and key mask)
-#ifdef KS_STAMPS  // diagnostic: cycles per phase, ctr[16..27] (tests/dev/diag_owner.py)
-    uint64_t acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-#endif
-    int i = 0;
-    for (; i < nb; ++i) {
-        KS_STAMP(s0);
-        const int64_t j = start + i;
-        const bool has_next = i + 1 < nb;
-        // the control slot (two 16-byte loads), and for the lane that would hold a new entry the
-        // record of pod i's best untouched list node
-        const OCtl& cs = sh.ctl[i & 3];
-        const ulonglong2 c0 = *reinterpret_cast<const ulonglong2*>(&cs.best);
-        const uint4 c1 = *reinterpret_cast<const uint4*>(&cs.kfull);
-        if (owner && r == nt) own = stage_node5(sh.stage[i & 1]);  // lane nt holds no entry yet
-        const uint64_t bw = c0.x, lbk = c0.y;
-        const uint32_t bits = (uint32_t)__builtin_amdgcn_readfirstlane((int)c1.y);
-        const int32_t exp_slot = __builtin_amdgcn_readfirstlane((int)c1.z);
-        const int32_t e1 = has_next ? __builtin_amdgcn_readfirstlane((int)c1.w) : 0;
-        int stop = 0;
-        if (c1.x) stop = 1;                                      // list exhausted: rescan
-        else if (bw == 0) stop = 2;                              // NotFound
-        else if (bits & (kFlagBadKey | kFlagBadSpec)) stop = 3;  // InvalidArgument
-        if (stop) {
-            if (tid == 0) {
-                sh.committed = i;
-                if (stop > 1) { sh.err_code = stop == 2 ? kErrNotFound : kErrEinval; sh.err_pod = (int32_t)j; }
-            }
-            break;
-        }
-        const int went = ikey_ent(bw);
-        const int32_t nd = ikey_node(bw);
-        const int t = went >= 0 ? went : nt;
-        KS_STAMP(s1);
-#ifdef KS_STAMPS
-        const bool binder_wave = owner && t >= wr0 && t < wr0 + kWave;
-        uint64_t s2 = s1, s3 = s1;
-#endif
-        if (owner) {
-            const PodRec pn = pod_from(pw1);  // pod i+1 (loaded one iteration ago)
-            if (i + 2 < nb) pod_issue(gpods + i + 2, pw1);
-            bool changed = false;
-            if (r == t) {  // the bind of pod i (kubesim/node/node.go:36-60)
-                if (went < 0) {
-                    own_node = nd;
-                    sh.tnode[t] = nd;
-                    t_insert(sh, nd, t, exact);
-                }
-                const bool ok = fits(p, own);
-                const bool gone = exp_slot >= 0 && exp_slot < e1;  // its own expiry is due before pod i+1
-                if (ok && (bits & kCtlDur) && !gone) {
-                    own.rc += p.req[0]; own.rm += p.req[1]; own.rg += p.req[2]; own.nr += 1;
-                    if (exp_slot >= 0) {  // due later in this batch: joins the entry's list
-                        sh.ex_next[exp_slot] = sh.ehead[r];
-                        sh.ehead[r] = exp_slot;
-                        next_x = exp_slot < next_x ? exp_slot : next_x;
-                    }
-                }
-                if (gone && ok) gptr(a.expired)[j] = 1;
-                gptr(a.b_node)[j] = nd;
-                gptr(a.b_status)[j] = ok ? 0 : 1;
-                changed = true;
-            }
-#ifdef KS_STAMPS
-            s2 = stamp();
-#endif
-            // expiries due on this entry before pod i+1 binds (rare: a register compare)
-            while (next_x < e1) {
-                const int32_t x = next_x;
-                own.rc -= sh.ex_req[x][0]; own.rm -= sh.ex_req[x][1]; own.rg -= sh.ex_req[x][2]; own.nr -= 1;
-                gptr(a.expired)[sh.ex_q[x]] = 1;
-                next_x = exp_min_above(sh, r, x);
-                changed = true;
-            }
-            const int nt1 = went < 0 ? nt + 1 : nt;
-            if (has_next && r < nt1) {
-                bool want = r == t;  // the bound entry is evaluated at once (its bound is stale)
-                if (!want) {
-                    if (changed) own_pf = prune_prep_t<kMode>(a.c, own);
-                    want = own_pf.live;
-                    if (want && lbk != 0) {
-                        // the exact conversion the bound's slack assumes (BalancedAllocation is not
-                        // monotone in the request, so no clamped stand-in)
-                        const float qfc = (float)pn.req[0], qfm = (float)pn.req[1];
-                        want = make_key(prune_tmax(a.c, own_pf, qfc, qfm) + 1u, (uint32_t)own_node) >= lbk;
-                    }
-                }
-                if (want) {
-                    const uint64_t k = make_key(eval_t<kMode>(a.c, pn, own), (uint32_t)own_node);
-                    if (k != 0 && k >= lbk) fold_best(&sh.ctl[(i + 1) & 3].best, ikey(k, r));
-                }
-            }
-#ifdef KS_STAMPS
-            s3 = stamp();
-#endif
-            if (r == t) own_pf = prune_prep_t<kMode>(a.c, own);
-            p = pn;
-        } else {
-            if (has_next) commit3(sh, i + 1, lane, pfa, w_prev, nd, true);
-#ifdef KS_STAMPS
-            s2 = stamp();
-#endif
-            pfa = pfb;
-            if (i + 3 < nb) walk3(a, sh, i + 3, lane, exact, nd, true, pfb);
-        }
-        nt = went < 0 ? nt + 1 : nt;
-        w_prev = nd;
-        KS_STAMP(s4);
-        __syncthreads();
-        KS_STAMP(s5);
-#ifdef KS_STAMPS
-        if (!owner) {
-            acc[0] += s1 - s0; acc[1] += s2 - s1; acc[2] += s4 - s2; acc[3] += s5 - s4; acc[10] += 1;
-        } else if (binder_wave) {
-            acc[4] += s1 - s0; acc[5] += s2 - s1; acc[6] += s3 - s2; acc[7] += s4 - s3; acc[8] += s5 - s4;
-            acc[9] += 1;
-        } else {
-            acc[11] += s4 - s0;  // other owner waves' work
-        }
-#endif
-    }
-#ifdef KS_STAMPS
-    if (lane == 0)
-        for (int k = 0; k < 12; ++k) atomicAdd((unsigned long long*)a.ctr + 16 + k, (unsigned long long)acc[k]);
-#endif
-    __syncthreads();
-
-    // ---- write back the mutable fields of every entry, straight from the owner registers
-    if (owner && r < nt && own_node >= 0) {
-        gptr(a.s.rc)[own_node] = own.rc;
-        gptr(a.s.rm)[own_node] = own.rm;
-        gptr(a.s.rg)[own_node] = own.rg;
-        gptr(a.s.nr)[own_node] = own.nr;
-    }
-    if (tid == 0) {
-        a.ctr[kCtrStart] = start + sh.committed;
-        if (sh.committed < a.B && sh.err_code == 0 && start + sh.committed < end) a.ctr[kCtrEarly] += 1;
-        if (sh.err_code) { a.ctr[kCtrErr] = sh.err_code; a.ctr[kCtrErrPod] = sh.err_pod; }
-    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1632,23 +1195,8 @@ static void launch_resolve_t(const EngineArgs* d, int S, int mode, hipStream_t s
     }
 }
 
-template <class C>
-static void launch_resolve_owner_t(const EngineArgs* d, int S, int mode, hipStream_t st) {
-    switch (mode) {
-        case kEvalMicro: hipLaunchKernelGGL((resolve_owner_kernel<kEvalMicro, C>), dim3(S), dim3(C::kThreads), 0, st, d); break;
-        case kEvalTiny: hipLaunchKernelGGL((resolve_owner_kernel<kEvalTiny, C>), dim3(S), dim3(C::kThreads), 0, st, d); break;
-        case kEvalNarrow: hipLaunchKernelGGL((resolve_owner_kernel<kEvalNarrow, C>), dim3(S), dim3(C::kThreads), 0, st, d); break;
-        default: hipLaunchKernelGGL((resolve_owner_kernel<kEvalWide, C>), dim3(S), dim3(C::kThreads), 0, st, d); break;
-    }
-}
-
 hipError_t launch_resolve(const EngineArgs* d, int S, int mode, hipStream_t st) {
-    static const int owner = [] {
-        const char* v = std::getenv("KS_RESOLVER");
-        return v && std::strcmp(v, "owner") == 0 ? 1 : 0;
-    }();
-    if (owner) launch_resolve_owner_t<OBig>(d, S, mode, st);
-    else launch_resolve_t<RBig>(d, S, mode, st);
+    launch_resolve_t<RBig>(d, S, mode, st);
     return hipGetLastError();
 }
 
