@@ -881,6 +881,10 @@ struct ks_group {
     int32_t* h_out = nullptr;           // pinned mirror of d_out
     int64_t out_cap = 0;
     hipEvent_t ev[2] = {nullptr, nullptr};
+    // the second half of the scenarios runs its batch rounds on its own stream: one half's
+    // latency-bound resolvers then share the GPU with the other half's throughput-bound scans
+    hipStream_t st2 = nullptr;
+    hipEvent_t xev = nullptr;  // argument upload done (st -> st2)
     std::string errmsg;
 };
 
@@ -892,6 +896,8 @@ ks_status ks_group_create(int32_t device, int32_t max_scenarios, ks_group** out)
     g->cap = max_scenarios;
     hipError_t r = hipSetDevice(device);
     if (r == hipSuccess) r = hipStreamCreateWithFlags(&g->st, hipStreamNonBlocking);
+    if (r == hipSuccess) r = hipStreamCreateWithFlags(&g->st2, hipStreamNonBlocking);
+    if (r == hipSuccess) r = hipEventCreateWithFlags(&g->xev, hipEventDisableTiming);
     if (r == hipSuccess) r = hipMalloc(&g->d_ctr, sizeof(int64_t) * 32 * max_scenarios);
     if (r == hipSuccess) r = hipHostMalloc(&g->h_ctr, sizeof(int64_t) * 32 * max_scenarios, hipHostMallocDefault);
     if (r == hipSuccess) r = hipMalloc(&g->d_args, sizeof(ks::EngineArgs) * max_scenarios);
@@ -922,7 +928,10 @@ void ks_group_destroy(ks_group* g) {
     if (g->h_seg) (void)hipHostFree(g->h_seg);
     if (g->d_out) (void)hipFree(g->d_out);
     if (g->h_out) (void)hipHostFree(g->h_out);
+    if (g->st2) (void)hipStreamSynchronize(g->st2);
     for (auto ev : g->ev) if (ev) (void)hipEventDestroy(ev);
+    if (g->xev) (void)hipEventDestroy(g->xev);
+    if (g->st2) (void)hipStreamDestroy(g->st2);
     if (g->st) (void)hipStreamDestroy(g->st);
     delete g;
 }
@@ -954,6 +963,12 @@ ks_status ks_group_add(ks_group* g, const ks_config* cfg, ks_engine** out) {
 }
 
 int32_t ks_group_size(const ks_group* g) { return g ? (int32_t)g->engs.size() : -1; }
+
+// groups of at least this many scenarios run as two halves on two streams
+#ifndef KS_GROUP_SPLIT_MIN
+#define KS_GROUP_SPLIT_MIN 64
+#endif
+constexpr int kGroupSplitMin = KS_GROUP_SPLIT_MIN;
 
 ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, int64_t* n_out, int32_t* status_out,
                         ks_step_stats* stats) {
@@ -1020,22 +1035,41 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
     std::vector<int64_t> start(S);
     for (int i = 0; i < S; i++) start[i] = g->engs[i]->done;
     int64_t launches = 0;
+    // scenario halves [h_lo[h], h_lo[h + 1]) on streams st / st2 (one stream for small groups)
+    const int nh = S >= kGroupSplitMin ? 2 : 1;
+    const int h_lo[3] = {0, nh == 2 ? S / 2 : S, S};
+    hipStream_t hst[2] = {st, g->st2};
+    if (nh == 2 && (!dev(hipEventRecord(g->xev, st)) || !dev(hipStreamWaitEvent(g->st2, g->xev, 0))))
+        return dev_fail("group step: stream ordering failed");
     while (true) {
-        int64_t nbat = 0;
-        for (int i = 0; i < S; i++)
-            if (live[i]) nbat = std::max(nbat, (p_hi[i] - start[i] + B - 1) / B);
-        if (nbat == 0) break;
-        for (int64_t b = 0; b < nbat; b++) {
-            if (!dev(ks::launch_expire_head(g->d_args, S, st)) ||
-                !dev(ks::launch_scan(g->d_args, S, blk_n, B, pg, mode, k16, st)) ||
-                !dev(ks::launch_merge(g->d_args, S, B, nullptr, 0, 0, 0, nullptr, blk_n, st)) ||
-                !dev(launch_resolver(g->d_args, S, mode, small, st)))
-                return dev_fail("group step: kernel launch failed");
+        int64_t nbat[2] = {0, 0};
+        for (int h = 0; h < nh; h++)
+            for (int i = h_lo[h]; i < h_lo[h + 1]; i++)
+                if (live[i]) nbat[h] = std::max(nbat[h], (p_hi[i] - start[i] + B - 1) / B);
+        if (nbat[0] == 0 && nbat[1] == 0) break;
+        // the halves' rounds issued alternately: independent scenarios, no ordering between them
+        // (a token that made the halves' scans take turns measured no better)
+        for (int64_t b = 0; b < std::max(nbat[0], nbat[1]); b++) {
+            for (int h = 0; h < nh; h++) {
+                if (b >= nbat[h]) continue;
+                const ks::EngineArgs* d = g->d_args + h_lo[h];
+                const int Sh = h_lo[h + 1] - h_lo[h];
+                if (!dev(ks::launch_expire_head(d, Sh, hst[h])) ||
+                    !dev(ks::launch_scan(d, Sh, blk_n, B, pg, mode, k16, hst[h])) ||
+                    !dev(ks::launch_merge(d, Sh, B, nullptr, 0, 0, 0, nullptr, blk_n, hst[h])) ||
+                    !dev(launch_resolver(d, Sh, mode, small, hst[h])))
+                    return dev_fail("group step: kernel launch failed");
+            }
             launches++;
         }
-        if (!dev(hipMemcpyAsync(g->h_ctr, g->d_ctr, sizeof(int64_t) * 32 * S, hipMemcpyDeviceToHost, st)) ||
-            !dev(hipStreamSynchronize(st)))
-            return dev_fail("group step: device synchronisation failed");
+        for (int h = 0; h < nh; h++) {
+            const int64_t lo = h_lo[h], n = h_lo[h + 1] - h_lo[h];
+            if (n && !dev(hipMemcpyAsync(g->h_ctr + 32 * lo, g->d_ctr + 32 * lo, sizeof(int64_t) * 32 * n,
+                                         hipMemcpyDeviceToHost, hst[h])))
+                return dev_fail("group step: device synchronisation failed");
+        }
+        for (int h = 0; h < nh; h++)
+            if (!dev(hipStreamSynchronize(hst[h]))) return dev_fail("group step: device synchronisation failed");
         for (int i = 0; i < S; i++) {
             if (!live[i]) continue;
             ks_engine* e = g->engs[i];
