@@ -336,17 +336,18 @@ __global__ __launch_bounds__(256) void merge_small_kernel(const EngineArgs* __re
 // issued together (a chain of dependent reads here costs ~150 cycles per link).
 struct alignas(16) Ctl {
     uint64_t best;   // pod's winner (ikey), folded during the previous iteration
-    uint64_t lbk;    // lower bound of the pod's winner key (prefetch_issue)
+    uint64_t lbk_next;  // lower bound of the NEXT pod's winner key (prefetch_issue), read with best
     int32_t kfull;   // every entry of a full list touched: the batch must stop
     int32_t ntab;    // table size when the pod is evaluated
     int32_t pad[2];
 };
-struct alignas(16) PodCtl {
-    uint32_t flags;
-    int32_t ex_lo, ex_hi;  // window range of the expiries due before the pod binds
-    int32_t dur;           // ticks the pod runs if bound Ok
-    int32_t exp_slot;      // window slot of this pod's own expiry, or -1
-    int32_t pad[3];
+// Per-pod control read by every wave each iteration: one 16-byte LDS load (pod i's flags, run
+// ticks and own expiry slot; pod i+1's expiry window)
+struct alignas(16) PodCC {
+    uint32_t w0;     // flags | (exp_slot + 1) << 2
+    int32_t dur;     // ticks the pod runs if bound Ok
+    int32_t ex_lo1;  // pod i+1's expiry window [ex_lo1, ex_hi1) (empty for the batch's last pod)
+    int32_t ex_hi1;
 };
 
 template <class C>
@@ -363,7 +364,7 @@ struct ResolveShared {
     uint32_t tfilt[kFilterBits / 32];
     PodRec pod[kMaxBatchR + 1];  // +1: pod i + 1 is read unconditionally
     float podf[kMaxBatchR][2];  // cpu / memory requests as float (prune_tmax)
-    PodCtl pctl[kMaxBatchR + 1];
+    PodCC pcc[kMaxBatchR];
     uint64_t cand[kMaxBatchR][kL];
     int32_t ex_q[kMaxExp];
     int32_t ex_node[kMaxExp];
@@ -551,7 +552,8 @@ __device__ __forceinline__ void prefetch_issue(const EngineArgs& a, SH& sh, int 
     const int pa2 = m ? __ffsll((unsigned long long)m) - 1 : -1;
     pf.key1 = pa1 >= 0 ? readlane64(c, pa1) : 0ull;
     pf.key2 = pa2 >= 0 ? readlane64(c, pa2) : 0ull;
-    if (lane == 0) sh.ctl[p % 3].lbk = pf.key2 ? pf.key2 : (pf.full ? pf.key1 : 0ull);
+    // into pod p-1's slot: read by every wave together with pod p-1's decision
+    if (lane == 0) sh.ctl[(p + 2) % 3].lbk_next = pf.key2 ? pf.key2 : (pf.full ? pf.key1 : 0ull);
     const uint64_t ks = lane < 10 ? pf.key1 : pf.key2;
     if (lane < 20 && ks != 0) pf.val = node_field(a.s, lane % 10, key_node(ks));
 }
@@ -638,17 +640,17 @@ __global__ __launch_bounds__(C::kThreads) void resolve_kernel(const EngineArgs* 
         sh.podf[i][0] = (float)a.pods[start + i].req[0];
         sh.podf[i][1] = (float)a.pods[start + i].req[1];
         const int64_t pos = a.exp_pos[start + i];
-        PodCtl pc;
-        pc.flags = a.pods[start + i].flags;
-        pc.ex_lo = i <= 1 ? 0 : (int32_t)(a.exp_off[start + i] - e_base);
-        pc.ex_hi = i + 1 <= 1 ? 0 : (int32_t)(a.exp_off[start + i + 1] - e_base);
+        const int32_t exp_slot = (pos >= e_base && pos - e_base < e_cnt) ? (int32_t)(pos - e_base) : -1;
+        PodCC pc;
+        pc.w0 = a.pods[start + i].flags | (uint32_t)(exp_slot + 1) << 2;
         pc.dur = a.dur[start + i];
-        pc.exp_slot = (pos >= e_base && pos - e_base < e_cnt) ? (int32_t)(pos - e_base) : -1;
-        pc.pad[0] = pc.pad[1] = pc.pad[2] = 0;
-        sh.pctl[i] = pc;
+        // pod i+1's window: the expiries due before it binds (pod start's were applied by expire_head)
+        const bool nx = i + 1 < nb;
+        pc.ex_lo1 = !nx || i + 1 <= 1 ? 0 : (int32_t)(a.exp_off[start + i + 1] - e_base);
+        pc.ex_hi1 = !nx ? 0 : (int32_t)(a.exp_off[start + i + 2] - e_base);
+        sh.pcc[i] = pc;
     }
     for (int i = tid; i < nb * kL; i += kResolveThreads) sh.cand[i / kL][i % kL] = a.cand[i];
-    if (tid == 0) sh.pctl[nb] = PodCtl{0, 0, 0, 0, -1, {0, 0, 0}};
     for (int e = tid; e < e_cnt; e += kResolveThreads) {
         const int32_t q = a.exp_pod[e_base + e];
         const PodRec& pq = a.pods[q];
@@ -760,13 +762,13 @@ __global__ __launch_bounds__(C::kThreads) void resolve_kernel(const EngineArgs* 
         const int b_cur = i % 3, b_nxt = (i + 1) % 3;
         // ---- every wave: pod i's winner and the stop decision (identical in all waves)
         const Ctl cc = sh.ctl[b_cur];
-        const PodCtl pci = sh.pctl[i], pcn = sh.pctl[i + 1];
-        const uint64_t lbk = sh.ctl[b_nxt].lbk;
+        const PodCC pci = sh.pcc[i];
+        const uint64_t lbk = cc.lbk_next;
         const uint64_t bw = cc.best;
         int stop = 0;
         if (cc.kfull) stop = 1;                                       // list exhausted: rescan
         else if (bw == 0) stop = 2;                                   // NotFound
-        else if (pci.flags & (kFlagBadKey | kFlagBadSpec)) stop = 3;  // InvalidArgument
+        else if (pci.w0 & (kFlagBadKey | kFlagBadSpec)) stop = 3;     // InvalidArgument
         if (stop) {
             if (tid == 0) {
                 sh.committed = i;
@@ -779,7 +781,7 @@ __global__ __launch_bounds__(C::kThreads) void resolve_kernel(const EngineArgs* 
         const int nt = cc.ntab;
         const int t = went >= 0 ? went : nt;  // an untouched winner becomes entry nt
         const bool has_next = i + 1 < nb;
-        const int e0 = has_next ? pcn.ex_lo : 0, e1 = has_next ? pcn.ex_hi : 0;
+        const int e0 = pci.ex_lo1, e1 = pci.ex_hi1;
         KS_STAMP(sw);
 #ifdef KS_STAMPS
         acc_sub[0] += sw - s0;
@@ -874,7 +876,7 @@ __global__ __launch_bounds__(C::kThreads) void resolve_kernel(const EngineArgs* 
                 }
                 sh.ts[4][t] = n.rc; sh.ts[5][t] = n.rm; sh.ts[6][t] = n.rg; sh.ts[7][t] = n.nr;
                 sh.dirty[t] = i + 1;
-                const int slot = pci.exp_slot;
+                const int slot = (int)(pci.w0 >> 2) - 1;
                 if (slot >= 0) { sh.ex_entry[slot] = t; sh.ex_ok[slot] = ok ? 1 : 0; }
                 gptr(a.b_node)[j] = nd;
                 gptr(a.b_status)[j] = ok ? 0 : 1;
