@@ -32,7 +32,10 @@ namespace ks {
 constexpr int kScanWaves = 4;            // 256-thread scan workgroups, one 256-node block each
 constexpr int kBlockNodes = kScanWaves * kWave;
 constexpr int kL = kTopL;                // candidate list length per pod
-constexpr int kMaxPG = 32;               // pods per scan workgroup (LDS list staging)
+#ifndef KS_MAX_PG
+#define KS_MAX_PG 32
+#endif
+constexpr int kMaxPG = KS_MAX_PG;        // pods per scan workgroup (LDS key table rows)
 #ifndef KS_SCAN_UNROLL
 #define KS_SCAN_UNROLL 4
 #endif
