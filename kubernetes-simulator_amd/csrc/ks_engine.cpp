@@ -487,10 +487,11 @@ ks_status ks_load_nodes(ks_engine* e, int64_t n, const int64_t* alloc, const uin
     e->blk_lo = e->part_lo[e->rank * e->vsh];
     e->blk_n = e->part_lo[(e->rank + 1) * e->vsh] - e->blk_lo;
     // default batch: small clusters exhaust a pod's top-L list after fewer binds, so a batch of
-    // 256 would mostly commit early and rescan; ~n/16 pods (>= 64) keeps most of each batch
-    // (measured on C4's 2,000-node scenarios: 128 pods 7.9e7 pods/s vs 256 pods 6.1e7)
+    // 256 would mostly commit early and rescan; ~n/16 pods rounded down to a multiple of 32
+    // (>= 64) keeps most of each batch (C4's 2,000-node scenarios: 96 pods 2.64e11 evals/s, 128
+    // pods 2.57e11, 64 pods 2.56-2.63e11; round 1: 256 pods 6.1e7 pods/s vs 128 pods 7.9e7)
     if (!e->cfg.batch_pods && n < 16 * kDefaultBatch)
-        e->B = (int)std::clamp<int64_t>((n / 16 + 31) / 32 * 32, 64, kDefaultBatch);
+        e->B = (int)std::clamp<int64_t>(n / 16 / 32 * 32, 64, kDefaultBatch);
     // pods per scan workgroup: the most pod reuse per node load that still leaves >= ~2048
     // workgroups (8 per CU) per scan
     int pg = 1;
