@@ -1,0 +1,227 @@
+"""Dev tool (not a test): exact integer model of the two-pods-per-barrier resolver.
+
+Runs the C3 batched walk (as `resolve_stats.py` does: snapshot top-L lists, touched set = expiry
+nodes of the window + in-batch winners) and decides the pods two at a time, the way the planned
+kernel would after one barrier:
+
+* pod i: its candidates C_i are the touched entries whose exact key reaches the key of the first
+  untouched entry of pod i's list (the list candidate), plus that list candidate; w_i = max of C_i;
+* pod i+1, from values computed BEFORE w_i is known:
+    K1(n) = key of pod i+1 on n if n does not win pod i (state: expiries of tick i+2 applied),
+    K2(c) = key of pod i+1 on c if c wins pod i (c in C_i: bind, its own expiry if it lasts
+            one tick),
+    M2'   = max of K1 over the touched entries that are not candidates of pod i,
+    u1/u2 = first and second untouched entries of pod i+1's list;
+  w_{i+1} = max(M2', K1(c) for touched c != w_i in C_i, K2(w_i), u1 if u1 != w_i else u2).
+
+Every decision is checked against the sequential argmax over all nodes. Reported: candidate-set
+sizes, how often the second list entry is needed, how many K1 evaluations survive a float bound
+against the lower bound key(u2) that is known before the barrier, and the commits per batch.
+
+    python tests/dev/pair_model.py --nodes 50000 --batches 8
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from resolve_stats import keys, scores, tracegen, encode  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nodes", type=int, default=50_000)
+    ap.add_argument("--pods", type=int, default=20_000)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--batches", type=int, default=8)
+    ap.add_argument("--skip", type=int, default=8000, help="pods bound sequentially before measuring")
+    ap.add_argument("--L", type=int, default=8)
+    a = ap.parse_args()
+    tr = tracegen.c3_trace(n_nodes=a.nodes, n_pods=a.pods)
+    enc = encode.encode_trace(tr)
+    al = enc["alloc"]
+    ac, am, ag, apd = al[:, 0].copy(), al[:, 1].copy(), al[:, 2].copy(), al[:, 3].copy()
+    N = a.nodes
+    st_ = [np.zeros(N, np.int64) for _ in range(4)]  # rc, rm, rg, nr
+    taint = enc["taint"].astype(np.uint64); label = enc["label"].astype(np.uint64)
+    P = enc["pods"]
+    req = P["req"].reshape(-1, 3)
+    km = P["keymask"]
+    req = req * ((km[:, None] >> np.arange(3)) & 1)
+    tol = P["tol"].astype(np.uint64); sel = P["sel"].astype(np.uint64)
+    poff, psec = P["phase_off"], P["phase_sec"]
+    S = np.add.reduceat(psec.astype(np.int64), poff[:-1]) if len(psec) else np.zeros(len(req))
+    dur = -(-S // tr["tick_seconds"])
+    nid = np.arange(N, dtype=np.int64)
+    fin = {}
+    node_of = np.full(len(req), -1)
+
+    def pod(j):
+        return dict(req=req[j], tol=tol[j], sel=sel[j])
+
+    def key_all(j, state=None):
+        s = st_ if state is None else state
+        return keys(scores(ac, am, ag, apd, s[0], s[1], s[2], s[3], taint, label, pod(j)), nid)
+
+    def expire(t, state=None, skip=None):
+        s = st_ if state is None else state
+        out = []
+        for q in fin.get(t, []) if state is not None else fin.pop(t, []):
+            if q == skip:
+                continue
+            n = node_of[q]
+            s[0][n] -= req[q, 0]; s[1][n] -= req[q, 1]; s[2][n] -= req[q, 2]; s[3][n] -= 1
+            out.append(int(n))
+        return out
+
+    def admitted(j, n, s):
+        qc, qm, qg = req[j]
+        return (s[3][n] < apd[n]) and s[0][n] + qc <= ac[n] and s[1][n] + qm <= am[n] and s[2][n] + qg <= ag[n]
+
+    def bind(j, n, t):
+        ok = admitted(j, n, st_)
+        node_of[j] = n
+        if ok and dur[j] > 0:
+            st_[0][n] += req[j, 0]; st_[1][n] += req[j, 1]; st_[2][n] += req[j, 2]; st_[3][n] += 1
+            fin.setdefault(t + dur[j], []).append(j)
+
+    def tbound(n_idx, j, s):
+        """prune_tmax's float upper bound of total (ks_device.h), filters ignored"""
+        qc, qm, _ = req[j]
+        a_c, a_m = ac[n_idx].astype(np.float32), am[n_idx].astype(np.float32)
+        ic = np.where(a_c > 0, 1 / np.maximum(a_c, 1), 0).astype(np.float32)
+        im = np.where(a_m > 0, 1 / np.maximum(a_m, 1), 0).astype(np.float32)
+        fc = np.where(a_c > 0, (a_c - s[0][n_idx]) * ic, -1) - qc * ic
+        fm = np.where(a_m > 0, (a_m - s[1][n_idx]) * im, -1) - qm * im
+        lc = np.where(fc > -1.5e-5, np.floor(10 * fc + 1.5e-5), 0)
+        lm = np.where(fm > -1.5e-5, np.floor(10 * fm + 1.5e-5), 0)
+        tot = (lc + lm) // 2
+        tot = tot + np.where((fc > -1.5e-5) & (fm > -1.5e-5), np.floor(10 - 10 * np.abs(fc - fm) + 3e-5), 0)
+        return keys(tot.astype(np.int64) + 1, n_idx)
+
+    j = 0
+    while j < a.skip:
+        expire(j + 1)
+        bind(j, int(np.argmax(key_all(j))), j + 1)
+        j += 1
+
+    stats = dict(pairs=0, single=0, checked=0, cand=[], from_list=0, need_u2=0, exhausted=0,
+                 k1_all=[], k1_bound=[], k1_bound_u1=[], commits=[], w1_src={})
+    for b in range(a.batches):
+        s0 = j
+        expire(s0 + 1)
+        lists = []
+        for i in range(a.batch):
+            k = key_all(s0 + i)
+            top = np.argsort(-k)[:a.L]
+            lists.append([(int(k[x]), int(x)) for x in top if k[x] > 0])
+        pre = set()
+        for i in range(1, a.batch):
+            for q in fin.get(s0 + i + 1, []):
+                pre.add(int(node_of[q]))
+        touched = set(pre)
+
+        def list_cand(i, excl):
+            lst = lists[i]
+            unt = [(kk, x) for kk, x in lst if x not in touched and x not in excl]
+            if not unt and len(lst) == a.L:
+                return None, None          # exhausted: the walk stops before this pod
+            u = unt[0] if unt else (0, -1)
+            u2 = unt[1] if len(unt) > 1 else ((0, -1) if len(lst) < a.L else None)
+            return u, u2
+
+        i = 0
+        while i < a.batch:
+            jj = s0 + i
+            if i > 0:
+                expire(jj + 1)
+            u, _ = list_cand(i, ())
+            if u is None:
+                stats["exhausted"] += 1
+                break
+            k_i = key_all(jj)
+            T = np.fromiter(touched, np.int64, len(touched))
+            cand = [int(n) for n in T[k_i[T] >= u[0]]] if len(T) else []
+            stats["cand"].append(len(cand))
+            best = max([(int(k_i[n]), n) for n in cand] + [u])
+            w = best[1]
+            assert w == int(np.argmax(k_i)), ("pod i", jj)
+            stats["checked"] += 1
+            if i + 1 >= a.batch:
+                bind(jj, w, jj + 1)
+                touched.add(w)
+                stats["single"] += 1
+                i += 1
+                break
+            # pod i+1, computed before w is known
+            v1, v2 = list_cand(i + 1, ())
+            if v1 is None:
+                # pod i+1 exhausted even before pod i's winner: commit pod i alone
+                bind(jj, w, jj + 1)
+                touched.add(w)
+                stats["single"] += 1
+                stats["exhausted"] += 1
+                i += 1
+                break
+            s1 = [x.copy() for x in st_]
+            expire(jj + 2, state=s1)                       # tick i+2's expiries (pod i excluded)
+            k1 = key_all(jj + 1, s1)
+            lb = v2[0] if v2 is not None else 0            # key(u2): a lower bound known early
+            if len(T):
+                stats["k1_all"].append(len(T))
+                stats["k1_bound"].append(int((tbound(T, jj + 1, s1) >= lb).sum()))
+                stats["k1_bound_u1"].append(int((tbound(T, jj + 1, s1) >= v1[0]).sum()))
+            cset = set(cand)
+            m2 = max([(int(k1[n]), int(n)) for n in T if int(n) not in cset] + [(0, -1)])
+            k1c = [(int(k1[c]), c) for c in cand if c != w]
+            # K2: the candidate's key for pod i+1 if it wins pod i
+            s2 = [x.copy() for x in s1]
+            if admitted(jj, w, st_) and dur[jj] > 1:
+                s2[0][w] += req[jj, 0]; s2[1][w] += req[jj, 1]; s2[2][w] += req[jj, 2]; s2[3][w] += 1
+            k2 = (int(key_all(jj + 1, s2)[w]), w)
+            if v1[1] == w:
+                stats["need_u2"] += 1
+                lcand = v2
+                if lcand is None:
+                    # exhausted for pod i+1 after w: commit pod i alone
+                    bind(jj, w, jj + 1)
+                    touched.add(w)
+                    stats["single"] += 1
+                    stats["exhausted"] += 1
+                    i += 1
+                    break
+            else:
+                lcand = v1
+            if w == u[1]:
+                stats["from_list"] += 1
+            w1 = max([m2, k2, lcand] + k1c)
+            # ground truth: the sequential walk
+            bind(jj, w, jj + 1)
+            touched.add(w)
+            expire(jj + 2)
+            kt = key_all(jj + 1)
+            assert w1[1] == int(np.argmax(kt)) and w1[0] == int(kt.max()), ("pod i+1", jj + 1, w1, kt.max())
+            src = "K2" if w1 is k2 else "list" if w1 is lcand else "M2'" if w1 is m2 else "K1"
+            stats["w1_src"][src] = stats["w1_src"].get(src, 0) + 1
+            bind(jj + 1, w1[1], jj + 2)
+            touched.add(w1[1])
+            stats["checked"] += 1
+            stats["pairs"] += 1
+            i += 2
+        stats["commits"].append(i)
+        j = s0 + i
+    c = np.array(stats["cand"])
+    print(f"decisions checked exact: {stats['checked']}  pairs {stats['pairs']}  single {stats['single']}  "
+          f"exhausted stops {stats['exhausted']}  commits/batch {np.mean(stats['commits']):.0f}")
+    print(f"pod-i touched candidates: mean {c.mean():.2f}  p90 {np.percentile(c, 90):.0f}  max {c.max()}  "
+          f"(winner from the list {stats['from_list']} of {stats['pairs']})")
+    print(f"pod i+1 needs the second untouched list entry: {stats['need_u2']}")
+    print(f"pod i+1 winner source: {stats['w1_src']}")
+    print(f"K1 evaluations per pair: touched {np.mean(stats['k1_all']):.0f}, passing the float bound vs "
+          f"key(u2) {np.mean(stats['k1_bound']):.2f} (vs key(u1) {np.mean(stats['k1_bound_u1']):.2f})")
+
+
+if __name__ == "__main__":
+    main()
