@@ -197,6 +197,12 @@ def main():
             if w == u[1]:
                 stats["from_list"] += 1
             w1 = max([m2, k2, lcand] + k1c)
+            # atomics-only decision: MC = max K1 over ALL touched candidates (w included) folded
+            # beside best_i; exact unless MC belongs to w and beats the other terms, when the
+            # max over candidates != w needs a second (rare) fold round
+            mc = max([(int(k1[c]), c) for c in cand] + [(0, -1)])
+            if mc[1] == w and mc > max(m2, k2, lcand):
+                stats["second_round"] = stats.get("second_round", 0) + 1
             # ground truth: the sequential walk
             bind(jj, w, jj + 1)
             touched.add(w)
@@ -219,6 +225,7 @@ def main():
           f"(winner from the list {stats['from_list']} of {stats['pairs']})")
     print(f"pod i+1 needs the second untouched list entry: {stats['need_u2']}")
     print(f"pod i+1 winner source: {stats['w1_src']}")
+    print(f"pairs needing the second fold round (atomics-only decision): {stats.get('second_round', 0)}")
     print(f"K1 evaluations per pair: touched {np.mean(stats['k1_all']):.0f}, passing the float bound vs "
           f"key(u2) {np.mean(stats['k1_bound']):.2f} (vs key(u1) {np.mean(stats['k1_bound_u1']):.2f})")
 
