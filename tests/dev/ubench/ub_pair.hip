@@ -48,6 +48,58 @@ __global__ __launch_bounds__(kThreads) void pair(int iters, unsigned long long* 
     out[tid] = acc;
 }
 
+// the atomics-only decision: one 32-byte control read (best_i, the non-candidate
+// maximum M2', MC = max K1 over the candidates, the list candidate's K2), then — for a touched
+// winner — its K2 from a per-entry slot; kFolds waves fold best_i, MC and M2' and store a K2
+struct alignas(16) CtlA { unsigned long long best, m2, mc, k2l; };
+template <int kThreads, int kFolds, bool kPacked = false, bool kLanes = false>
+__global__ __launch_bounds__(kThreads) void pair_atomic(int iters, unsigned long long* out) {
+    __shared__ CtlA ctl[3];
+    __shared__ unsigned long long k2[1024];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    if (tid < 3) ctl[tid] = CtlA{1, 1, 1, 1};
+    k2[tid] = tid;
+    __syncthreads();
+    unsigned long long acc = 0;
+    for (int it = 0; it < iters; ++it) {
+        // both 16-byte halves issued together and pinned (otherwise the compiler reads `best`,
+        // branches on it, and only then reads the rest: two dependent LDS round trips)
+        const uint4* q = reinterpret_cast<const uint4*>(&ctl[it % 3]);
+        const uint4 h0 = q[0], h1 = q[1];
+        asm volatile("" ::"v"(h0.x), "v"(h0.y), "v"(h0.z), "v"(h0.w), "v"(h1.x), "v"(h1.y), "v"(h1.z), "v"(h1.w));
+        CtlA c;
+        __builtin_memcpy(&c, &h0, 16);
+        __builtin_memcpy(reinterpret_cast<char*>(&c) + 16, &h1, 16);
+        if (c.best == 0) break;
+        const int e = (int)(c.best & 1023u);
+        // kPacked: the winner's K2 total rides in best_i's low bits (no dependent read)
+        const unsigned long long kw = kPacked ? (c.best >> 10) & 0xFFFFu : e == 1023 ? c.k2l : k2[e];
+        unsigned long long w1 = c.m2 > kw ? c.m2 : kw;
+        const bool mc_is_w = (c.mc & 1023u) == (c.best & 1023u);
+        if (!mc_is_w) w1 = c.mc > w1 ? c.mc : w1;
+        acc += c.best ^ w1;
+        if (kLanes && wave >= 1 && wave <= kFolds && lane < 3) {
+            // the three folds as ONE ds_max_u64 over lanes 0..2 (three addresses of the slot)
+            const int s = (it + 1) % 3;
+            const unsigned long long ent = (unsigned long long)((acc + wave) & 511u);
+            const unsigned long long v = lane == 0 ? ((acc + wave) << 10) | ent
+                                       : lane == 1 ? ((acc * 3 + wave) << 10) | ent : acc + 7 * wave;
+            unsigned long long* dst = lane == 0 ? &ctl[s].best : lane == 1 ? &ctl[s].mc : &ctl[s].m2;
+            atomicMax(dst, v);
+        } else if (!kLanes && wave >= 1 && wave <= kFolds && lane == 0) {
+            const int s = (it + 1) % 3;
+            const unsigned long long ent = (unsigned long long)((acc + wave) & 511u);
+            atomicMax(&ctl[s].best, ((acc + wave) << 10) | ent);
+            atomicMax(&ctl[s].mc, ((acc * 3 + wave) << 10) | ent);
+            atomicMax(&ctl[s].m2, acc + 7 * wave);
+            k2[ent] = acc * 5 + wave;
+        }
+        if (wave == 0 && lane == 0) ctl[(it + 2) % 3] = CtlA{1, 1, 1, 1};
+        __syncthreads();
+    }
+    out[tid] = acc;
+}
+
 // the one-pod skeleton (as ub_iter.hip) for the side-by-side figure
 struct alignas(16) C1 { unsigned long long best; int kfull; int pad; };
 template <int kThreads, int kFolds>
@@ -91,6 +143,13 @@ int main() {
     run("pair:   16 waves, 1 candidate", pair<1024, 1>, 1024, d, 2);
     run("pair:   16 waves, 3 candidates", pair<1024, 3>, 1024, d, 2);
     run("pair:   16 waves, 8 candidates", pair<1024, 8>, 1024, d, 2);
+    run("pair, atomics only: 16 waves, 1 candidate", pair_atomic<1024, 1>, 1024, d, 2);
+    run("pair, atomics only: 16 waves, 3 candidates", pair_atomic<1024, 3>, 1024, d, 2);
+    run("pair, atomics only: 16 waves, 8 candidates", pair_atomic<1024, 8>, 1024, d, 2);
+    run("pair, K2 packed in best: 16 waves, 1 candidate", pair_atomic<1024, 1, true>, 1024, d, 2);
+    run("pair, K2 packed in best: 16 waves, 3 candidates", pair_atomic<1024, 3, true>, 1024, d, 2);
+    run("pair, packed, folds across lanes: 1 cand", pair_atomic<1024, 1, true, true>, 1024, d, 2);
+    run("pair, packed, folds across lanes: 3 cands", pair_atomic<1024, 3, true, true>, 1024, d, 2);
     run("single: 8 waves, 3 folds", single<512, 3>, 512, d, 1);
     run("pair:   8 waves, 3 candidates", pair<512, 3>, 512, d, 2);
     return 0;
