@@ -4,7 +4,9 @@
 // count) and the candidate array lane-parallel (ikey_i, K1, K2 per candidate), takes pod i's
 // winner and pod i+1's winner (K2 for the entry that won pod i, K1 for the others) with uniform
 // readlane loops, then kFolds waves append one candidate each into the next slot and fold the
-// maximum; one barrier.   hipcc -O3 --offload-arch=gfx950 ub_pair.hip -o ub_pair
+// maximum; one barrier.
+//   hipcc -O3 --offload-arch=gfx950 -mllvm -amdgpu-atomic-optimizer-strategy=None ub_pair.hip -o ub_pair
+// (the engine's flags: the atomic optimizer would turn each LDS atomic into a readlane loop)
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
