@@ -97,7 +97,11 @@ typedef struct {
  * (micro 24-bit / tiny int32 / narrow 32x32->64 / wide 64/128-bit).  FORCE_WIDE keeps the wide
  * one, NO_TINY skips tiny and micro, NO_MICRO skips micro; all are exact, the flags exist to test
  * them against each other. */
-enum { KS_ENGINE_FORCE_WIDE = 1, KS_ENGINE_NO_TINY = 2, KS_ENGINE_NO_MICRO = 4 };
+enum { KS_ENGINE_FORCE_WIDE = 1, KS_ENGINE_NO_TINY = 2, KS_ENGINE_NO_MICRO = 4,
+       /* resolvers: batches of clusters above the small class go to the pair resolver (two
+        * pods per barrier) when every total + 1 < 2^15; ONE_POD_RESOLVER keeps the role-split
+        * one-pod resolver instead (same binds — the flag exists to test them against each other) */
+       KS_ENGINE_ONE_POD_RESOLVER = 8 };
 
 typedef struct {
     int64_t pod;    /* FIFO index (submission order) */

@@ -589,6 +589,11 @@ hipError_t launch_resolve(const EngineArgs* d, int S, int mode, hipStream_t st);
 hipError_t launch_resolve_small(const EngineArgs* d, int S, int mode, hipStream_t st);
 int small_resolver_max_batch();
 int small_resolver_max_nodes();
+// the pair resolver (ks_pair.hip): two pods per barrier, batches of <= pair_resolver_max_batch()
+// pods, any cluster, when every total + 1 < 2^15 (its decision words carry a second total)
+hipError_t launch_resolve_pair(const EngineArgs* d, int S, int mode, hipStream_t st);
+int pair_resolver_max_batch();
+constexpr int64_t kPairTotalCap = 1LL << 15;
 struct BindSeg {
     const int32_t* node;
     const int32_t* status;

@@ -239,8 +239,21 @@ bool small_resolver(const ks_engine* e) {
 // shortest per-pod chain and takes big batches; the register-table resolver (4 waves,
 // ks_resolve.hip) is lighter — four per CU, so a what-if group's resolvers run side by side (C4
 // 2.29e11 against 2.16e11 evals/s with the role-split kernel's half-size class).
-hipError_t launch_resolver(const ks::EngineArgs* d, int S, int mode, bool small, hipStream_t st) {
-    return small ? ks::launch_resolve_small(d, S, mode, st) : ks::launch_resolve(d, S, mode, st);
+// The pair resolver (ks_pair.hip) decides two pods per barrier; its decision words carry a
+// second total, so it takes engines whose totals + 1 stay below 2^15 (weights and constant
+// values are >= 0).
+bool pair_resolver(const ks_engine* e) {
+    return !(e->flags & KS_ENGINE_ONE_POD_RESOLVER) &&
+           (int64_t)e->dc.const_total + 10 * ((int64_t)e->dc.w_lr + e->dc.w_ba) + 1 < ks::kPairTotalCap;
+}
+enum Resolver { kResolveRole = 0, kResolveSmall = 1, kResolvePair = 2 };
+int resolver_of(const ks_engine* e) {
+    return small_resolver(e) ? kResolveSmall : pair_resolver(e) ? kResolvePair : kResolveRole;
+}
+hipError_t launch_resolver(const ks::EngineArgs* d, int S, int mode, int which, hipStream_t st) {
+    return which == kResolveSmall ? ks::launch_resolve_small(d, S, mode, st)
+         : which == kResolvePair ? ks::launch_resolve_pair(d, S, mode, st)
+                                 : ks::launch_resolve(d, S, mode, st);
 }
 void update_mode(ks_engine* e) {
     int64_t m[3];
@@ -276,7 +289,8 @@ ks_status engine_init(const ks_config* cfg, ks_engine** out) {
     if (cfg->filters & ~7u) return KS_EINVAL;
     if (cfg->n_scorers < 0 || cfg->n_scorers > 8) return KS_EINVAL;
     if (cfg->batch_pods < 0 || cfg->batch_pods > kMaxBatch) return KS_EINVAL;
-    if (cfg->engine_flags & ~(uint32_t)(KS_ENGINE_FORCE_WIDE | KS_ENGINE_NO_TINY | KS_ENGINE_NO_MICRO))
+    if (cfg->engine_flags &
+        ~(uint32_t)(KS_ENGINE_FORCE_WIDE | KS_ENGINE_NO_TINY | KS_ENGINE_NO_MICRO | KS_ENGINE_ONE_POD_RESOLVER))
         return KS_EINVAL;
     int64_t const_total = 0, w_lr = 0, w_ba = 0;
     for (int i = 0; i < cfg->n_scorers; i++) {
@@ -820,7 +834,7 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
                 HIPCHK(e, ks::launch_merge(d, 1, e->B, e->cand_all, L, G, BL, e->cand, G, st));
             }
             if (ev[3]) HIPCHK(e, hipEventRecord(ev[3], st));
-            HIPCHK(e, launch_resolver(d, 1, e->mode, small_resolver(e), st));
+            HIPCHK(e, launch_resolver(d, 1, e->mode, resolver_of(e), st));
             if (ev[4]) HIPCHK(e, hipEventRecord(ev[4], st));
             launches++;
         }
@@ -980,12 +994,14 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
     std::vector<int64_t> p_hi(S, 0), t_end(S, 0);
     std::vector<char> live(S, 0), part(S, 0);  // part: takes part in this step
     int mode = ks::kEvalMicro, blk_n = 0, B = 0;  // B: the largest member batch (grid size)
-    bool k16 = true, small = true;
+    bool k16 = true, small = true, pair = true;
     for (ks_engine* e : g->engs) {
         B = std::max(B, e->B);
         k16 = k16 && key16(e);
         small = small && small_resolver(e);
+        pair = pair && pair_resolver(e);
     }
+    const int which = small ? kResolveSmall : pair ? kResolvePair : kResolveRole;
     int64_t blocks = 0;
     for (int i = 0; i < S; i++) {
         ks_engine* e = g->engs[i];
@@ -1058,7 +1074,7 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
                 if (!dev(ks::launch_expire_head(d, Sh, hst[h])) ||
                     !dev(ks::launch_scan(d, Sh, blk_n, B, pg, mode, k16, hst[h])) ||
                     !dev(ks::launch_merge(d, Sh, B, nullptr, 0, 0, 0, nullptr, blk_n, hst[h])) ||
-                    !dev(launch_resolver(d, Sh, mode, small, hst[h])))
+                    !dev(launch_resolver(d, Sh, mode, which, hst[h])))
                     return dev_fail("group step: kernel launch failed");
             }
             launches++;
