@@ -20,11 +20,10 @@ node-sharded across the N ranks (ks_shard: each rank scans its node range, one R
 of the per-pod candidate lists per batch), total work fixed as N grows (strong scaling): the
 north star's scaling target.  Skipped (with the reason) when ranks share a GPU.
 
-roofline: "frac" is the whole path's fraction of the 80-B-per-evaluation model at 8 TB/s
-(SURVEY.md §8(d)): evals/s x 80 B / 8 TB/s; "stream_copy_gbs" is the HBM ceiling measured on the
-box (a 2 GiB device copy) and "frac_of_stream_copy" the same model against it.  The scan
-kernel's measured HBM traffic (PMC, profiles/pmc_scan.json) and the resolver's per-pod latency
-are reported under it.
+roofline (roofline_block): the path is latency-bound (the resolver), so "achieved" / "frac" are
+the MEASURED HBM bandwidth of a batch round (PMC bytes per round, profiles/pmc_<config>.json,
+over its device time by HIP events) against 8 TB/s; the 80-B-per-evaluation model of SURVEY.md
+§8(d) is "model_gbs" / "model_frac"; "stream_copy_gbs" is the HBM ceiling measured on the box.
 """
 from __future__ import annotations
 
@@ -125,16 +124,75 @@ def stream_copy_gbs(device: int, mib: int = 2048, reps: int = 10):
         return None
 
 
-def load_traffic():
-    """Measured HBM bytes per scan launch (2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of
-    MI355X_MICROARCH.md §HBM) from the committed PMC summary, if present."""
-    p = os.path.join(ROOT, "profiles", "pmc_scan.json")
+# the kernels of one batch round (ks_step: expire_head -> scan -> merge -> resolve); every
+# resolver variant counts as "resolve"
+BATCH_KERNELS = {"ks::expire_head_kernel": "expire_head", "ks::scan_kernel": "scan", "ks::merge_kernel": "merge",
+                 "ks::resolve_kernel": "resolve", "ks::pr::resolve_pair_kernel": "resolve",
+                 "ks::resolve_pair_kernel": "resolve"}
+
+
+def load_traffic(config: str = "c3"):
+    """Measured HBM bytes per launch of each batch kernel (2 x FETCH_SIZE + WRITE_SIZE, the gfx950
+    correction of MI355X_MICROARCH.md §HBM) from the committed PMC summary of this workload
+    (profiles/pmc_<config>.json, made by profiles/collect.sh + profiles/db_summary.py)."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
     if not os.path.exists(p):
         return None
     with open(p) as f:
         d = json.load(f)
-    b = d.get("hbm_bytes_per_scan_launch")
-    return {"bytes": b, "source": d.get("source", "profiles/pmc_scan.json")} if b else None
+    per = {}
+    for k, v in d.get("per_kernel", {}).items():
+        role = BATCH_KERNELS.get(k)
+        if role and "FETCH_SIZE_KB_avg" in v and "WRITE_SIZE_KB_avg" in v:
+            per[role] = int((2 * v["FETCH_SIZE_KB_avg"] + v["WRITE_SIZE_KB_avg"]) * 1024)
+    if "scan" not in per:
+        return None
+    return {"per_kernel": per, "per_batch": sum(per.values()), "source": d.get("source", p),
+            "file": os.path.relpath(p, ROOT)}
+
+
+def roofline_block(value, st, nodes, config, stream_gbs=None):
+    """The roofline object: the path is bound by the resolver's latency (one
+    workgroup walks each batch in FIFO order), so "achieved" is the MEASURED HBM bandwidth of the
+    whole batch chain — PMC bytes per batch round over its device time (HIP events on the
+    engine's stream) — against the 8 TB/s peak; the 80-B-per-evaluation model of SURVEY.md §8(d)
+    is reported beside it as model_gbs / model_frac."""
+    launches = max(st["launches"], 1)
+    pods_per_launch = st["pods"] / launches
+    dev_ms = (st["scan_ms"] + st["resolve_ms"] + st["other_ms"]) / launches
+    scan_ms, res_ms = st["scan_ms"] / launches, st["resolve_ms"] / launches
+    tr = load_traffic(config)
+    model_gbs = value * BYTES_PER_EVAL / 1e9
+    achieved = tr["per_batch"] / (dev_ms * 1e-3) / 1e9 if tr and dev_ms > 0 else None
+    res_ns_pod = st["resolve_ms"] * 1e6 / max(st["pods"], 1)
+    per = tr["per_kernel"] if tr else {}
+    return {
+        "bound": "latency (resolve kernel: one workgroup per batch walks its pods in FIFO order)",
+        "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS if achieved is not None else None,
+        "traffic": tr["per_batch"] if tr else None,
+        "traffic_note": "HBM bytes per batch round (expire_head + scan + merge + resolve), PMC "
+                        "2 x FETCH_SIZE + WRITE_SIZE" + (f" from {tr['file']}" if tr else " (no PMC summary)"),
+        "batch_device_ms": dev_ms, "pods_per_batch": pods_per_launch,
+        "model_gbs": model_gbs, "model_frac": model_gbs / HBM_PEAK_GBS,
+        "model": "80 B per (pod, node) evaluation (SURVEY.md 8(d)) x evals/s; node records are reused "
+                 "across a scan workgroup's pods, so the model exceeds the measured traffic",
+        "stream_copy_gbs": stream_gbs,
+        "model_frac_of_stream_copy": model_gbs / stream_gbs if stream_gbs else None,
+        "kernels": {
+            "scan": {"ms": scan_ms, "hbm_bytes": per.get("scan"),
+                     "gbs": per["scan"] / (scan_ms * 1e-3) / 1e9 if per.get("scan") and scan_ms > 0 else None,
+                     "model_bytes": BYTES_PER_EVAL * pods_per_launch * nodes,
+                     "bound": "VALU issue: fused Filter+Score evaluations + top-L extraction per 256-node "
+                              "block (SQ counters in profiles/)"},
+            "resolve": {"ms": res_ms, "hbm_bytes": per.get("resolve"), "ns_per_pod": res_ns_pod,
+                        "cycles_per_pod_at_2_4ghz": res_ns_pod * 2.4,
+                        "share_of_device_time": res_ms / dev_ms if dev_ms > 0 else None,
+                        "bound": "latency: dependent per-pair decision chain in one workgroup"},
+            "merge_and_expire_head": {"ms": st["other_ms"] / launches,
+                                      "hbm_bytes": (per.get("merge") or 0) + (per.get("expire_head") or 0) or None},
+        },
+    }
 
 
 def main():
@@ -239,10 +297,10 @@ def main():
     eng.usage_at(t_now)
     t_u = time.perf_counter()
     for k in range(10):
-        eng.usage_at(t_now - 1000 * k)
+        eng.usage_at(max(0, t_now - 1000 * k))
     usage_ms = (time.perf_counter() - t_u) * 100.0
     t_u = time.perf_counter()
-    eng.usage_digest(t_now - S + 1, t_now + 1)
+    eng.usage_digest(max(0, t_now - S + 1), t_now + 1)
     digest_ms = (time.perf_counter() - t_u) * 1e3
     eng.close()
     line = None
@@ -257,12 +315,6 @@ def main():
         scan_avg_ms = st["scan_ms"] / launches
         res_avg_ms = st["resolve_ms"] / launches
         other_avg_ms = st["other_ms"] / launches
-        # the whole path against the 80-B model: evals/s x 80 B
-        achieved = value * BYTES_PER_EVAL / 1e9
-        traffic = load_traffic()
-        scan_s = scan_avg_ms * 1e-3
-        scan_model = BYTES_PER_EVAL * pods_per_launch * nodes
-        res_ns_pod = st["resolve_ms"] * 1e6 / max(st["pods"], 1)
         cpu = None
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N=1 figure
             cpu = cpu_baseline(trace, scorers, args.cpu_sample_pods, args.cpu_budget_s)
@@ -285,29 +337,7 @@ def main():
                        "parallelism": "replicas" if world > 1 else "single-gpu",
                        "batch_pods": args.batch or 256},
             "pods_per_s": pods_per_s,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS,
-                         "stream_copy_gbs": (sc := stream_copy_gbs(local)),
-                         "frac_of_stream_copy": achieved / sc if sc else None,
-                         "traffic": traffic["bytes"] if traffic else None,
-                         "kernel": "whole path per batch (expire_head + scan + merge + resolve)",
-                         "model": "80 B per (pod, node) evaluation (SURVEY.md 8(d)) x evals/s over the timed "
-                                  "region; traffic = measured HBM bytes per scan launch (PMC)",
-                         "scan": {"ms_per_launch": scan_avg_ms, "pods_per_launch": pods_per_launch,
-                                  "model_bytes_per_launch": scan_model,
-                                  "measured_bytes_per_launch": traffic["bytes"] if traffic else None,
-                                  "measured_gbs": traffic["bytes"] / scan_s / 1e9 if traffic and scan_s > 0 else None,
-                                  "measured_frac": traffic["bytes"] / scan_s / 1e9 / HBM_PEAK_GBS
-                                  if traffic and scan_s > 0 else None,
-                                  "node_record_reuse": scan_model / traffic["bytes"] if traffic else None,
-                                  "traffic_source": traffic["source"] if traffic else None,
-                                  "bound": "VALU issue: fused Filter+Score evaluations + top-L extraction per "
-                                           "256-node block (SQ counters in profiles/)"},
-                         "resolve": {"ns_per_pod": res_ns_pod, "cycles_per_pod_at_2_4ghz": res_ns_pod * 2.4,
-                                     "share_of_device_time": st["resolve_ms"] / max(st["scan_ms"] + st["resolve_ms"]
-                                                                                   + st["other_ms"], 1e-9),
-                                     "bound": "latency: one workgroup per batch walks its pods in FIFO order "
-                                              "(DESIGN.md 4); no HBM or MFMA roofline applies"}},
+            "roofline": roofline_block(value, st, nodes, "c3", stream_copy_gbs(local)),
             "kernels": {"launches_per_step": launches, "pods_per_launch": pods_per_launch,
                         "scan_avg_ms": scan_avg_ms, "resolve_avg_ms": res_avg_ms,
                         "other_avg_ms": other_avg_ms,
@@ -324,8 +354,9 @@ def main():
         c5 = c5_leg(args, rank, world, local, dist, line=line)
         if rank == 0:
             line["c5_sharded"] = c5
-    if rank == 0:
-        print(json.dumps(line), flush=True)
+    if rank == 0 and not line.get("_printed"):
+        line["_printed"] = True
+        print(json.dumps({k: v for k, v in line.items() if k != "_printed"}), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
@@ -416,22 +447,38 @@ def main_c4(args):
 
 def c5_leg(args, rank, world, local, dist, steps=None, warmup=1, line=None):
     """The C5 leg, never fatal to the bench line: an error on this rank is reported in rank 0's
-    line (a rank left waiting in a collective is ended by the leg's watchdog)."""
+    line.  A leg that hangs (e.g. a rank left waiting in an RCCL rendezvous) is ended by a
+    watchdog after --c5-timeout s: rank 0 prints the C3 line with the leg marked abandoned (once)
+    and every rank exits with status 3, so torchrun and the driver see the failure."""
+    import threading
+    timer = None
+    if args.c5_timeout > 0:
+        def _abandon():
+            if rank == 0 and line is not None and not line.get("_printed"):
+                line["c5_sharded"] = {"error": f"abandoned after {args.c5_timeout:.0f} s"}
+                line["_printed"] = True
+                print(json.dumps({k: v for k, v in line.items() if k != "_printed"}), flush=True)
+            os._exit(3)
+        timer = threading.Timer(args.c5_timeout, _abandon)
+        timer.daemon = True
+        timer.start()
     try:
-        return _c5_leg_body(args, rank, world, local, dist, steps, warmup, line)
+        return _c5_leg_body(args, rank, world, local, dist, steps, warmup)
     except Exception as ex:  # e.g. an RCCL or HIP failure of a multi-rank run
         log(f"[rank {rank}] C5 leg failed: {ex!r}")
         return {"error": repr(ex)[:500]} if rank == 0 else None
+    finally:
+        if timer is not None:
+            timer.cancel()
 
 
-def _c5_leg_body(args, rank, world, local, dist, steps=None, warmup=1, line=None):
+def _c5_leg_body(args, rank, world, local, dist, steps=None, warmup=1):
     """BASELINE.json configs[4]: one 1M-node cluster (tracegen C5, seed 0x5EED0005) node-sharded
     across the ranks — rank r scans its contiguous node range, the per-pod top-L candidate lists
     are all-gathered over RCCL once per batch, every rank resolves the same binds (ks_shard).
     Total work is fixed as N grows: strong scaling.  At N=1 the engine is unsharded unless
     --vshards > 1 (virtual shards on one GPU, the exchange without RCCL).  Returns rank 0's
     result dict (None on other ranks); a leg that cannot run says why."""
-    import threading
     steps = args.c5_steps if steps is None else steps
     if world > 1:
         try:
@@ -441,19 +488,6 @@ def _c5_leg_body(args, rank, world, local, dist, steps=None, warmup=1, line=None
             n_dev = 0
         if n_dev < world and not os.environ.get("KS_BENCH_SHARED_GPU"):  # rehearsal override
             return {"skipped": f"{world} ranks share {n_dev} GPU(s): RCCL needs one GPU per rank"}
-    box = {"line": line} if line is not None else {}
-    timer = None
-    if args.c5_timeout > 0:
-        def _abandon():
-            # the C5 leg hung (e.g. an RCCL rendezvous): the C3 line must still come out
-            box["timeout"] = True
-            if rank == 0 and "line" in box:
-                box["line"]["c5_sharded"] = {"error": f"abandoned after {args.c5_timeout:.0f} s"}
-                print(json.dumps(box["line"]), flush=True)
-            os._exit(0)  # rank 0 printed the line with the error; the others have no output
-        timer = threading.Timer(args.c5_timeout, _abandon)
-        timer.daemon = True
-        timer.start()
     from kubesim_amd import encode, tracegen
     from kubesim_amd.engine import Engine, comm_unique_id
     need = (steps + warmup + 1) * args.pods_per_step
@@ -506,8 +540,6 @@ def _c5_leg_body(args, rank, world, local, dist, steps=None, warmup=1, line=None
     st = eng.last_step_stats()
     eng.set_profiling(False)
     eng.close()
-    if timer is not None:
-        timer.cancel()
     if rank != 0:
         return None
     nodes = args.c5_nodes
@@ -526,6 +558,7 @@ def _c5_leg_body(args, rank, world, local, dist, steps=None, warmup=1, line=None
         "kernels": {"launches_per_step": launches, "pods_per_launch": st["pods"] / launches,
                     "scan_avg_ms": st["scan_ms"] / launches, "resolve_avg_ms": st["resolve_ms"] / launches,
                     "other_avg_ms": st["other_ms"] / launches, "profiled_step_ms": st["step_ms"]},
+        "roofline": roofline_block(binds * nodes / t_el, st, nodes, "c5"),
     }
 
 

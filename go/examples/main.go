@@ -55,6 +55,9 @@ func (s *everyFive) Submit(c clock.Clock, _ []*v1.Node) ([]*v1.Pod, error) {
 	return []*v1.Pod{p}, nil
 }
 
+// PlacementBlind: Submit reads only the clock (engine.RunWindowed may call it ahead).
+func (s *everyFive) PlacementBlind() bool { return true }
+
 func readConfig(path string) (*config.Config, error) {
 	viper.SetConfigName(path)
 	viper.AddConfigPath(".")
@@ -84,7 +87,9 @@ func main() {
 		<-sig
 		cancel()
 	}()
-	if err := k.Run(ctx); err != nil && errors.Cause(err) != context.Canceled {
+	defer k.Close()
+	// the submitter never reads placements: 1,024 ticks per device step, same binds as Run
+	if err := k.RunWindowed(ctx, 1024); err != nil && errors.Cause(err) != context.Canceled {
 		log.L.Fatal(err)
 	}
 }

@@ -29,7 +29,12 @@ import (
 var ErrOutOfDomain = errors.New("outside the engine's exact domain")
 
 // Engine is one simulated cluster on one device (a handle is single-threaded, like Run).
-type Engine struct{ h *C.ks_engine }
+// n is the node count of LoadNodes: every per-node output buffer is sized from it, never from a
+// caller's argument (the C side always writes n rows).
+type Engine struct {
+	h *C.ks_engine
+	n int
+}
 
 func status(e *Engine, rc C.ks_status) error {
 	msg := ""
@@ -133,8 +138,12 @@ func (e *Engine) LoadNodes(alloc []int64, taint, label []uint64) error {
 	if n == 0 {
 		return status(e, C.ks_load_nodes(e.h, 0, nil, nil, nil))
 	}
-	return status(e, C.ks_load_nodes(e.h, C.int64_t(n), (*C.int64_t)(unsafe.Pointer(&alloc[0])),
+	err := status(e, C.ks_load_nodes(e.h, C.int64_t(n), (*C.int64_t)(unsafe.Pointer(&alloc[0])),
 		(*C.uint64_t)(unsafe.Pointer(&taint[0])), (*C.uint64_t)(unsafe.Pointer(&label[0]))))
+	if err == nil {
+		e.n = n
+	}
+	return err
 }
 
 // Pods is a batch of encoded pods in FIFO order (EncodePods builds it from []*v1.Pod).
@@ -230,23 +239,29 @@ func (e *Engine) Step(ticks int64) ([]Bind, error) {
 	return binds, status(e, rc)
 }
 
-// FilterMask is api.Filter over every node for queued pod `pod` (ks_filter).
-func (e *Engine) FilterMask(pod int64, nodes int) ([]uint8, error) {
-	mask := make([]uint8, nodes+1)
-	return mask[:nodes], status(e, C.ks_filter(e.h, C.int64_t(pod), u8p(mask)))
+// FilterMask is api.Filter over every node for queued pod `pod` (ks_filter): one byte per
+// loaded node.
+func (e *Engine) FilterMask(pod int64) ([]uint8, error) {
+	mask := make([]uint8, e.n+1)
+	return mask[:e.n], status(e, C.ks_filter(e.h, C.int64_t(pod), u8p(mask)))
 }
 
-// Scores is the aggregated score of every node for queued pod `pod` (-1 = no entry, ks_score).
-func (e *Engine) Scores(pod int64, nodes int) ([]int64, error) {
-	s := make([]int64, nodes+1)
-	return s[:nodes], status(e, C.ks_score(e.h, C.int64_t(pod), i64p(s)))
+// Scores is the aggregated score of every loaded node for queued pod `pod` (-1 = no entry,
+// ks_score).
+func (e *Engine) Scores(pod int64) ([]int64, error) {
+	s := make([]int64, e.n+1)
+	return s[:e.n], status(e, C.ks_score(e.h, C.int64_t(pod), i64p(s)))
 }
 
-// UsageAt is Σ Pod.ResourceUsage per node at tick t <= Tick() (n*3: cpu, memory, gpu milli).
-func (e *Engine) UsageAt(t int64, nodes int) ([]int64, error) {
-	u := make([]int64, 3*nodes+1)
-	return u[:3*nodes], status(e, C.ks_usage_at(e.h, C.int64_t(t), i64p(u)))
+// UsageAt is Σ Pod.ResourceUsage per node at tick t <= Tick() (3 per loaded node: cpu, memory,
+// gpu milli).
+func (e *Engine) UsageAt(t int64) ([]int64, error) {
+	u := make([]int64, 3*e.n+1)
+	return u[:3*e.n], status(e, C.ks_usage_at(e.h, C.int64_t(t), i64p(u)))
 }
+
+// Nodes is the node count of LoadNodes.
+func (e *Engine) Nodes() int { return e.n }
 
 // PodLookup is Node.GetPod by key (kubesim/node/node.go:62-75): the FIFO index stored there.
 func (e *Engine) PodLookup(node int32, key int64) (int64, error) {

@@ -138,11 +138,12 @@ func (k *KubeSim) start() error {
 // Run executes the main loop (kubesim/kubesim.go:90-123): every tick the submitters are called
 // in registration order, their pods are appended FIFO, and one queued pod is scheduled on the
 // device; any plugin or CreatePod error ends the run with that error.
+// The engine stays alive after Run returns (queries through Engine(), a later Run continues
+// the same simulation); Close releases it.
 func (k *KubeSim) Run(ctx context.Context) error {
 	if err := k.start(); err != nil {
 		return err
 	}
-	defer k.eng.Close()
 	k.startClk = clock.NewClock(time.Now())
 	nodes := k.nodes
 	for {
@@ -159,6 +160,64 @@ func (k *KubeSim) Run(ctx context.Context) error {
 		if err := k.step(1); err != nil {
 			return err
 		}
+	}
+}
+
+// PlacementBlind is implemented by an api.Submitter whose Submit never reads placement state —
+// which pods are bound where, or usage — from its arguments (it may read the clock and the node
+// list's static fields).  The reference example's submitter is one (examples/main.go:96-128).
+type PlacementBlind interface {
+	PlacementBlind() bool
+}
+
+// RunWindowed is Run for placement-blind submitters: each round calls the submitters for the
+// next `window` ticks (clock and arrival tick exactly as Run would give them), then advances
+// the device once over the whole window (one ks_step instead of `window`).  Binds, bind ticks
+// and errors are identical to Run's — a pod's placement depends only on the pods submitted
+// before it, and every submit happens before the step that binds it; a submitter error at tick t
+// is returned after ticks < t are scheduled, as Run returns it.  ctx is checked once per window.
+// Every registered submitter must implement PlacementBlind (else an error, nothing run).
+func (k *KubeSim) RunWindowed(ctx context.Context, window int64) error {
+	if window <= 1 {
+		return k.Run(ctx)
+	}
+	for _, s := range k.submitters {
+		if b, ok := s.(PlacementBlind); !ok || !b.PlacementBlind() {
+			return errors.New("RunWindowed: every submitter must implement PlacementBlind")
+		}
+	}
+	if err := k.start(); err != nil {
+		return err
+	}
+	k.startClk = clock.NewClock(time.Now())
+	nodes := k.nodes
+	for {
+		select {
+		case <-ctx.Done():
+			return ctx.Err()
+		default:
+		}
+		for i := int64(0); i < window; i++ {
+			k.tick++
+			clk := k.startClk.Add(time.Duration(int64(k.conf.Tick)*k.tick) * time.Second)
+			if err := k.submit(clk, nodes); err != nil {
+				if e2 := k.step(k.tick - 1 - k.eng.Tick()); e2 != nil {
+					return e2
+				}
+				return err
+			}
+		}
+		if err := k.step(k.tick - k.eng.Tick()); err != nil {
+			return err
+		}
+	}
+}
+
+// Close releases the device engine (Run and RunWindowed leave it open for queries).
+func (k *KubeSim) Close() {
+	if k.eng != nil {
+		k.eng.Close()
+		k.eng = nil
 	}
 }
 

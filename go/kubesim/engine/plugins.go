@@ -88,7 +88,7 @@ func (d *Device) Filter(pod *v1.Pod, node *v1.Node) (bool, error) {
 	if !ok {
 		return false, errors.Errorf("node %q unknown to the engine", node.Name)
 	}
-	mask, err := d.k.eng.FilterMask(q, len(d.k.nodes))
+	mask, err := d.k.eng.FilterMask(q)
 	if err != nil {
 		return false, err
 	}
@@ -102,7 +102,7 @@ func (d *Device) Score(pod *v1.Pod, nodes []*v1.Node) (sched.HostPriorityList, i
 	if err != nil {
 		return nil, 0, err
 	}
-	all, err := d.k.eng.Scores(q, len(d.k.nodes))
+	all, err := d.k.eng.Scores(q)
 	if err != nil {
 		return nil, 0, err
 	}

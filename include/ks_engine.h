@@ -165,7 +165,8 @@ ks_status ks_load_nodes(ks_engine* eng, int64_t n, const int64_t* alloc, const u
  * dictionary labels required (bit 63 = impossible); simSpec as CSR: phase_off[m+1],
  * phase_sec[Φ] (int32), phase_use[Φ][3]; flags = KS_PODFLAG_* (may be NULL).
  *
- * key_id[m] (may be NULL: every pod its own key, key id = FIFO index): the caller's interned
+ * key_id[m] (>= 0; may be NULL: every pod its own key, key id = -(FIFO index) - 1, a namespace
+ * no explicit key shares): the caller's interned
  * "namespace-name" pod key (kubesim/node/node.go:146-160).  Node.CreatePod stores the pod under
  * its key, replacing a same-key pod already stored on that node (node.go:58,
  * kubesim/pod/podmap.go:27-29); a replaced pod that is still running stops counting toward the
@@ -180,7 +181,12 @@ ks_status ks_submit_pods(ks_engine* eng, int64_t m, const int64_t* arrival_tick,
                          const int64_t* phase_use, const uint8_t* flags, const int64_t* key_id);
 
 /* Advance `ticks` ticks.  Writes up to `cap` binds to out (one per tick that had a queued
- * pod) and the number of binds made to *n_out. */
+ * pod) and the number of binds made to *n_out.
+ *
+ * Domain: Pod.passedSeconds is int32(seconds since the pod's start) (kubesim/pod/pod.go:148-153);
+ * past 2^31 s Go's conversion is implementation-defined and IsRunning (pod.go:67-69) may revive
+ * finished pods.  A step that would take the clock 2^31 s or more past the run's first bind, and
+ * a ks_submit_pods whose pods would bind there, are refused with KS_ERANGE (nothing changes). */
 ks_status ks_step(ks_engine* eng, int64_t ticks, ks_bind* out, int64_t cap, int64_t* n_out);
 
 /* Filter mask (all enabled filters) / aggregated score (-1 = no entry) of queued pod `pod`

@@ -185,6 +185,14 @@ namespace {
 
 void engine_free(ks_engine* e);  // ks_destroy's body; a group frees its members with it
 
+// Pod.passedSeconds is int32(clock.Sub(start).Seconds()) (kubesim/pod/pod.go:148-153): past 2^31
+// seconds Go's float -> int32 conversion is implementation-defined (amd64: INT32_MIN, so
+// IsRunning, pod.go:67-69, would revive every finished pod).  The engine's domain: every tick at
+// which a bound pod is evaluated stays below 2^31 seconds after the run's first bind; steps,
+// submits and usage queries past it are refused with KS_ERANGE (the oracle refuses the same).
+bool in_passed_domain(const ks_engine* e, int64_t first_bind, int64_t t) {
+    return t - first_bind <= (int64_t)INT32_MAX / e->cfg.tick_seconds;
+}
 ks_status fail(ks_engine* e, ks_status code, const char* fmt, ...) {
     char buf[512];
     va_list ap;
@@ -542,12 +550,27 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
         if (arrival[i] < last) return fail(e, KS_EINVAL, "arrival ticks must be non-decreasing (pod %lld)", (long long)(e->P + i));
         last = arrival[i];
         if (phase_off[i + 1] < phase_off[i]) return fail(e, KS_EINVAL, "phase_off must be non-decreasing");
+        if (key_id && key_id[i] < 0) return fail(e, KS_EINVAL, "pod %lld: key ids must be >= 0", (long long)(e->P + i));
         for (int k = 0; k < 3; k++)
             if (req[i * 3 + k] < 0 || req[i * 3 + k] >= kMaxValue)
                 return fail(e, KS_EINVAL, "pod %lld: request out of range", (long long)(e->P + i));
     }
     for (int64_t f = 0; f < nf * 3; f++)
         if (phase_use[f] < 0 || phase_use[f] >= kMaxValue) return fail(e, KS_EINVAL, "usage out of range");
+    // the int32 passed-seconds domain (kubesim/pod/pod.go:148-153): every bind tick must stay
+    // within 2^31 seconds of the run's first bind
+    {
+        int64_t pb = e->P ? e->h_bind_tick[e->P - 1] : e->tick;
+        const int64_t first = e->P ? e->h_bind_tick[0] : std::max<int64_t>(pb + 1, std::max<int64_t>(arrival[0], e->tick + 1));
+        for (int64_t i = 0; i < m; i++) {
+            pb = std::max<int64_t>(pb + 1, std::max<int64_t>(arrival[i], e->tick + 1));
+            if (!in_passed_domain(e, first, pb))
+                return fail(e, KS_ERANGE, "pod %lld: bind tick %lld is %lld ticks after the first bind (tick %lld): "
+                            "(t - t0) * %d s reaches 2^31 and Go's int32(passed seconds) leaves its domain",
+                            (long long)(e->P + i), (long long)pb, (long long)(pb - first), (long long)first,
+                            e->cfg.tick_seconds);
+        }
+    }
     // Pod keys: a Store over a same-key pod that is still running on the chosen node would drop
     // that pod from the node's totals (kubesim/node/node.go:58).  Refuse the one case where that
     // can happen — an earlier pod with the key may still run at this pod's bind tick — so every
@@ -683,7 +706,9 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
     e->h_dur.insert(e->h_dur.end(), dur.begin(), dur.end());
     e->h_total_sec.insert(e->h_total_sec.end(), tsec.begin(), tsec.end());
     e->h_exp_off.insert(e->h_exp_off.end(), eoff.begin(), eoff.end());
-    for (int64_t i = 0; i < m; i++) e->h_key.push_back(key_id ? key_id[i] : e->P + i);
+    // default keys (key_id NULL) live in their own namespace: pod j is key -(j + 1), explicit
+    // keys are >= 0, so a mix of both on one engine never aliases
+    for (int64_t i = 0; i < m; i++) e->h_key.push_back(key_id ? key_id[i] : -(e->P + i) - 1);
     for (const auto& kv : new_end) e->key_end[kv.first] = kv.second;
     e->h_node.resize(e->P + m, -1);
     e->h_status.resize(e->P + m, -1);
@@ -777,6 +802,9 @@ ks_status ks_step(ks_engine* e, int64_t ticks, ks_bind* out, int64_t cap, int64_
     *n_out = 0;
     if (e->err) return (ks_status)e->err;
     if (!e->nodes_loaded) return fail(e, KS_EINVAL, "no nodes loaded");
+    if (e->P > 0 && !in_passed_domain(e, e->h_bind_tick[0], e->tick + ticks))
+        return fail(e, KS_ERANGE, "step to tick %lld: more than 2^31 s after the first bind (tick %lld)",
+                    (long long)(e->tick + ticks), (long long)e->h_bind_tick[0]);
     return device_stop(e, step_body(e, ticks, out, cap, n_out));
 }
 
@@ -1007,9 +1035,13 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
         ks_engine* e = g->engs[i];
         n_out[i] = 0;
         status_out[i] = KS_OK;
-        if (e->err || !e->nodes_loaded || e->world * e->vsh != 1) {
-            status_out[i] = e->err ? e->err : KS_EINVAL;
-            if (!e->err) fail(e, KS_EINVAL, "group step needs loaded, unsharded nodes");
+        const bool out_of_domain = e->P > 0 && !in_passed_domain(e, e->h_bind_tick[0], e->tick + ticks);
+        if (e->err || !e->nodes_loaded || e->world * e->vsh != 1 || out_of_domain) {
+            status_out[i] = e->err ? e->err : out_of_domain ? KS_ERANGE : KS_EINVAL;
+            if (!e->err) {
+                if (out_of_domain) fail(e, KS_ERANGE, "step past 2^31 s after the first bind");
+                else fail(e, KS_EINVAL, "group step needs loaded, unsharded nodes");
+            }
             e->h_ctr[0] = e->h_ctr[1] = e->done;
             e->h_ctr[2] = 0;
             *e->h_args = e->nodes_loaded ? make_args(e) : ks::EngineArgs{};

@@ -289,7 +289,8 @@ class Group:
         ``binds`` is one structured array (pod, node, status, tick) holding member i's binds at
         rows [i * cap, i * cap + counts[i]) — :meth:`split` cuts it per member."""
         S = len(self.members)
-        cap = ticks if cap is None else cap
+        if cap is None:  # at most one bind per tick and per queued pod of the longest queue
+            cap = max(0, min(ticks, max((e.queued for e in self.members), default=0)))
         if getattr(self, "_out_n", -1) < S * cap:  # reused across steps (no per-step 10s of MB)
             self._out = (KsBind * max(S * cap, 1))()
             self._out_n = S * cap

@@ -73,6 +73,7 @@ struct ko_sim {
     int32_t* p_total; /* int32 (wrapping) sum of phase seconds, pod.go:155-162 */
 
     int64_t tick, qhead, arrived;
+    int64_t first_bind; /* tick of the run's first bind, -1 before */
     int err;
     char errmsg[256];
     /* scratch */
@@ -102,6 +103,7 @@ ko_sim* ko_create(const ko_config* cfg, int64_t n, const int64_t* alloc, const u
     s->cfg = *cfg;
     s->n = n;
     s->threads = 1;
+    s->first_bind = -1;
     s->alloc = (int64_t*)dupmem(alloc, sizeof(int64_t) * 4 * (size_t)n);
     s->alloc_has = (uint8_t*)dupmem(alloc_has, (size_t)n);
     s->taint_off = (int32_t*)dupmem(taint_off, sizeof(int32_t) * (size_t)(n + 1));
@@ -200,7 +202,10 @@ int ko_submit(ko_sim* s, int64_t m, const int64_t* arrival, const int64_t* req,
     return KO_OK;
 }
 
-/* passedSeconds (pod.go:148-153): int32 of whole seconds since the pod's start clock. */
+/* passedSeconds (pod.go:148-153): int32 of whole seconds since the pod's start clock.  Go's
+ * float64 -> int32 conversion is implementation-defined past 2^31, so the oracle (like the
+ * engine) stays inside the domain: ko_step never evaluates a tick 2^31 s or more after the first
+ * bind (KO_ERANGE).  There secs < 2^31 and the conversion is exact. */
 static int32_t passed_seconds(const ko_sim* s, int64_t p, int64_t t) {
     if (s->p_status[p] != KO_STATUS_OK) return 0;
     int64_t secs = (t - s->p_t0[p]) * (int64_t)s->cfg.tick_seconds;
@@ -224,7 +229,8 @@ static void node_views(ko_sim* s, int64_t t) {
         for (int32_t i = 0; i < L->n; i++) {
             int32_t p = L->v[i];
             if (!is_running(s, p, t)) {
-                /* terminated (Ok and passed >= total) — can never run again: prune */
+                /* terminated (Ok and passed >= total): inside the domain passed only grows with
+                 * t (no int32 wrap, see passed_seconds), so it can never run again — prune */
                 continue;
             }
             L->v[w++] = p;
@@ -435,6 +441,7 @@ static int schedule_one(ko_sim* s, int64_t p, int64_t t, int64_t* out_node, int3
     s->p_node[p] = (int32_t)bn;
     s->p_status[p] = status;
     s->p_t0[p] = t;
+    if (s->first_bind < 0) s->first_bind = t;
     if (status == KO_STATUS_OK) ivec_push(L, (int32_t)p);
     *out_node = bn;
     *out_status = status;
@@ -447,6 +454,10 @@ int ko_step(ko_sim* s, int64_t ticks, int64_t* out_pod, int32_t* out_node, int64
     if (s->err) return s->err;
     for (int64_t i = 0; i < ticks; i++) {
         int64_t t = s->tick + 1;
+        if (s->first_bind >= 0 && t - s->first_bind > (int64_t)INT32_MAX / s->cfg.tick_seconds) {
+            snprintf(s->errmsg, sizeof s->errmsg, "tick %lld: 2^31 s after the first bind", (long long)t);
+            return KO_ERANGE;
+        }
         while (s->arrived < s->m && s->arrival[s->arrived] <= t) s->arrived++;
         if (s->qhead < s->arrived) {
             int64_t p = s->qhead;

@@ -26,7 +26,9 @@
 extern "C" {
 #endif
 
-enum { KO_OK = 0, KO_EINVAL = 1, KO_ENOTFOUND = 2 };
+/* KO_ERANGE (= KS_ERANGE): a tick 2^31 s or more after the first bind — outside the int32
+ * passed-seconds domain (kubesim/pod/pod.go:148-153); the step stops before it, not sticky. */
+enum { KO_OK = 0, KO_EINVAL = 1, KO_ENOTFOUND = 2, KO_ERANGE = 5 };
 enum { KO_FILTER_REFERENCE_LITERAL = 0, KO_FILTER_FEEDS_SCORE = 1 };
 enum { KO_FILTER_FIT = 1, KO_FILTER_TAINT = 2, KO_FILTER_SELECTOR = 4 };
 enum { KO_SCORER_CONST = 0, KO_SCORER_LEAST_REQUESTED = 1, KO_SCORER_BALANCED = 2 };

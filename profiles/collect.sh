@@ -1,7 +1,7 @@
 #!/bin/bash
 # Profile recipe for the committed summaries (run on the GPU box from the repo root):
 #   bash profiles/collect.sh OUTDIR
-# 1. rocprofv3 kernel trace + stats of the C3 bench (short) and of the C4 bench;
+# 1. rocprofv3 kernel trace + stats of the C3 bench (short), the C4 bench and the C5 bench;
 # 2. the PMC passes (one counter group per run): FETCH_SIZE, WRITE_SIZE, and the SQ instruction /
 #    wave-cycle counters; 3. CSV / JSON summaries of the result databases (profiles/db_summary.py).
 # Every step has its own time limit and the chain stops at the first failure.
@@ -18,10 +18,17 @@ timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$DB/c4" -o run -- python3
 timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE -d "$DB/fetch" -o run -- python3 $B --steps 2 > /dev/null
 timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE -d "$DB/write" -o run -- python3 $B --steps 2 > /dev/null
 timeout -k 10 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$DB/sq" -o run -- python3 $B --steps 2 > /dev/null
+C5="$ROOT/bench.py --config c5 --steps 2 --warmup 1"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$DB/c5" -o run -- python3 $C5 > "$ROOT/$OUT/c5_bench.json"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$DB/c5fetch" -o run -- python3 $C5 > /dev/null
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$DB/c5write" -o run -- python3 $C5 > /dev/null
 cd "$ROOT"
+python3 profiles/db_summary.py stats "$DB/c5/run_results.db" "$OUT/c5_kernel_stats.csv"
+python3 profiles/db_summary.py pmc "$DB/c5fetch/run_results.db" "$DB/c5write/run_results.db" "" \
+    "$OUT/pmc_c5.json" "rocprofv3 --pmc passes over bench.py --config c5 --steps 2 --warmup 1 (C5, 1M nodes), MI355X"
 python3 profiles/db_summary.py stats "$DB/c3/run_results.db" "$OUT/c3_kernel_stats.csv"
 python3 profiles/db_summary.py stats "$DB/c4/run_results.db" "$OUT/c4_kernel_stats.csv"
 python3 profiles/db_summary.py pmc "$DB/fetch/run_results.db" "$DB/write/run_results.db" "$DB/sq/run_results.db" \
-    "$OUT/pmc_summary.json" "rocprofv3 --pmc passes over bench.py --steps 2 --warmup 1 (C3), MI355X"
+    "$OUT/pmc_c3.json" "rocprofv3 --pmc passes over bench.py --steps 2 --warmup 1 (C3), MI355X"
 rm -rf "$DB"
 echo "profiles collected in $OUT"

@@ -1,0 +1,95 @@
+"""The drop-in's own call sequence on the device.
+
+go/kubesim/engine/kubesim.go's Run issues, per tick, the submitters' pods to ks_submit_pods with
+arrival = the tick and then ks_step(1) (kubesim/kubesim.go:90-123 restated); RunWindowed calls
+placement-blind submitters `window` ticks ahead and steps once.  kubesim_amd.kubesim.KubeSim is
+that loop call for call (no Go toolchain here or on the box), and this file checks both forms
+bind-for-bind against the reference's KAT and the oracle, with ks_filter / ks_score probed on
+the queue head every tick as the api.Filter / api.Scorer adapters would.  The rates are printed
+(bench.py reports them in its line under "dropin").
+"""
+import json
+import os
+import time
+
+import numpy as np
+import pytest
+
+from harness import assert_same_binds, encoded, make_engine, make_oracle
+from kubesim_amd import tracegen
+from kubesim_amd.kubesim import KubeSim, TraceSubmitter, head_probe
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _sim(tr, enc, mode, **kw):
+    eng = make_engine(tr, enc, mode, **kw)
+    ks = KubeSim(eng, tr["tick_seconds"])
+    ks.register_submitter(TraceSubmitter(enc["pods"]))
+    return ks
+
+
+@pytest.mark.parametrize("windowed", [False, True])
+def test_c1_kat_through_the_run_loop(windowed):
+    with open(os.path.join(GOLDEN, "c1_kat.json")) as f:
+        kat = json.load(f)
+    T = kat["ticks"]
+    tr = tracegen.c1_trace(T)
+    enc = encoded(tr)
+    ks = _sim(tr, enc, "literal_const")
+    if windowed:
+        ks.run_windowed(T, 16)
+    else:
+        ks.run(T, probe=head_probe)
+    b = ks.all_binds()
+    got = [[int(x["pod"]), int(x["node"]), int(x["tick"]), int(x["status"])] for x in b]
+    assert got == kat["binds"]
+    np.testing.assert_array_equal(ks.eng.usage(), np.array(kat["usage"][T - 1]))
+    if not windowed:
+        assert ks.calls["step"] == T and ks.calls["probe"] == T
+
+
+def test_c2_prefix_per_tick_and_windowed_equal_oracle():
+    """5k nodes, stream arrivals (0-2 ticks apart): per-tick Run, windowed Run and the oracle."""
+    P, T = 1500, 1600
+    tr = tracegen.c2_trace(n_pods=P, arrival="stream")
+    enc = encoded(tr)
+    mode = "feeds_all_lrba"
+    ora = make_oracle(tr, mode)
+    ora.submit(tr)
+    ob, rc = ora.step(T, cap=T)
+    assert rc == 0
+
+    ks = _sim(tr, enc, mode)
+    t0 = time.perf_counter()
+    ks.run(T)
+    dt_tick = time.perf_counter() - t0
+    assert_same_binds(ks.all_binds(), ob)
+    np.testing.assert_array_equal(ks.eng.usage(), ora.usage())
+
+    ks2 = _sim(tr, enc, mode)
+    t0 = time.perf_counter()
+    ks2.run_windowed(T, 256)
+    dt_win = time.perf_counter() - t0
+    assert_same_binds(ks2.all_binds(), ob)
+    np.testing.assert_array_equal(ks2.eng.usage(), ora.usage())
+
+    ks3 = _sim(tr, enc, mode)
+    t0 = time.perf_counter()
+    ks3.run(300, probe=head_probe)
+    dt_probe = time.perf_counter() - t0
+    assert_same_binds(ks3.all_binds(), {k: v[:len(ks3.all_binds())] for k, v in ob.items()})
+    n = len(ob["pod"])
+    print(f"\ndrop-in C2 prefix: per-tick Run {n / dt_tick:.0f} pods/s ({dt_tick / T * 1e6:.0f} us/tick), "
+          f"windowed(256) {n / dt_win:.0f} pods/s, per-tick + filter/score probe "
+          f"{dt_probe / 300 * 1e6:.0f} us/tick")
+
+
+def test_windowed_refuses_placement_aware_submitters():
+    tr = tracegen.c1_trace(10)
+    enc = encoded(tr)
+    ks = _sim(tr, enc, "literal_const")
+    ks.register_submitter(lambda t, c: None)   # no placement_blind declaration
+    with pytest.raises(ValueError):
+        ks.run_windowed(10, 4)

@@ -98,3 +98,22 @@ def test_threaded_oracle_matches_serial(mode):
     for k in ("pod", "node", "tick", "status"):
         np.testing.assert_array_equal(b1[k], b4[k])
     np.testing.assert_array_equal(u1, u4)
+
+
+def test_oracle_refuses_ticks_past_int32_passed_seconds():
+    """Pod.passedSeconds is int32(seconds) (kubesim/pod/pod.go:148-153): the oracle evaluates no
+    tick 2^31 s or more after the first bind (KO_ERANGE = KS_ERANGE, not sticky)."""
+    tr = small_trace(5, n_nodes=32, n_pods=40, arrival="stream", selectors=False)
+    tr["tick_seconds"] = 1 << 20          # the domain ends 2047 ticks after the first bind
+    co = make_oracle(tr, "feeds_all_lrba")
+    co.submit(tr)
+    b, rc = co.step(200)
+    assert rc == 0 and len(b["pod"]) > 0
+    t0 = int(b["tick"][0])
+    last = t0 + (2**31 - 1) // (1 << 20)
+    b, rc = co.step(last - co.tick)
+    assert rc == 0 and co.tick == last
+    b, rc = co.step(1)
+    assert rc == 5 and co.tick == last and len(b["pod"]) == 0
+    b, rc = co.step(1)                    # refused again, nothing changes
+    assert rc == 5 and co.tick == last
