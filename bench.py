@@ -218,6 +218,7 @@ def main():
     ap.add_argument("--c5-pods", type=int, default=100_000)
     ap.add_argument("--vshards", type=int, default=1, help="c5: virtual node shards per rank")
     ap.add_argument("--no-c5", action="store_true", help="c3: skip the C5 node-sharded leg")
+    ap.add_argument("--no-dropin", action="store_true", help="c3: skip the drop-in Run-loop leg")
     ap.add_argument("--c5-steps", type=int, default=4, help="c3: timed steps of the C5 leg")
     ap.add_argument("--c5-timeout", type=float, default=240.0,
                     help="c3: seconds the C5 leg may take before it is abandoned (the C3 line still prints)")
@@ -303,6 +304,7 @@ def main():
     eng.usage_digest(max(0, t_now - S + 1), t_now + 1)
     digest_ms = (time.perf_counter() - t_u) * 1e3
     eng.close()
+    dropin = dropin_leg(trace, enc, scorers, local) if rank == 0 and not args.no_dropin else None
     line = None
 
     if rank == 0:
@@ -346,6 +348,7 @@ def main():
                             "digest_ms": digest_ms, "digest_ticks": S,
                             "note": "ks_usage_at wall time at ticks near the end of the run, incl. the "
                                     "24 B/node copy to the host; digest = every tick of the last step's window"},
+            "dropin": dropin,
             "c5_sharded": None,
             "cpu_baseline": cpu,
             "host": {"cpu": platform.processor() or platform.machine(), "nproc": os.cpu_count()},
@@ -359,6 +362,51 @@ def main():
         print(json.dumps({k: v for k, v in line.items() if k != "_printed"}), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def dropin_leg(trace, enc, scorers, device, per_tick=1000, probe_ticks=200, windowed=8192, window=1024):
+    """The drop-in's own call sequence (go/kubesim/engine/kubesim.go Run / RunWindowed, replayed
+    call for call by kubesim_amd.kubesim.KubeSim) on the C3 cluster with one pod arriving per
+    tick: per-tick Run (ks_submit_pods + ks_step(1) every tick), the same with the api.Filter /
+    api.Scorer adapters probing the queue head (ks_filter + ks_score), and RunWindowed.  Rates in
+    pods/s (one pod binds per tick); wall time incl. every host call."""
+    import numpy as np
+    from kubesim_amd.engine import Engine
+    from kubesim_amd.kubesim import KubeSim, TraceSubmitter, head_probe, slice_encoded
+
+    def sim(n_pods):
+        pods = dict(slice_encoded(enc["pods"], 0, n_pods))
+        pods["arrival"] = np.arange(1, n_pods + 1, dtype=np.int64)
+        eng = Engine(tick_seconds=trace["tick_seconds"], filter_mode=1, filters=7, scorers=scorers, device=device)
+        eng.load_nodes(enc["alloc"], enc["taint"], enc["label"])
+        ks = KubeSim(eng, trace["tick_seconds"])
+        ks.register_submitter(TraceSubmitter(pods))
+        return ks
+
+    out = {"workload": f"C3 cluster ({trace['nodes']['n']} nodes), trace pods 0.., one arrival per tick"}
+    ks = sim(per_tick + 16)
+    ks.run(16)   # warm-up
+    t0 = time.perf_counter()
+    ks.run(per_tick)
+    dt = time.perf_counter() - t0
+    out["per_tick"] = {"pods_per_s": per_tick / dt, "us_per_tick": dt / per_tick * 1e6, "ticks": per_tick}
+    ks.eng.close()
+    ks = sim(probe_ticks + 16)
+    ks.run(16)
+    t0 = time.perf_counter()
+    ks.run(probe_ticks, probe=head_probe)
+    dt = time.perf_counter() - t0
+    out["per_tick_with_filter_score_probe"] = {"pods_per_s": probe_ticks / dt, "us_per_tick": dt / probe_ticks * 1e6,
+                                               "ticks": probe_ticks}
+    ks.eng.close()
+    ks = sim(windowed + window)
+    ks.run_windowed(window, window)
+    t0 = time.perf_counter()
+    ks.run_windowed(windowed, window)
+    dt = time.perf_counter() - t0
+    out["windowed"] = {"pods_per_s": windowed / dt, "window": window, "ticks": windowed}
+    ks.eng.close()
+    return out
 
 
 def main_c4(args):

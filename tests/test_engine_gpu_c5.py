@@ -7,8 +7,8 @@ merge the all-gather feeds (ks_engine.cpp, ks_shard).  Checked:
   * an exact prefix bind-for-bind and usage-for-usage against the CPU oracle
     (kubesim/kubesim.go:90-225) at 1M nodes: 2,000 pods (the OpenMP oracle needs a few ms per pod
     here on the box's 16 threads);
-  * the sharded engine equals the unsharded engine over the whole 100k-pod trace (integer work,
-    so any difference is a bug in the exchange);
+  * the WHOLE 196,608-pod trace (every pod the bench's C5 leg binds), sharded and unsharded,
+    window by window against the oracle's committed digests (tests/golden/full_run.json);
   * the invariants of test_engine_gpu_large.py on the full run: FIFO one bind per tick, every
     bind Ok and satisfying the taint / selector filters, usage within capacity.
 At 1M nodes the resolver's touched-node filter is the hashed one (nodes > the exact-bitmap range),
@@ -19,12 +19,13 @@ import os
 import numpy as np
 import pytest
 
+import full_run_digest
 from harness import assert_same_binds, encoded, make_engine, make_oracle, oracle_run
 from kubesim_amd import tracegen
 
 pytestmark = pytest.mark.gpu
 MODE = "feeds_all_lrba"
-N_PODS = 100_000
+N_PODS = 196_608   # the pods bench.py's C5 leg binds (warm-up + 4 timed + 1 profiled steps)
 
 
 def _threads():
@@ -52,38 +53,34 @@ def test_c5_sharded_prefix_matches_oracle(c5):
     np.testing.assert_array_equal(eng.usage(), ora.usage())
 
 
-def test_c5_sharded_equals_unsharded_full_run(c5):
+def test_c5_whole_trace_sharded_and_unsharded_match_oracle_golden(c5):
+    """Every pod the bench's C5 leg binds (196,608), window by window against the oracle's
+    committed digests (tests/golden/full_run.json), both unsharded and with 8 virtual shards;
+    plus the invariants on the full run."""
     tr, enc = c5
-    m = tr["pods"]["m"]
+    g = full_run_digest.load("c5")
+    if g is None:
+        pytest.skip("tests/golden/full_run.json has no c5 run yet (tests/golden/make_full_run.py --only c5)")
+    assert g["pods"] == tr["pods"]["m"] and g["nodes"] == tr["nodes"]["n"]
     a = make_engine(tr, enc, MODE, shard=(1, 0, None, 8))
     a.submit(enc["pods"])
+    ea = full_run_digest.check_engine_run(a, g, "c5 sharded x8")
+    a.close()
     b = make_engine(tr, enc, MODE)
     b.submit(enc["pods"])
-    alloc = enc["alloc"]
+    eb = full_run_digest.check_engine_run(b, g, "c5 unsharded")
+    np.testing.assert_array_equal(ea, eb)
+    m = tr["pods"]["m"]
     taint = enc["taint"].astype(np.uint64)
     label = enc["label"].astype(np.uint64)
     tol = enc["pods"]["tol"].astype(np.uint64)
     sel = enc["pods"]["sel"].astype(np.uint64)
-    done, last_tick = 0, 0
-    for chunk in (10_000, 40_000, 50_000):
-        ea = a.step(chunk)
-        eb = b.step(chunk)
-        np.testing.assert_array_equal(ea, eb)
-        assert len(ea) == min(chunk, m - done)
-        np.testing.assert_array_equal(ea["pod"], np.arange(done, done + len(ea)))
-        assert (np.diff(ea["tick"]) > 0).all() and ea["tick"][0] > last_tick
-        assert (ea["status"] == 0).all()
-        nd = ea["node"]
-        assert ((nd >= 0) & (nd < tr["nodes"]["n"])).all()
-        pods = ea["pod"]
-        assert ((taint[nd] & ~tol[pods]) == 0).all()
-        assert ((label[nd] & sel[pods]) == sel[pods]).all()
-        ua, ub = a.usage(), b.usage()
-        np.testing.assert_array_equal(ua, ub)
-        for k in range(3):
-            cap = alloc[:, k]
-            has = cap >= 0
-            assert (ua[has, k] <= cap[has]).all(), f"resource {k} over capacity"
-        done += len(ea)
-        last_tick = int(ea["tick"][-1])
-    assert done == m
+    np.testing.assert_array_equal(eb["pod"], np.arange(m))
+    assert (np.diff(eb["tick"]) > 0).all() and (eb["status"] == 0).all()
+    nd, pods = eb["node"], eb["pod"]
+    assert ((taint[nd] & ~tol[pods]) == 0).all()
+    assert ((label[nd] & sel[pods]) == sel[pods]).all()
+    u, alloc = b.usage(), enc["alloc"]
+    for k in range(3):
+        has = alloc[:, k] >= 0
+        assert (u[has, k] <= alloc[has, k]).all(), f"resource {k} over capacity"

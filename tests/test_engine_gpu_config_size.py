@@ -10,16 +10,23 @@ C3 (50k nodes, 1M-pod trace, Filter fit+taint+selector -> LR+BA):
     predicate, kubesim/node/node.go:44-47), chosen nodes satisfy the pod's taint / selector
     filters, and the running pods' requests recomputed on the host from the binds never exceed
     any node's capacity; the per-tick usage digest agrees with ks_usage_at at sampled ticks.
+  * the WHOLE trace bind-for-bind against the oracle's committed per-window digests
+    (tests/golden/full_run.json) at the bench's batch, usage at every other window end;
+  * the reference-literal filter mode (kubesim/kubesim.go:182: the filter result is discarded)
+    on a 20,000-pod prefix against the oracle.
 C4 (1024 what-if scenarios x 2,000 nodes x 10,000 pods, one group, the default batch — so the
-  half-size RSmall resolver and the group-wide pods-per-workgroup are the ones exercised):
-  16 scenarios spread over the group bind-for-bind and usage-for-usage against the oracle over
-  their whole traces, every scenario checked with the invariants above.
+  small-class resolver and the group-wide pods-per-workgroup are the ones exercised): EVERY
+  scenario bind-for-bind and usage-for-usage against the oracle's committed digests
+  (tests/golden/c4_golden.json, tests/golden/make_c4_golden.py), the aborted-scenario count
+  pinned to the oracle's, every scenario checked with the invariants above.
 """
+import json
 import os
 
 import numpy as np
 import pytest
 
+import full_run_digest
 from harness import assert_same_binds, encoded, make_engine, make_oracle
 from kubesim_amd import tracegen
 
@@ -98,6 +105,37 @@ def test_c3_40k_pods_bit_exact_with_usage_samples(c3):
     assert_same_binds(eb, ob)
 
 
+def test_c3_whole_trace_matches_oracle_golden(c3):
+    """Every pod of the 1M-pod trace — the whole range bench.py times — bind-for-bind against the
+    oracle's committed digests (tests/golden/full_run.json, tests/golden/make_full_run.py), at
+    the bench's batch (the engine default), with usage at every other window end."""
+    tr, enc = c3
+    g = full_run_digest.load("c3")
+    assert g is not None and g["pods"] == tr["pods"]["m"] and g["nodes"] == tr["nodes"]["n"]
+    eng = make_engine(tr, enc, MODE)
+    eng.submit(enc["pods"])
+    full_run_digest.check_engine_run(eng, g, "c3")
+
+
+def test_c3_reference_literal_prefix(c3):
+    """The reference's own filter behaviour at C3 size: scheduleOneFilter's result is discarded
+    (kubesim/kubesim.go:182), so the filters constrain nothing and only admission decides Ok vs
+    OverCapacity — 20,000 pods bind-for-bind and usage-for-usage against the oracle."""
+    tr, enc = c3
+    P = 20_000
+    mode = "literal_lrba_filters_ignored"
+    eng = make_engine(tr, enc, mode)
+    eng.submit(enc["pods"])
+    ora = make_oracle(tr, mode)
+    ora.set_threads(_threads())
+    ora.submit(tracegen.slice_pods(tr, 0, P))
+    eb = eng.step(P)
+    ob, rc = ora.step(P, cap=P)
+    assert rc == 0
+    assert_same_binds(eb, ob)
+    np.testing.assert_array_equal(eng.usage(), ora.usage())
+
+
 def test_c3_full_trace_batch_independent_and_invariants(c3):
     tr, enc = c3
     m, n = tr["pods"]["m"], tr["nodes"]["n"]
@@ -155,22 +193,24 @@ def test_c4_1024_scenarios_config_size():
         traces.append(tr)
         encs.append(enc)
     per, st = _group_step_all(g, P, 2500)
-    sample = list(range(0, S, S // 16))
-    ok_runs = 0
-    for s in range(S):
+    with open(os.path.join(os.path.dirname(__file__), "golden", "c4_golden.json")) as f:
+        gold = json.load(f)
+    assert (gold["scenarios"], gold["nodes"], gold["pods"]) == (S, N, P)
+    # the abort count the oracle predicts for the whole group (NotFound runs stop as Run would)
+    assert sum(1 for x in st if x != 0) == gold["aborted"]
+    for s, rc, nb, bd, ud in gold["rows"]:
         b = per[s]
-        if st[s] == 0:
-            assert len(b) == P
-            ok_runs += 1
+        assert int(st[s]) == rc, (s, int(st[s]), rc)
+        assert len(b) == nb, (s, len(b), nb)
         _check_invariants(b, 0, N, encs[s])
-    assert ok_runs >= S // 2
-    for s in sample:
+        assert full_run_digest.bind_digest(b) == bd, f"scenario {s}: binds differ from the oracle's"
+        assert full_run_digest.digest(g.members[s].usage().astype(np.int64)) == ud, f"scenario {s}: usage"
+    # two scenarios also directly against the oracle (the golden's own generator path)
+    for s in (0, S - 1):
         ora = make_oracle(traces[s], MODE)
         ora.set_threads(_threads())
         ora.submit(traces[s])
         ob, rc = ora.step(P, cap=P)
         assert rc == int(st[s]), (s, rc, st[s])
         assert_same_binds(per[s], ob)
-        if rc == 0:
-            np.testing.assert_array_equal(g.members[s].usage(), ora.usage(), err_msg=f"scenario {s}")
     g.close()
