@@ -128,6 +128,23 @@ struct Shared {
     int32_t n_t, nb, e_cnt, pad_;
 };
 
+// Diagnostic build only (-DKS_STAMPS, `make stamps`): per-role cycle sums accumulated in
+// ctr[16..31] (layout: tests/dev/diag_pair.py); the real kernel executes no stamp.
+#ifdef KS_STAMPS
+__device__ __forceinline__ uint64_t pstamp() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define PR_STAMP(var) const uint64_t var = pstamp()
+#define PR_ACC(i, v) acc[i] += (v)
+#else
+#define PR_STAMP(var)
+#define PR_ACC(i, v)
+#endif
+
 __device__ __forceinline__ uint32_t hslot(int32_t node) { return ((uint32_t)node * 2654435761u) >> (32 - kHashLog2); }
 
 __device__ __forceinline__ int h_find(const Shared& sh, int32_t node) {
@@ -230,55 +247,61 @@ struct Dec {
     int32_t sa, sb;              // stage slots of untouched winners
     int32_t stop_a;              // 0 go; 1 exhausted list (commit before a); 2 NotFound; 3 InvalidArgument
     int32_t stop_b;              // the same for pod b (after pod a binds); 4: pod b is past the batch
-    int32_t extra;               // the mc term needs the extra fold round
-    uint64_t rest;               // pod b's maximum without the candidates' K1 (extra round)
-    int32_t su;                  // stage slot of pod b's untouched candidate
 };
 
-__device__ __forceinline__ void finish_b(Dec& d, uint64_t wbw, const PodW& pwb, int nt) {
-    if (wbw == 0) { d.stop_b = 2; return; }
-    if (pwb.w0 & (kFlagBadKey | kFlagBadSpec)) { d.stop_b = 3; return; }
-    d.wb = dw_node(wbw);
-    if (d.wb == d.wa) {
-        d.eb = d.ea;
-        return;
-    }
-    const int e = dw_ent(wbw);
-    if (e >= nt) {  // pod b's untouched list candidate (its word carries the new entry index)
-        d.eb = nt + d.na;
-        d.nbw = 1;
-        d.sb = d.su;
-    } else {
-        d.eb = e;
-    }
+// Pod a's winner and pod b's maximum without the extra round, straight-line (selects only: a
+// struct filled through references on early-return paths became a scratch-memory alloca on the
+// per-pair chain).  Returns pod b's decision word (before the extra round) in *wbw, its
+// candidates-excluded part in *rest, and whether the extra fold round is needed.
+__device__ __forceinline__ Dec decide(const Pc& p, uint32_t fa, uint32_t fb, bool b_in, int nt,
+                                      uint64_t* wbw_out, uint64_t* rest_out, bool* extra_out, int32_t* su_out) {
+    constexpr uint32_t kBad = kFlagBadKey | kFlagBadSpec;
+    const int32_t stop_a = p.kfull_a ? 1 : (p.best == 0 ? 2 : ((fa & kBad) ? 3 : 0));
+    const int32_t wa = dw_node(p.best);
+    const int e = dw_ent(p.best);
+    const int32_t na = e == kUnt ? 1 : 0;
+    const int32_t ea = na ? nt : e;
+    const uint32_t k2 = dw_k2(p.best);
+    const uint64_t k2w = k2 ? dword(k2, (uint32_t)wa, (uint32_t)ea, 0) : 0ull;
+    const bool v1_is_a = p.vb1 != 0 && key_node(p.vb1) == wa;
+    const uint64_t ub = v1_is_a ? p.vb2 : p.vb1;
+    const int32_t su = v1_is_a ? p.sb2 : p.sb1;
+    const bool exhausted_b = ub == 0 && p.full_b;
+    const uint64_t uw = dword_key(ub, (uint32_t)(nt + na), 0);
+    const uint64_t rest = umax64(umax64(p.m2, k2w), uw);
+    const bool mc_a = p.mc != 0 && dw_node(p.mc) == wa;
+    const uint64_t wbw = mc_a ? rest : umax64(rest, p.mc);
+    const int32_t stop_b = stop_a ? 4 : (!b_in ? 4 : (exhausted_b ? 1 : (wbw == 0 ? 2 : ((fb & kBad) ? 3 : 0))));
+    *extra_out = stop_a == 0 && b_in && !exhausted_b && mc_a && p.mc > rest;
+    *wbw_out = wbw;
+    *rest_out = rest;
+    *su_out = su;
+    Dec d;
+    d.stop_a = stop_a;
+    d.stop_b = stop_b;
+    d.wa = stop_a ? -1 : wa;
+    d.ea = stop_a ? -1 : ea;
+    d.na = stop_a ? 0 : na;
+    d.sa = (stop_a || !na) ? -1 : p.sa;
+    d.wb = d.eb = -1;
+    d.nbw = 0;
+    d.sb = -1;
+    return d;
 }
 
-__device__ __forceinline__ Dec decide(const Pc& p, const PodW& pwa, const PodW& pwb, bool b_in, int nt) {
-    Dec d;
-    d.wa = d.ea = d.wb = d.eb = -1;
-    d.na = d.nbw = 0;
-    d.sa = d.sb = d.su = -1;
-    d.stop_a = d.stop_b = 0;
-    d.extra = 0;
-    d.rest = 0;
-    if (p.kfull_a) { d.stop_a = 1; return d; }
-    if (p.best == 0) { d.stop_a = 2; return d; }
-    if (pwa.w0 & (kFlagBadKey | kFlagBadSpec)) { d.stop_a = 3; return d; }
-    d.wa = dw_node(p.best);
-    const int e = dw_ent(p.best);
-    if (e == kUnt) { d.ea = nt; d.na = 1; d.sa = p.sa; } else { d.ea = e; }
-    if (!b_in) { d.stop_b = 4; return d; }
-    const uint32_t k2 = dw_k2(p.best);
-    const uint64_t k2w = k2 ? dword(k2, (uint32_t)d.wa, (uint32_t)d.ea, 0) : 0ull;
-    const bool v1_is_a = p.vb1 != 0 && key_node(p.vb1) == d.wa;
-    const uint64_t ub = v1_is_a ? p.vb2 : p.vb1;
-    d.su = v1_is_a ? p.sb2 : p.sb1;
-    if (ub == 0 && p.full_b) { d.stop_b = 1; return d; }
-    const uint64_t uw = dword_key(ub, (uint32_t)(nt + d.na), 0);
-    d.rest = umax64(umax64(p.m2, k2w), uw);
-    const bool mc_a = p.mc != 0 && dw_node(p.mc) == d.wa;
-    if (mc_a && p.mc > d.rest) { d.extra = 1; return d; }
-    finish_b(d, mc_a ? d.rest : umax64(d.rest, p.mc), pwb, nt);
+// pod b's winner from its decision word (after the extra round when there was one)
+__device__ __forceinline__ Dec finish_b(Dec d, uint64_t wbw, uint32_t fb, int nt, int32_t su) {
+    constexpr uint32_t kBad = kFlagBadKey | kFlagBadSpec;
+    if (d.stop_b == 0) d.stop_b = wbw == 0 ? 2 : ((fb & kBad) ? 3 : 0);
+    const int32_t wb = dw_node(wbw);
+    const int e = dw_ent(wbw);
+    const bool same = wb == d.wa;
+    const bool bnew = !same && e >= nt;  // pod b's untouched list candidate (word carries entry nt + na)
+    const bool ok = d.stop_b == 0;
+    d.wb = ok ? wb : -1;
+    d.eb = ok ? (same ? d.ea : (bnew ? nt + d.na : e)) : -1;
+    d.nbw = ok && bnew ? 1 : 0;
+    d.sb = ok && bnew ? su : -1;
     return d;
 }
 
@@ -507,34 +530,43 @@ __global__ __launch_bounds__(kThreads) void resolve_pair_kernel(const EngineArgs
 
     int nt = n_pre;
     int committed = nb, err_code = 0, err_pod = -1;
+#ifdef KS_STAMPS
+    uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // work, wait, decision, role segments 1-4, extra rounds
+#endif
     for (int k = -1;; ++k) {
+        PR_STAMP(s0);
         const int pa = 2 * k, pb = pa + 1, pcn = pa + 2, pd = pa + 3;
         const int s_cur = (k + 3) % 3, s_nxt = (k + 4) % 3, s_nn = (k + 5) % 3;
         Dec dc;
         dc.wa = dc.ea = dc.wb = dc.eb = -1;
         dc.na = dc.nbw = 0;
-        dc.sa = dc.sb = dc.su = -1;
+        dc.sa = dc.sb = -1;
         dc.stop_a = 0;
         dc.stop_b = 4;
-        dc.extra = 0;
-        dc.rest = 0;
         if (k >= 0) {
             const Pc p = pc_regs(&sh.pc[s_cur]);
-            dc = decide(p, sh.pw[pa], sh.pw[pb], pb < nb, nt);
-            if (dc.extra) {
+            const uint32_t fa = sh.pw[pa].w0, fb = sh.pw[pb].w0;
+            uint64_t wbw, rest;
+            bool extra;
+            int32_t su;
+            dc = decide(p, fa, fb, pb < nb, nt, &wbw, &rest, &extra, &su);
+            if (extra) {
                 // the candidates of pod a other than w_a refold their K1_b (kept from the last
                 // iteration) into mcx; one more barrier
                 if (mc_keep != 0 && dw_node(mc_keep) != dc.wa) fold(&sh.pc[s_cur].mcx, mc_keep);
+                PR_ACC(7, 1);
                 __syncthreads();
-                const uint64_t mcx = sh.pc[s_cur].mcx;
-                finish_b(dc, umax64(dc.rest, mcx), sh.pw[pb], nt);
+                wbw = umax64(rest, sh.pc[s_cur].mcx);
             }
+            dc = finish_b(dc, wbw, fb, nt, su);
             if (dc.stop_a) {
                 committed = pa;
                 if (dc.stop_a > 1) { err_code = dc.stop_a == 2 ? kErrNotFound : kErrEinval; err_pod = (int32_t)(start + pa); }
                 break;
             }
         }
+        PR_STAMP(sd);
+        PR_ACC(2, sd - s0);
         const bool have_b = k >= 0 && dc.stop_b == 0;
         const bool prep = pcn < nb && (k < 0 || have_b);  // the next pair will be decided
         // window ranges: b = [lo_b, hi_b), c = [hi_b, hi_c), d = [lo_d, hi_d) — adjacent; for the
@@ -563,6 +595,8 @@ __global__ __launch_bounds__(kThreads) void resolve_pair_kernel(const EngineArgs
                 k2 = eval_t<kMode>(a.c, p_d, s2);
                 if (!(lane < 3 && xk != 0)) k2 = 0;
             }
+            PR_STAMP(w1);
+            PR_ACC(3, w1 - sd);
             // stage the pair's kept records for the bind (next iteration)
             if (prep && lane < kKeep && xk != 0) {
                 int64_t* d = sh.stage[(k + 1) & 1][lane];
@@ -599,8 +633,12 @@ __global__ __launch_bounds__(kThreads) void resolve_pair_kernel(const EngineArgs
                 Pc& q = sh.pc[s_nn];
                 q.best = 0; q.m2 = 0; q.mc = 0; q.mcx = 0;
             }
+            PR_STAMP(w2);
+            PR_ACC(4, w2 - w1);
             if (prep && pcn + 2 < nb) walk(pcn + 2, s_nn, xa, xb);
             else xk = 0;
+            PR_STAMP(w3);
+            PR_ACC(5, w3 - w2);
         } else if (wave == 1) {
             // ================= bind wave =================
             if (k >= 0) {
@@ -643,6 +681,8 @@ __global__ __launch_bounds__(kThreads) void resolve_pair_kernel(const EngineArgs
                         }
                     }
                 }
+                PR_STAMP(b1);
+                PR_ACC(3, b1 - sd);
                 const int own_a = own_slot(wpa), own_b = own_slot(wpb);
                 St s = isnew ? st_stage<St>(sh, k & 1, slot < 0 ? 0 : slot) : st_entry<St>(sh, ent < 0 ? 0 : ent);
                 bool ok_a = false, ok_b = false;
@@ -667,6 +707,8 @@ __global__ __launch_bounds__(kThreads) void resolve_pair_kernel(const EngineArgs
                         if (ok_a && own_a >= hi_b && own_a < hi_c) add_t(s, p_a, -1);
                     }
                 }
+                PR_STAMP(b2);
+                PR_ACC(4, b2 - b1);
                 // s: the node's state before pod c.  One evaluator pass over the six lanes:
                 // var 0 key_c, var 1 K1_d (window d applied), var 2 K2_d (c bound, window d)
                 uint32_t t = 0;
@@ -705,6 +747,8 @@ __global__ __launch_bounds__(kThreads) void resolve_pair_kernel(const EngineArgs
                         else fold(&sh.pc[s_nxt].m2, w1);
                     }
                 }
+                PR_STAMP(b3);
+                PR_ACC(5, b3 - b2);
                 // state, table and outputs (lane 0: w_a; lane 1: w_b when distinct)
                 if (writer) {
                     if (isnew) {
@@ -778,6 +822,8 @@ __global__ __launch_bounds__(kThreads) void resolve_pair_kernel(const EngineArgs
                 st_store(sh, r, st);
                 pf_stale = true;
             }
+            PR_STAMP(o1);
+            PR_ACC(3, o1 - sd);
             mc_keep = 0;
             bool pass_c = false, pass_d = false;
             if (prep && valid) {
@@ -790,6 +836,8 @@ __global__ __launch_bounds__(kThreads) void resolve_pair_kernel(const EngineArgs
                              (pf.live && make_key(prune_tmax(a.c, pf, qd0, qd1) + 1u, (uint32_t)st_node) >= lbk_d);
                 }
             }
+            PR_STAMP(o2);
+            PR_ACC(4, o2 - o1);
             if (__ballot(pass_c || pass_d)) {
                 // key_c on the entry's state, K1_d with window d applied
                 St s1 = st;
@@ -818,8 +866,14 @@ __global__ __launch_bounds__(kThreads) void resolve_pair_kernel(const EngineArgs
                     else fold(&sh.pc[s_nxt].m2, w1);
                 }
             }
+            PR_STAMP(o3);
+            PR_ACC(5, o3 - o2);
         }
+        PR_STAMP(s1);
         __syncthreads();
+        PR_STAMP(s2);
+        PR_ACC(0, s1 - s0);
+        PR_ACC(1, s2 - s1);
         nt += dc.na + dc.nbw;
         if (k >= 0) {
             if (!have_b) {
@@ -834,6 +888,21 @@ __global__ __launch_bounds__(kThreads) void resolve_pair_kernel(const EngineArgs
         }
     }
     __syncthreads();
+#ifdef KS_STAMPS
+    {   // ctr[8 + 6 * role + i]: role 0 walker (wave 0), 1 bind wave, 2 owner wave 2, 3 owner wave 7;
+        // i: 0 work, 1 barrier wait, 2 decision, 3-5 role segments; ctr[5] launches, ctr[6] pods,
+        // ctr[7] extra fold rounds
+        unsigned long long* d = (unsigned long long*)a.ctr;
+        const int role = wave <= 2 ? wave : (wave == 7 ? 3 : -1);
+        if (lane == 0 && role >= 0)
+            for (int q = 0; q < 6; ++q) atomicAdd(&d[8 + 6 * role + q], acc[q]);
+        if (tid == 0) {
+            atomicAdd(&d[5], 1ull);
+            atomicAdd(&d[6], (unsigned long long)committed);
+            atomicAdd(&d[7], acc[7]);
+        }
+    }
+#endif
     // ---- write back the mutable fields of every touched node
     for (int e = tid; e < nt; e += kThreads) {
         const int64_t ndx = sh.tnode[e];

@@ -206,5 +206,5 @@ def test_submit_checks_array_lengths():
     with pytest.raises(ValueError):
         eng.submit(bad)
     eng.submit(enc["pods"])
-    b = eng.step(10**9)            # cap defaults to the queued pods, not 10^9 rows
+    b = eng.step(10**8)            # cap defaults to the queued pods, not 10^8 rows (10^8 ticks of 10 s: inside the int32 passed-seconds domain)
     assert len(b) == 50
