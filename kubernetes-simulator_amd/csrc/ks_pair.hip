@@ -63,7 +63,7 @@ constexpr int kOwner0 = 2;               // waves 2..15 own the entries
 constexpr int kUnt = 1023;               // entry field of an untouched node
 constexpr int kKeep = 7;                 // walker lanes: 3 candidates of pod c, 4 of pod d
 constexpr int kPodPad = 4;
-static_assert(kTMax <= (kThreads / kWave - kOwner0) * kWave, "one entry per owner lane");
+static_assert(kTMax <= (kThreads / kWave - kOwner0) * kWave, "one entry per owner lane");  // slots 0..13
 static_assert(kMaxExp <= kThreads, "one thread per pre-inserted expiry");
 static_assert(kTMax < kUnt, "entry index fits 10 bits");
 
@@ -88,17 +88,20 @@ __device__ __forceinline__ void fold(uint64_t* slot, uint64_t v) {
 __device__ __forceinline__ uint64_t umax64(uint64_t x, uint64_t y) { return x > y ? x : y; }
 
 // Control record of pair k (ring of three): folds made in iteration k-1, the walker's list
-// candidates of pod b (iteration k-1) and lower bounds of both pods (iteration k-2).
+// candidates of pod b (iteration k-1) and lower bounds of both pods (iteration k-2).  The first
+// 48 bytes are what every wave's decision reads.
 struct alignas(16) Pc {
-    uint64_t best, m2, mc, mcx;  // folds (zeroed two iterations ahead)
-    uint64_t vb1, vb2;           // pod b's untouched list candidates, packed-key form, 0 = none
+    uint64_t best, m2, mc;       // folds (zeroed two iterations ahead)
+    uint64_t vb1, vb2;           // pod b's untouched list candidates, decision words (entry kUnt), 0 = none
+    uint32_t fl;                 // kfull_a | full_b << 1 | (sa + 1) << 4 | (sb1 + 1) << 8 | (sb2 + 1) << 12
+    uint32_t pad0;
     uint64_t lbk_a, lbk_b;       // lower bounds of the pair's winners (packed-key form)
-    int32_t kfull_a;             // pod a: a full list with no untouched entry left -> stop
-    int32_t full_b;              // pod b's list holds L entries
-    int32_t sa, sb1, sb2;        // stage slots of pod a's / pod b's untouched candidates
-    int32_t pad[3];
+    uint64_t mcx, pad1;          // extra fold round
 };
-static_assert(sizeof(Pc) == 96, "Pc: six 16-byte words");
+static_assert(sizeof(Pc) == 80, "Pc: five 16-byte words");
+__device__ __forceinline__ bool pc_kfull_a(const Pc& p) { return p.fl & 1u; }
+__device__ __forceinline__ bool pc_full_b(const Pc& p) { return (p.fl >> 1) & 1u; }
+__device__ __forceinline__ int32_t pc_slot(const Pc& p, int which) { return (int32_t)((p.fl >> (4 + 4 * which)) & 15u) - 1; }
 
 // Per-pod control: flags | (own expiry slot + 1) << 2, run ticks, the pod's window [lo, hi).
 struct alignas(16) PodW {
@@ -116,7 +119,7 @@ struct Shared {
     uint32_t tfilt[kFilterBits / 32];
     PodRec pod[kMaxB + kPodPad];
     float podf[kMaxB + kPodPad][2];
-    PodW pw[kMaxB + kPodPad];
+    PodW pwx[kMaxB + kPodPad + 2];  // pod i at pwx[i + 2] (the prologue reads pods -2, -1)
     uint64_t cand[kMaxB][kL];
     int32_t ex_q[kMaxExp];
     int32_t ex_node[kMaxExp];
@@ -125,6 +128,7 @@ struct Shared {
     int64_t ex_req[kMaxExp][3];
     Pc pc[3];
     int64_t stage[2][kKeep][10];  // snapshot records of a pair's kept list candidates
+    uint64_t dec_word;  // the bind wave's published decision: (2k + final) << 32 | dec_pack()
     int32_t n_t, nb, e_cnt, pad_;
 };
 
@@ -224,20 +228,95 @@ __device__ __forceinline__ PodRec pod_regs(const PodRec* src) {
     __builtin_memcpy(reinterpret_cast<char*>(&p) + 32, &w2, 16);
     return p;
 }
+// The decision's 48 bytes of a control record.  Every wave reads the same bytes: as a
+// full-wave ds_read each 16-byte load costs the LDS 64 lanes x 16 B; KS_PR_UNI reads them with
+// lane 0 alone and broadcasts through SGPRs (readfirstlane).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+#ifndef KS_PR_UNI
+#define KS_PR_UNI 0
+#endif
 __device__ __forceinline__ Pc pc_regs(const Pc* src) {
-    const uint4* w = reinterpret_cast<const uint4*>(src);
-    const uint4 w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4], w5 = w[5];
-    asm volatile("" ::"v"(w0.x), "v"(w0.y), "v"(w0.z), "v"(w0.w), "v"(w1.x), "v"(w1.y), "v"(w1.z), "v"(w1.w),
-                 "v"(w2.x), "v"(w2.y), "v"(w2.z), "v"(w2.w), "v"(w3.x), "v"(w3.y), "v"(w3.z), "v"(w3.w),
-                 "v"(w4.x), "v"(w4.y), "v"(w4.z), "v"(w4.w), "v"(w5.x), "v"(w5.y), "v"(w5.z), "v"(w5.w));
+    u32x4 w0, w1, w2;
+#if KS_PR_UNI
+    uint64_t sv;
+    asm volatile(
+        "s_mov_b64 %[sv], exec\n\t"
+        "s_mov_b64 exec, 1\n\t"
+        "ds_read_b128 %[a], %[ad]\n\t"
+        "ds_read_b128 %[b], %[ad] offset:16\n\t"
+        "ds_read_b128 %[c], %[ad] offset:32\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_mov_b64 exec, %[sv]"
+        : [a] "=&v"(w0), [b] "=&v"(w1), [c] "=&v"(w2), [sv] "=&s"(sv)
+        : [ad] "v"(lds_addr(src))
+        : "memory");
+    w0 = u32x4{rfl(w0.x), rfl(w0.y), rfl(w0.z), rfl(w0.w)};
+    w1 = u32x4{rfl(w1.x), rfl(w1.y), rfl(w1.z), rfl(w1.w)};
+    w2 = u32x4{rfl(w2.x), rfl(w2.y), rfl(w2.z), rfl(w2.w)};
+#else
+    const u32x4* w = reinterpret_cast<const u32x4*>(src);
+    w0 = w[0]; w1 = w[1]; w2 = w[2];
+    asm volatile("" ::"v"(w0), "v"(w1), "v"(w2));
+#endif
     Pc p;
     __builtin_memcpy(&p, &w0, 16);
     __builtin_memcpy(reinterpret_cast<char*>(&p) + 16, &w1, 16);
     __builtin_memcpy(reinterpret_cast<char*>(&p) + 32, &w2, 16);
-    __builtin_memcpy(reinterpret_cast<char*>(&p) + 48, &w3, 16);
-    __builtin_memcpy(reinterpret_cast<char*>(&p) + 64, &w4, 16);
-    __builtin_memcpy(reinterpret_cast<char*>(&p) + 80, &w5, 16);
     return p;
+}
+
+// Everything uniform an iteration starts from: the pair's control record, the four pods' PodW
+// (a, b, c, d: contiguous), the next pair's lower bounds.  One round of LDS reads.
+struct Head {
+    Pc p;
+    PodW w[4];
+    uint64_t lbk_c, lbk_d;
+};
+__device__ __forceinline__ PodW podw_of(u32x4 v) { return PodW{v.x, (int32_t)v.y, (int32_t)v.z, (int32_t)v.w}; }
+__device__ __forceinline__ Head head_regs(const Pc* pcur, const PodW* pw4, const Pc* pnxt) {
+    u32x4 w0, w1, w2, q0, q1, q2, q3, l;
+#if KS_PR_UNI
+    uint64_t sv;
+    asm volatile(
+        "s_mov_b64 %[sv], exec\n\t"
+        "s_mov_b64 exec, 1\n\t"
+        "ds_read_b128 %[w0], %[ap]\n\t"
+        "ds_read_b128 %[w1], %[ap] offset:16\n\t"
+        "ds_read_b128 %[w2], %[ap] offset:32\n\t"
+        "ds_read_b128 %[q0], %[aw]\n\t"
+        "ds_read_b128 %[q1], %[aw] offset:16\n\t"
+        "ds_read_b128 %[q2], %[aw] offset:32\n\t"
+        "ds_read_b128 %[q3], %[aw] offset:48\n\t"
+        "ds_read_b128 %[l], %[al] offset:48\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_mov_b64 exec, %[sv]"
+        : [w0] "=&v"(w0), [w1] "=&v"(w1), [w2] "=&v"(w2), [q0] "=&v"(q0), [q1] "=&v"(q1), [q2] "=&v"(q2),
+          [q3] "=&v"(q3), [l] "=&v"(l), [sv] "=&s"(sv)
+        : [ap] "v"(lds_addr(pcur)), [aw] "v"(lds_addr(pw4)), [al] "v"(lds_addr(pnxt))
+        : "memory");
+#define PR_RFL(v) v = u32x4{rfl(v.x), rfl(v.y), rfl(v.z), rfl(v.w)}
+    PR_RFL(w0); PR_RFL(w1); PR_RFL(w2); PR_RFL(q0); PR_RFL(q1); PR_RFL(q2); PR_RFL(q3); PR_RFL(l);
+#undef PR_RFL
+#else
+    const u32x4* a = reinterpret_cast<const u32x4*>(pcur);
+    const u32x4* b = reinterpret_cast<const u32x4*>(pw4);
+    w0 = a[0]; w1 = a[1]; w2 = a[2];
+    q0 = b[0]; q1 = b[1]; q2 = b[2]; q3 = b[3];
+    l = reinterpret_cast<const u32x4*>(pnxt)[3];
+    asm volatile("" ::"v"(w0), "v"(w1), "v"(w2), "v"(q0), "v"(q1), "v"(q2), "v"(q3), "v"(l));
+#endif
+    Head h;
+    __builtin_memcpy(&h.p, &w0, 16);
+    __builtin_memcpy(reinterpret_cast<char*>(&h.p) + 16, &w1, 16);
+    __builtin_memcpy(reinterpret_cast<char*>(&h.p) + 32, &w2, 16);
+    h.w[0] = podw_of(q0); h.w[1] = podw_of(q1); h.w[2] = podw_of(q2); h.w[3] = podw_of(q3);
+    h.lbk_c = (uint64_t)l.x | (uint64_t)l.y << 32;
+    h.lbk_d = (uint64_t)l.z | (uint64_t)l.w << 32;
+    return h;
 }
 
 // The pair's decision, computed identically by every wave from Pc[k] (uniform values).
@@ -255,54 +334,96 @@ struct Dec {
 // candidates-excluded part in *rest, and whether the extra fold round is needed.
 __device__ __forceinline__ Dec decide(const Pc& p, uint32_t fa, uint32_t fb, bool b_in, int nt,
                                       uint64_t* wbw_out, uint64_t* rest_out, bool* extra_out, int32_t* su_out) {
+    // Every wave makes this decision from the same words, and the compiler runs it on the scalar
+    // unit: it is the per-pair burst that fills each SIMD's scalar issue after the barrier, so it
+    // is written for the fewest scalar instructions — node identity by masked XOR, the K2 word
+    // by one shift and mask, b's list candidates pre-packed as decision words by the walker.
     constexpr uint32_t kBad = kFlagBadKey | kFlagBadSpec;
-    const int32_t stop_a = p.kfull_a ? 1 : (p.best == 0 ? 2 : ((fa & kBad) ? 3 : 0));
-    const int32_t wa = dw_node(p.best);
-    const int e = dw_ent(p.best);
+    constexpr uint64_t kNodeBits = 0xFFFFFFull << 25;
+    constexpr uint64_t kNodeEntBits = ((1ull << 34) - 1) << 15;
+    const uint64_t best = p.best;
+    const int32_t stop_a = (p.fl & 1u) ? 1 : (best == 0 ? 2 : ((fa & kBad) ? 3 : 0));
+    const int e = dw_ent(best);
     const int32_t na = e == kUnt ? 1 : 0;
     const int32_t ea = na ? nt : e;
-    const uint32_t k2 = dw_k2(p.best);
-    const uint64_t k2w = k2 ? dword(k2, (uint32_t)wa, (uint32_t)ea, 0) : 0ull;
-    const bool v1_is_a = p.vb1 != 0 && key_node(p.vb1) == wa;
-    const uint64_t ub = v1_is_a ? p.vb2 : p.vb1;
-    const int32_t su = v1_is_a ? p.sb2 : p.sb1;
-    const bool exhausted_b = ub == 0 && p.full_b;
-    const uint64_t uw = dword_key(ub, (uint32_t)(nt + na), 0);
+    const uint64_t k2 = best & 0x7FFFull;
+    const uint64_t k2w = k2 ? (k2 << 49) | (best & kNodeEntBits) : 0ull;
+    const bool v1_is_a = p.vb1 != 0 && ((p.vb1 ^ best) & kNodeBits) == 0;
+    const uint64_t uw = v1_is_a ? p.vb2 : p.vb1;
+    const int32_t su = pc_slot(p, v1_is_a ? 2 : 1);
+    const bool exhausted_b = uw == 0 && (p.fl & 2u);
     const uint64_t rest = umax64(umax64(p.m2, k2w), uw);
-    const bool mc_a = p.mc != 0 && dw_node(p.mc) == wa;
+    const bool mc_a = p.mc != 0 && ((p.mc ^ best) & kNodeBits) == 0;
     const uint64_t wbw = mc_a ? rest : umax64(rest, p.mc);
-    const int32_t stop_b = stop_a ? 4 : (!b_in ? 4 : (exhausted_b ? 1 : (wbw == 0 ? 2 : ((fb & kBad) ? 3 : 0))));
-    *extra_out = stop_a == 0 && b_in && !exhausted_b && mc_a && p.mc > rest;
+    // pod b's stop before its word is final (NotFound / bad pod: finish_b, after the extra round)
+    const int32_t stop_b = stop_a ? 4 : (!b_in ? 4 : (exhausted_b ? 1 : 0));
+    *extra_out = stop_b == 0 && mc_a && p.mc > rest;
     *wbw_out = wbw;
     *rest_out = rest;
     *su_out = su;
     Dec d;
     d.stop_a = stop_a;
     d.stop_b = stop_b;
-    d.wa = stop_a ? -1 : wa;
-    d.ea = stop_a ? -1 : ea;
-    d.na = stop_a ? 0 : na;
-    d.sa = (stop_a || !na) ? -1 : p.sa;
+    d.wa = dw_node(best);
+    d.ea = ea;
+    d.na = na;
+    d.sa = na ? pc_slot(p, 0) : -1;
     d.wb = d.eb = -1;
     d.nbw = 0;
     d.sb = -1;
     return d;
 }
 
-// pod b's winner from its decision word (after the extra round when there was one)
-__device__ __forceinline__ Dec finish_b(Dec d, uint64_t wbw, uint32_t fb, int nt, int32_t su) {
+// pod b's winner from its decision word (after the extra round when there was one); only
+// meaningful while stop_a == 0 (the loop ends otherwise)
+__device__ __forceinline__ Dec finish_b(Dec d, uint64_t wbw, uint64_t best, uint32_t fb, int nt, int32_t su) {
     constexpr uint32_t kBad = kFlagBadKey | kFlagBadSpec;
+    constexpr uint64_t kNodeBits = 0xFFFFFFull << 25;
     if (d.stop_b == 0) d.stop_b = wbw == 0 ? 2 : ((fb & kBad) ? 3 : 0);
-    const int32_t wb = dw_node(wbw);
     const int e = dw_ent(wbw);
-    const bool same = wb == d.wa;
-    const bool bnew = !same && e >= nt;  // pod b's untouched list candidate (word carries entry nt + na)
+    const bool same = ((wbw ^ best) & kNodeBits) == 0;
+    const bool bnew = !same && e >= nt;  // b's untouched list candidate: its word carries kUnt
     const bool ok = d.stop_b == 0;
-    d.wb = ok ? wb : -1;
+    d.wb = ok ? dw_node(wbw) : -1;
     d.eb = ok ? (same ? d.ea : (bnew ? nt + d.na : e)) : -1;
     d.nbw = ok && bnew ? 1 : 0;
     d.sb = ok && bnew ? su : -1;
     return d;
+}
+
+// The owners' part of a decision, as the bind wave publishes it (KS_PR_PUB): entries of the two
+// winners, the table growth, the stops and the extra-round flag in 29 bits.
+#ifndef KS_PR_PUB
+#define KS_PR_PUB 1
+#endif
+#ifndef KS_PR_PRE
+#define KS_PR_PRE 0
+#endif
+__device__ __forceinline__ uint32_t dec_pack(const Dec& d, bool extra) {
+    return (uint32_t)(d.ea + 1) | (uint32_t)(d.eb + 1) << 10 | (uint32_t)(d.na + d.nbw) << 20 |
+           (uint32_t)d.stop_a << 22 | (uint32_t)d.stop_b << 25 | (extra ? 1u << 28 : 0u);
+}
+__device__ __forceinline__ Dec dec_unpack(uint32_t w) {
+    Dec d;
+    d.ea = (int32_t)(w & 1023u) - 1;
+    d.eb = (int32_t)((w >> 10) & 1023u) - 1;
+    d.na = (int32_t)((w >> 20) & 3u);  // na + nbw: only the table growth matters to an owner
+    d.nbw = 0;
+    d.stop_a = (int32_t)((w >> 22) & 7u);
+    d.stop_b = (int32_t)((w >> 25) & 7u);
+    d.wa = d.wb = -1;
+    d.sa = d.sb = -1;
+    return d;
+}
+// an owner waits for the bind wave's word of iteration k, phase ph (0: pre-extra, 1: final)
+__device__ __forceinline__ uint32_t dec_wait(const uint64_t* word, int k, int ph) {
+    const uint32_t want = (uint32_t)(2 * k + ph);
+    for (;;) {
+        const uint64_t w = *reinterpret_cast<const volatile uint64_t*>(word);
+        const uint32_t hi = (uint32_t)(w >> 32);
+        if (hi == want || (ph == 0 && hi == want + 1)) return (uint32_t)w | (hi & 1u) << 31;
+        __builtin_amdgcn_s_sleep(1);
+    }
 }
 
 // Entry state in registers: 32-bit fields for the narrow evaluators (every capacity < 2^29 and
@@ -373,105 +494,19 @@ __device__ __forceinline__ void sub_dl(T& s, const Dl<F>& d) {
 // the pod's own expiry slot within the batch window, or -1
 __device__ __forceinline__ int own_slot(const PodW& w) { return (int)(w.w0 >> 2) - 1; }
 
-// ---------------------------------------------------------------------------------------------
-template <int kMode>
-__global__ __launch_bounds__(kThreads) void resolve_pair_kernel(const EngineArgs* __restrict__ A) {
+// One role's whole loop (kRole 0 walker, 1 bind wave, 2 owners): each role carries only its own
+// state around its loop, so the register allocator sees three disjoint loops instead of one
+// loop whose every branch keeps every role's loop-carried values live.  All roles execute the
+// same barriers (one per pair, one more per extra fold round).
+struct LoopOut {
+    int nt, committed, err_code, err_pod;
+};
+template <int kMode, int kRole>
+__device__ __forceinline__ LoopOut pair_loop(const EngineArgs& a, Shared& sh, const int tid, const int lane,
+                                             const int wave, const int nb, const int n_pre, const bool exact,
+                                             const int64_t start, const int oslot) {
     using St = typename StSel<kMode>::T;
     using DF = typename DlSel<kMode>::T;
-    __shared__ Shared sh;
-    const EngineArgs& a = A[blockIdx.x];  // fields read where used (scalar loads): fewer live SGPRs
-    const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid >> 6;
-    const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
-    if (a.ctr[kCtrErr] != 0) return;
-    const bool exact = a.c.n_nodes <= kFilterBits;
-    int nb = (int)min<int64_t>(min<int64_t>(a.B, kMaxB), end - start);
-    if (nb <= 0) return;
-
-    // ---- setup (as resolve_kernel): the largest batch whose expiry window fits the pre-insert
-    // budget, pods / lists / window slots into LDS, pre-insert the nodes the window's expiries
-    // land on, their records
-    const int64_t e_base = a.exp_off[start + 1];
-    const int64_t off_mid = tid < nb ? a.exp_off[start + tid + 1] : 0;
-    const bool fits_win = tid < nb && off_mid - e_base <= kMaxExp;
-    if (tid == 0) sh.n_t = 0;
-    if (tid < 3) {
-        uint4* w = reinterpret_cast<uint4*>(&sh.pc[tid]);
-        for (int q = 0; q < 6; ++q) w[q] = make_uint4(0, 0, 0, 0);
-    }
-    for (int h = tid; h < kHash; h += kThreads) sh.hkey[h] = -1;
-    for (int w = tid; w < kFilterBits / 32; w += kThreads) sh.tfilt[w] = 0;
-    nb = __syncthreads_count(fits_win);
-    if (tid == nb - 1) { sh.nb = nb; sh.e_cnt = nb > 1 ? (int32_t)(off_mid - e_base) : 0; }
-    __syncthreads();
-    const int e_cnt = sh.e_cnt;
-    for (int i = tid; i < kMaxB + kPodPad; i += kThreads) {
-        PodRec p{};
-        PodW w{0, 0, e_cnt, e_cnt};
-        if (i < nb) {
-            p = a.pods[start + i];
-            const int64_t pos = a.exp_pos[start + i];
-            const int32_t own = (pos >= e_base && pos - e_base < e_cnt) ? (int32_t)(pos - e_base) : -1;
-            w.w0 = p.flags | (uint32_t)(own + 1) << 2;
-            w.dur = a.dur[start + i];
-            w.lo = i >= 1 ? (int32_t)(a.exp_off[start + i] - e_base) : 0;
-            w.hi = i >= 1 ? (int32_t)(a.exp_off[start + i + 1] - e_base) : 0;
-        }
-        sh.pod[i] = p;
-        sh.podf[i][0] = (float)p.req[0];
-        sh.podf[i][1] = (float)p.req[1];
-        sh.pw[i] = w;
-    }
-    for (int i = tid; i < nb * kL; i += kThreads) sh.cand[i / kL][i % kL] = a.cand[i];
-    for (int e = tid; e < e_cnt; e += kThreads) {
-        const int32_t q = a.exp_pod[e_base + e];
-        const PodRec& pq = a.pods[q];
-        sh.ex_q[e] = q;
-        sh.ex_entry[e] = -1;
-        sh.ex_req[e][0] = pq.req[0]; sh.ex_req[e][1] = pq.req[1]; sh.ex_req[e][2] = pq.req[2];
-        if (q < start) {
-            sh.ex_node[e] = a.b_node[q];
-            sh.ex_ok[e] = (a.b_status[q] == 0) && !a.expired[q];
-        } else {
-            sh.ex_node[e] = -1;
-            sh.ex_ok[e] = 0;  // set when the pod binds
-        }
-    }
-    __syncthreads();
-    const bool pre_want = tid < e_cnt && sh.ex_ok[tid];
-    int pre_slot = -1;
-    bool pre_claim = false;
-    if (pre_want) {
-        const int32_t nd = sh.ex_node[tid];
-        uint32_t hs = hslot(nd);
-        for (;;) {  // the table holds <= kMaxExp < kHash nodes: terminates
-            const int32_t prev = atomicCAS(&sh.hkey[hs], -1, nd);
-            if (prev == -1 || prev == nd) { pre_slot = (int)hs; pre_claim = prev == -1; break; }
-            hs = (hs + 1) & (kHash - 1);
-        }
-    }
-    __syncthreads();
-    if (pre_claim) {
-        const int32_t nd = sh.ex_node[tid];
-        const int idx = atomicAdd(&sh.n_t, 1);
-        sh.hval[pre_slot] = idx;
-        sh.tnode[idx] = nd;
-        const uint32_t f = (uint32_t)nd & (kFilterBits - 1);
-        atomicOr(&sh.tfilt[f >> 5], 1u << (f & 31));
-    }
-    __syncthreads();
-    if (pre_want) sh.ex_entry[tid] = sh.hval[pre_slot];
-    const int n_pre = sh.n_t;
-    for (int e = tid; e < kTMax; e += kThreads) sh.dirty[e] = -1;
-    for (int e = tid; e < n_pre; e += kThreads) {
-        const NodeV v = load_node(a.s, sh.tnode[e]);
-        sh.ts[0][e] = v.ac; sh.ts[1][e] = v.am; sh.ts[2][e] = v.ag; sh.ts[3][e] = v.ap;
-        sh.ts[4][e] = v.rc; sh.ts[5][e] = v.rm; sh.ts[6][e] = v.rg; sh.ts[7][e] = v.nr;
-        sh.tu[0][e] = v.taint; sh.tu[1][e] = v.label;
-    }
-
-    // ---- per-thread state, shared by the roles (a wave has one role for the whole launch):
-    // st = an owner's entry state / the walker's kept record; xk = the walker's kept key
-    const int oslot = wave - kOwner0;           // owner slot (waves 2..15)
     const int r = oslot >= 0 ? oslot * kWave + lane : kTMax;
     bool loaded = false, pf_stale = true, full_c = false, full_d = false;
     St st{};
@@ -518,14 +553,9 @@ __global__ __launch_bounds__(kThreads) void resolve_pair_kernel(const EngineArgs
             conv(v, st);
         }
     };
-    __syncthreads();
-
-    // owner waves that can never own an entry end here (the table grows by <= nb entries);
-    // s_barrier waits only for the surviving waves
-    if (oslot >= 0 && oslot * kWave >= n_pre + nb) return;
 
     // pre-prologue: pair 0's lists (no winner known yet)
-    if (wave == 0) walk(0, 0, -1, -1);
+    if constexpr (kRole == 0) walk(0, 0, -1, -1);
     __syncthreads();
 
     int nt = n_pre;
@@ -533,19 +563,42 @@ __global__ __launch_bounds__(kThreads) void resolve_pair_kernel(const EngineArgs
 #ifdef KS_STAMPS
     uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // work, wait, decision, role segments 1-4, extra rounds
 #endif
+    int s_cur = 2, s_nxt = 0, s_nn = 1;  // control-record ring slots of pairs k, k+1, k+2 (k = -1 first)
     for (int k = -1;; ++k) {
         PR_STAMP(s0);
         const int pa = 2 * k, pb = pa + 1, pcn = pa + 2, pd = pa + 3;
-        const int s_cur = (k + 3) % 3, s_nxt = (k + 4) % 3, s_nn = (k + 5) % 3;
         Dec dc;
         dc.wa = dc.ea = dc.wb = dc.eb = -1;
         dc.na = dc.nbw = 0;
         dc.sa = dc.sb = -1;
         dc.stop_a = 0;
         dc.stop_b = 4;
-        if (k >= 0) {
-            const Pc p = pc_regs(&sh.pc[s_cur]);
-            const uint32_t fa = sh.pw[pa].w0, fb = sh.pw[pb].w0;
+        const Head hd = head_regs(&sh.pc[s_cur], &sh.pwx[pa + 2], &sh.pc[s_nxt]);
+        // bind wave (KS_PR_PRE): what its bind reads that does not depend on the decision, loaded before it
+        // (the loads' latency hides under the decision's scalar work): the expiry slots of
+        // windows b..d (first 64) and the staged record of pod a's (even lanes) / pod b's first
+        // (odd lanes) list candidate
+        int32_t pq = -1, pte = -1, pok = 0, pslot = -1;
+        DF pr0 = 0, pr1 = 0, pr2 = 0;
+        St spre{};
+        if constexpr (kRole == 1 && KS_PR_PRE) {
+            if (k >= 0) {
+                const int x = hd.w[1].lo + lane;
+                if (x < hd.w[3].hi) {
+                    pq = sh.ex_q[x]; pte = sh.ex_entry[x]; pok = sh.ex_ok[x];
+                    pr0 = (DF)sh.ex_req[x][0]; pr1 = (DF)sh.ex_req[x][1]; pr2 = (DF)sh.ex_req[x][2];
+                }
+                pslot = pc_slot(hd.p, lane & 1);
+                if (lane < 6 && pslot >= 0) spre = st_stage<St>(sh, k & 1, pslot);
+            }
+        }
+        if (k >= 0 && (!KS_PR_PUB || kRole <= 1)) {
+            // the walker and the bind wave decide for themselves; the bind wave publishes the
+            // owners' part (KS_PR_PUB) so that the other waves do not repeat the decision — it
+            // runs on the scalar unit, and 10-16 waves repeating it filled each SIMD's scalar
+            // issue for ~1,200 cycles after every barrier
+            const Pc& p = hd.p;
+            const uint32_t fa = hd.w[0].w0, fb = hd.w[1].w0;
             uint64_t wbw, rest;
             bool extra;
             int32_t su;
@@ -553,17 +606,30 @@ __global__ __launch_bounds__(kThreads) void resolve_pair_kernel(const EngineArgs
             if (extra) {
                 // the candidates of pod a other than w_a refold their K1_b (kept from the last
                 // iteration) into mcx; one more barrier
-                if (mc_keep != 0 && dw_node(mc_keep) != dc.wa) fold(&sh.pc[s_cur].mcx, mc_keep);
+                if (KS_PR_PUB && kRole == 1 && lane == 0)
+                    *reinterpret_cast<volatile uint64_t*>(&sh.dec_word) = (uint64_t)(2 * k) << 32 | dec_pack(dc, true);
+                if (mc_keep != 0 && dw_ent(mc_keep) != dc.ea) fold(&sh.pc[s_cur].mcx, mc_keep);
                 PR_ACC(7, 1);
                 __syncthreads();
                 wbw = umax64(rest, sh.pc[s_cur].mcx);
             }
-            dc = finish_b(dc, wbw, fb, nt, su);
-            if (dc.stop_a) {
-                committed = pa;
-                if (dc.stop_a > 1) { err_code = dc.stop_a == 2 ? kErrNotFound : kErrEinval; err_pod = (int32_t)(start + pa); }
-                break;
+            dc = finish_b(dc, wbw, p.best, fb, nt, su);
+            if (KS_PR_PUB && kRole == 1 && lane == 0)
+                *reinterpret_cast<volatile uint64_t*>(&sh.dec_word) = (uint64_t)(2 * k + 1) << 32 | dec_pack(dc, false);
+        } else if (k >= 0) {
+            uint32_t w = dec_wait(&sh.dec_word, k, 0);
+            if (!(w >> 31)) {  // the extra fold round (phase 0 word): refold, barrier, final word
+                const Dec d0 = dec_unpack(w);
+                if (mc_keep != 0 && dw_ent(mc_keep) != d0.ea) fold(&sh.pc[s_cur].mcx, mc_keep);
+                __syncthreads();
+                w = dec_wait(&sh.dec_word, k, 1);
             }
+            dc = dec_unpack(w);
+        }
+        if (k >= 0 && dc.stop_a) {
+            committed = pa;
+            if (dc.stop_a > 1) { err_code = dc.stop_a == 2 ? kErrNotFound : kErrEinval; err_pod = (int32_t)(start + pa); }
+            break;
         }
         PR_STAMP(sd);
         PR_ACC(2, sd - s0);
@@ -571,15 +637,15 @@ __global__ __launch_bounds__(kThreads) void resolve_pair_kernel(const EngineArgs
         const bool prep = pcn < nb && (k < 0 || have_b);  // the next pair will be decided
         // window ranges: b = [lo_b, hi_b), c = [hi_b, hi_c), d = [lo_d, hi_d) — adjacent; for the
         // prologue (k = -1) only window d (pod 1's) exists
-        const PodW wpc = sh.pw[pcn], wpd = sh.pw[pd];
-        const PodW wpb = sh.pw[k >= 0 ? pb : pd];
+        const PodW wpc = hd.w[2], wpd = hd.w[3];
+        const PodW wpb = k >= 0 ? hd.w[1] : hd.w[3];
         const int lo_b = k >= 0 ? wpb.lo : wpd.lo, hi_b = k >= 0 ? wpb.hi : wpd.lo;
         const int hi_c = k >= 0 ? (have_b ? wpc.hi : hi_b) : wpd.lo;
         const int lo_d = k >= 0 ? wpc.hi : wpd.lo;
         const int hi_d = prep && pd < nb ? wpd.hi : (have_b ? hi_c : hi_b);
-        const uint64_t lbk_c = sh.pc[s_nxt].lbk_a, lbk_d = sh.pc[s_nxt].lbk_b;
+        const uint64_t lbk_c = hd.lbk_c, lbk_d = hd.lbk_d;
 
-        if (wave == 0) {
+        if constexpr (kRole == 0) {
             // ================= walker =================
             // K2 of pod c's kept candidates (lanes 0..2): admission of c, bind, c's own expiry
             // when it is due before d, then d's key
@@ -619,13 +685,10 @@ __global__ __launch_bounds__(kThreads) void resolve_pair_kernel(const EngineArgs
                 if (lane == 0) {
                     Pc& q = sh.pc[s_nxt];
                     if (uc) fold(&q.best, dword_key(uc, kUnt, k2u));
-                    q.kfull_a = (uc == 0 && full_c && pcn > 0) ? 1 : 0;
-                    q.sa = lc;
-                    q.vb1 = v1;
-                    q.vb2 = v2;
-                    q.sb1 = l1;
-                    q.sb2 = l2;
-                    q.full_b = full_d ? 1 : 0;
+                    q.fl = ((uc == 0 && full_c && pcn > 0) ? 1u : 0u) | (full_d ? 2u : 0u) | (uint32_t)(lc + 1) << 4 |
+                           (uint32_t)(l1 + 1) << 8 | (uint32_t)(l2 + 1) << 12;
+                    q.vb1 = dword_key(v1, kUnt, 0);  // decision words; entry kUnt = untouched
+                    q.vb2 = dword_key(v2, kUnt, 0);
                 }
             }
             // zero the folds of the pair after next (its slot was last read in iteration k-1)
@@ -639,7 +702,7 @@ __global__ __launch_bounds__(kThreads) void resolve_pair_kernel(const EngineArgs
             else xk = 0;
             PR_STAMP(w3);
             PR_ACC(5, w3 - w2);
-        } else if (wave == 1) {
+        } else if constexpr (kRole == 1) {
             // ================= bind wave =================
             if (k >= 0) {
                 const bool same = have_b && dc.wb == dc.wa;
@@ -651,7 +714,7 @@ __global__ __launch_bounds__(kThreads) void resolve_pair_kernel(const EngineArgs
                 const bool isnew = on_b && !same ? dc.nbw : dc.na;
                 const int slot = on_b && !same ? dc.sb : dc.sa;
                 const int64_t ja = start + pa, jb = start + pb;
-                const PodW wpa = sh.pw[pa];
+                const PodW wpa = hd.w[0];
                 // expiries of earlier-bound pods in windows b..d landing on this lane's node
                 // (own expiries of pods a, b: below), summed per window; applied ones marked
                 Dl<DF> d0{}, d1{}, d2{};
@@ -661,10 +724,14 @@ __global__ __launch_bounds__(kThreads) void resolve_pair_kernel(const EngineArgs
                     int32_t te = -1;
                     DF q0 = 0, q1 = 0, q2 = 0;
                     if (x < hi_d) {
-                        const int32_t q = sh.ex_q[x];
-                        te = sh.ex_entry[x];
-                        hit = sh.ex_ok[x] != 0 && q != ja && q != jb && (te == dc.ea || (have_b && te == dc.eb));
-                        q0 = (DF)sh.ex_req[x][0]; q1 = (DF)sh.ex_req[x][1]; q2 = (DF)sh.ex_req[x][2];
+                        int32_t q, ok;
+                        if (KS_PR_PRE && x0 == lo_b) {
+                            q = pq; te = pte; ok = pok; q0 = pr0; q1 = pr1; q2 = pr2;
+                        } else {
+                            q = sh.ex_q[x]; te = sh.ex_entry[x]; ok = sh.ex_ok[x];
+                            q0 = (DF)sh.ex_req[x][0]; q1 = (DF)sh.ex_req[x][1]; q2 = (DF)sh.ex_req[x][2];
+                        }
+                        hit = ok != 0 && q != ja && q != jb && (te == dc.ea || (have_b && te == dc.eb));
                         if (hit && x < hi_c) gptr(a.expired)[q] = 1;
                     }
                     uint64_t m = __ballot(hit);
@@ -684,7 +751,8 @@ __global__ __launch_bounds__(kThreads) void resolve_pair_kernel(const EngineArgs
                 PR_STAMP(b1);
                 PR_ACC(3, b1 - sd);
                 const int own_a = own_slot(wpa), own_b = own_slot(wpb);
-                St s = isnew ? st_stage<St>(sh, k & 1, slot < 0 ? 0 : slot) : st_entry<St>(sh, ent < 0 ? 0 : ent);
+                St s = isnew ? ((KS_PR_PRE && slot == pslot) ? spre : st_stage<St>(sh, k & 1, slot < 0 ? 0 : slot))
+                             : st_entry<St>(sh, ent < 0 ? 0 : ent);
                 bool ok_a = false, ok_b = false;
                 {
                     const PodRec p_a = pod_regs(&sh.pod[pa]);
@@ -886,16 +954,19 @@ __global__ __launch_bounds__(kThreads) void resolve_pair_kernel(const EngineArgs
             }
             if (pb + 1 >= nb) { committed = nb; break; }
         }
+        const int s_old = s_cur;
+        s_cur = s_nxt;
+        s_nxt = s_nn;
+        s_nn = s_old;
     }
-    __syncthreads();
 #ifdef KS_STAMPS
-    {   // ctr[8 + 6 * role + i]: role 0 walker (wave 0), 1 bind wave, 2 owner wave 2, 3 owner wave 7;
-        // i: 0 work, 1 barrier wait, 2 decision, 3-5 role segments; ctr[5] launches, ctr[6] pods,
-        // ctr[7] extra fold rounds
+    {   // ctr[8 + 6 * role + i] for role 0 walker, 1 bind wave (i: 0 work, 1 barrier wait, 2
+        // decision, 3-5 role segments); ctr[20 + w - 2]: work of owner wave w (2..13); ctr[5]
+        // launches, ctr[6] pods, ctr[7] extra fold rounds
         unsigned long long* d = (unsigned long long*)a.ctr;
-        const int role = wave <= 2 ? wave : (wave == 7 ? 3 : -1);
-        if (lane == 0 && role >= 0)
-            for (int q = 0; q < 6; ++q) atomicAdd(&d[8 + 6 * role + q], acc[q]);
+        if (lane == 0 && kRole <= 1)
+            for (int q = 0; q < 6; ++q) atomicAdd(&d[8 + 6 * kRole + q], acc[q]);
+        if (lane == 0 && kRole == 2 && wave <= 13) atomicAdd(&d[20 + wave - 2], acc[0]);
         if (tid == 0) {
             atomicAdd(&d[5], 1ull);
             atomicAdd(&d[6], (unsigned long long)committed);
@@ -903,8 +974,130 @@ __global__ __launch_bounds__(kThreads) void resolve_pair_kernel(const EngineArgs
         }
     }
 #endif
-    // ---- write back the mutable fields of every touched node
-    for (int e = tid; e < nt; e += kThreads) {
+    return LoopOut{nt, committed, err_code, err_pod};
+}
+
+// ---------------------------------------------------------------------------------------------
+template <int kMode>
+__global__ __launch_bounds__(kThreads) void resolve_pair_kernel(const EngineArgs* __restrict__ A) {
+    __shared__ Shared sh;
+    const EngineArgs& a = A[blockIdx.x];  // fields read where used (scalar loads): fewer live SGPRs
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid >> 6;
+    const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
+    if (a.ctr[kCtrErr] != 0) return;
+    const bool exact = a.c.n_nodes <= kFilterBits;
+    int nb = (int)min<int64_t>(min<int64_t>(a.B, kMaxB), end - start);
+    if (nb <= 0) return;
+
+    // ---- setup (as resolve_kernel): the largest batch whose expiry window fits the pre-insert
+    // budget, pods / lists / window slots into LDS, pre-insert the nodes the window's expiries
+    // land on, their records
+    const int64_t e_base = a.exp_off[start + 1];
+    const int64_t off_mid = tid < nb ? a.exp_off[start + tid + 1] : 0;
+    const bool fits_win = tid < nb && off_mid - e_base <= kMaxExp;
+    if (tid == 0) { sh.n_t = 0; sh.dec_word = ~0ull; }
+    if (tid < 3) {
+        uint4* w = reinterpret_cast<uint4*>(&sh.pc[tid]);
+        for (int q = 0; q < (int)(sizeof(Pc) / 16); ++q) w[q] = make_uint4(0, 0, 0, 0);
+    }
+    for (int h = tid; h < kHash; h += kThreads) sh.hkey[h] = -1;
+    for (int w = tid; w < kFilterBits / 32; w += kThreads) sh.tfilt[w] = 0;
+    nb = __syncthreads_count(fits_win);
+    if (tid == nb - 1) { sh.nb = nb; sh.e_cnt = nb > 1 ? (int32_t)(off_mid - e_base) : 0; }
+    __syncthreads();
+    const int e_cnt = sh.e_cnt;
+    for (int i = tid; i < kMaxB + kPodPad; i += kThreads) {
+        PodRec p{};
+        PodW w{0, 0, e_cnt, e_cnt};
+        if (i < nb) {
+            p = a.pods[start + i];
+            const int64_t pos = a.exp_pos[start + i];
+            const int32_t own = (pos >= e_base && pos - e_base < e_cnt) ? (int32_t)(pos - e_base) : -1;
+            w.w0 = p.flags | (uint32_t)(own + 1) << 2;
+            w.dur = a.dur[start + i];
+            w.lo = i >= 1 ? (int32_t)(a.exp_off[start + i] - e_base) : 0;
+            w.hi = i >= 1 ? (int32_t)(a.exp_off[start + i + 1] - e_base) : 0;
+        }
+        sh.pod[i] = p;
+        sh.podf[i][0] = (float)p.req[0];
+        sh.podf[i][1] = (float)p.req[1];
+        sh.pwx[i + 2] = w;
+    }
+    if (tid < 2) sh.pwx[tid] = PodW{0, 0, 0, 0};
+    for (int i = tid; i < nb * kL; i += kThreads) sh.cand[i / kL][i % kL] = a.cand[i];
+    for (int e = tid; e < e_cnt; e += kThreads) {
+        const int32_t q = a.exp_pod[e_base + e];
+        const PodRec& pq = a.pods[q];
+        sh.ex_q[e] = q;
+        sh.ex_entry[e] = -1;
+        sh.ex_req[e][0] = pq.req[0]; sh.ex_req[e][1] = pq.req[1]; sh.ex_req[e][2] = pq.req[2];
+        if (q < start) {
+            sh.ex_node[e] = a.b_node[q];
+            sh.ex_ok[e] = (a.b_status[q] == 0) && !a.expired[q];
+        } else {
+            sh.ex_node[e] = -1;
+            sh.ex_ok[e] = 0;  // set when the pod binds
+        }
+    }
+    __syncthreads();
+    const bool pre_want = tid < e_cnt && sh.ex_ok[tid];
+    int pre_slot = -1;
+    bool pre_claim = false;
+    if (pre_want) {
+        const int32_t nd = sh.ex_node[tid];
+        uint32_t hs = hslot(nd);
+        for (;;) {  // the table holds <= kMaxExp < kHash nodes: terminates
+            const int32_t prev = atomicCAS(&sh.hkey[hs], -1, nd);
+            if (prev == -1 || prev == nd) { pre_slot = (int)hs; pre_claim = prev == -1; break; }
+            hs = (hs + 1) & (kHash - 1);
+        }
+    }
+    __syncthreads();
+    if (pre_claim) {
+        const int32_t nd = sh.ex_node[tid];
+        const int idx = atomicAdd(&sh.n_t, 1);
+        sh.hval[pre_slot] = idx;
+        sh.tnode[idx] = nd;
+        const uint32_t f = (uint32_t)nd & (kFilterBits - 1);
+        atomicOr(&sh.tfilt[f >> 5], 1u << (f & 31));
+    }
+    __syncthreads();
+    if (pre_want) sh.ex_entry[tid] = sh.hval[pre_slot];
+    const int n_pre = sh.n_t;
+    for (int e = tid; e < kTMax; e += kThreads) sh.dirty[e] = -1;
+    for (int e = tid; e < n_pre; e += kThreads) {
+        const NodeV v = load_node(a.s, sh.tnode[e]);
+        sh.ts[0][e] = v.ac; sh.ts[1][e] = v.am; sh.ts[2][e] = v.ag; sh.ts[3][e] = v.ap;
+        sh.ts[4][e] = v.rc; sh.ts[5][e] = v.rm; sh.ts[6][e] = v.rg; sh.ts[7][e] = v.nr;
+        sh.tu[0][e] = v.taint; sh.tu[1][e] = v.label;
+    }
+
+    // ---- per-thread state, shared by the roles (a wave has one role for the whole launch):
+    // st = an owner's entry state / the walker's kept record; xk = the walker's kept key
+    // owner slot of this wave (-1: walker / bind wave).  KS_PR_SIMD fills the SIMDs the walker
+    // (wave 0, SIMD 0) and the bind wave (wave 1, SIMD 1) do not run on first: waves 2, 3, 6, 7,
+    // 10, 11, 14, 15 own slots 0-7 (512 entries), waves 4, 5, 8, 9, 12, 13 slots 8-13 — with a
+    // typical table the critical waves then have their SIMDs to themselves.
+#ifndef KS_PR_SIMD
+#define KS_PR_SIMD 0
+#endif
+    const int oslot = wave < kOwner0 ? -1
+                    : !KS_PR_SIMD ? wave - kOwner0
+                    : (wave & 3) >= 2 ? (wave >> 2) * 2 + (wave & 3) - 2 : 8 + ((wave >> 2) - 1) * 2 + (wave & 3);
+    __syncthreads();
+    // owner waves that can never own an entry end here (the table grows by <= nb entries);
+    // s_barrier waits only for the surviving waves
+    if (oslot >= 0 && oslot * kWave >= n_pre + nb) return;
+    LoopOut lo;
+    if (wave == 0) lo = pair_loop<kMode, 0>(a, sh, tid, lane, wave, nb, n_pre, exact, start, oslot);
+    else if (wave == 1) lo = pair_loop<kMode, 1>(a, sh, tid, lane, wave, nb, n_pre, exact, start, oslot);
+    else lo = pair_loop<kMode, 2>(a, sh, tid, lane, wave, nb, n_pre, exact, start, oslot);
+    const int nt = lo.nt, committed = lo.committed, err_code = lo.err_code, err_pod = lo.err_pod;
+    __syncthreads();
+    // ---- write back the mutable fields of every touched node (by each entry's owner lane: with
+    // KS_PR_SIMD the waves that ended early may hold low thread ids)
+    const int r_own = oslot >= 0 ? oslot * kWave + lane : kTMax;
+    for (int e = KS_PR_SIMD ? r_own : tid; e < nt; e += KS_PR_SIMD ? kTMax : kThreads) {
         const int64_t ndx = sh.tnode[e];
         a.s.rc[ndx] = sh.ts[4][e];
         a.s.rm[ndx] = sh.ts[5][e];

@@ -1,7 +1,8 @@
 """Diagnostic: pair-resolver phase breakdown (s_memtime stamps build, `make stamps`) on the C3
 bench workload.  Layout (ks_pair.hip, KS_STAMPS): ctr[8 + 6 * role + i], role 0 walker (wave 0),
 1 bind wave (wave 1), 2 owner wave 2, 3 owner wave 7; i 0 work, 1 barrier wait, 2 decision,
-3-5 role segments; ctr[5] launches, ctr[6] pods committed, ctr[7] extra fold rounds."""
+3-5 role segments (walker, bind wave); ctr[20..31] work of owner waves 2..13; ctr[5] launches,
+ctr[6] pods committed, ctr[7] extra fold rounds."""
 import os, sys, time
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -24,12 +25,13 @@ d = eng.debug_counters() - c0
 pods, L = max(d[6], 1), max(d[5], 1)
 pairs = pods / 2
 print(f"pods={pods} launches={L} ({pods / L:.1f} pods/launch) wall {dt * 1e3:.1f} ms -> {32768 / dt:.0f} pods/s")
-seg = {0: ("K2 of c", "stage + fold", "walk"), 1: ("expiry scan", "fetch + binds", "eval + fold"),
-       2: ("reload + expiries", "prune", "evals + folds"), 3: ("reload + expiries", "prune", "evals + folds")}
-for role, name in ((0, "walker"), (1, "bind wave"), (2, "owner wave 2"), (3, "owner wave 7")):
+seg = {0: ("K2 of c", "stage + fold", "walk"), 1: ("expiry scan", "fetch + binds", "eval + fold")}
+for role, name in ((0, "walker"), (1, "bind wave")):
     b = 8 + 6 * role
     print(f"{name:13s} work {d[b] / pairs:7.0f}  wait {d[b + 1] / pairs:6.0f}  decision {d[b + 2] / pairs:5.0f}  " +
           "  ".join(f"{seg[role][i]} {d[b + 3 + i] / pairs:5.0f}" for i in range(3)) + "  cycles/pair")
+print("owner waves 2..13 work (cycles/pair, 0 = ended early): " +
+      " ".join(f"{d[20 + w] / pairs:.0f}" for w in range(12)))
 print(f"extra fold rounds: {d[7] / L:.2f} per launch ({d[7] / pairs * 100:.2f} % of pairs)")
 nl = max(st["launches"], 1)
 print(f"resolve {st['resolve_ms'] / nl * 1e3:.1f} us/launch, scan {st['scan_ms'] / nl * 1e3:.1f}, other {st['other_ms'] / nl * 1e3:.1f}; "
