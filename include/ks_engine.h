@@ -98,10 +98,11 @@ typedef struct {
  * one, NO_TINY skips tiny and micro, NO_MICRO skips micro; all are exact, the flags exist to test
  * them against each other. */
 enum { KS_ENGINE_FORCE_WIDE = 1, KS_ENGINE_NO_TINY = 2, KS_ENGINE_NO_MICRO = 4,
-       /* resolvers: batches of clusters above the small class go to the pair resolver (two
-        * pods per barrier) when every total + 1 < 2^15; ONE_POD_RESOLVER keeps the role-split
-        * one-pod resolver instead (same binds — the flag exists to test them against each other) */
-       KS_ENGINE_ONE_POD_RESOLVER = 8 };
+       /* resolvers for batches of clusters above the small class (all give the same binds; the
+        * flags exist to test them against each other): ONE_POD = the role-split one-pod-per-
+        * barrier resolver; PAIR = two pods per barrier (when every total + 1 < 2^15); SWEEP =
+        * parallel Jacobi sweeps to the sequential fixed point (ks_step only, not groups) */
+       KS_ENGINE_ONE_POD_RESOLVER = 8, KS_ENGINE_PAIR_RESOLVER = 16, KS_ENGINE_SWEEP_RESOLVER = 32 };
 
 typedef struct {
     int64_t pod;    /* FIFO index (submission order) */

@@ -544,6 +544,28 @@ enum : int64_t { kCtrStart = 0, kCtrEnd = 1, kCtrErr = 2, kCtrErrPod = 3, kCtrEa
 enum : uint32_t { kFlagBadKey = 1, kFlagBadSpec = 2 };
 enum : int64_t { kErrEinval = 1, kErrNotFound = 2 };
 
+// Workspace of the sweep resolver (ks_sweep.hip), one per engine, in HBM.  Sized for batches of
+// up to kSweepMaxB pods whose expiry window holds up to kSweepMaxSlots slots.
+constexpr int kSweepMaxB = 256;
+constexpr int kSweepMaxSlots = 1024;
+constexpr int kSweepMaxSweeps = 24;
+struct SweepWS {
+    int32_t nb, e_cnt, n_e, pad_;
+    int32_t win_hi[kSweepMaxB];           // pod i: expiry slots < win_hi[i] are applied before it binds
+    int32_t own[kSweepMaxB];              // pod i's own expiry slot in the window, or -1
+    int32_t w[2][kSweepMaxB];             // winners of the last two sweeps (node, -1 none)
+    int32_t code[2][kSweepMaxB];          // 0 ok, 1 list exhausted, 2 NotFound, 3 bad pod key / spec
+    int32_t fc[kSweepMaxSweeps];          // sweep s: first pod whose result changed (INT32_MAX: none)
+    int32_t fs[kSweepMaxSweeps];          // sweep s: first pod with a stop code (INT32_MAX: none)
+    int32_t ran[kSweepMaxSweeps];         // sweep s executed
+    int32_t ex_q[kSweepMaxSlots];         // slot -> expiring pod
+    int32_t ex_ok[kSweepMaxSlots];        // pre-batch pod bound Ok and not expired yet
+    int64_t ex_req[kSweepMaxSlots][3];
+    int32_t e_node[kSweepMaxSlots];       // distinct nodes of the pre-batch expiries (E)
+    int32_t e_off[kSweepMaxSlots + 1];    // E node k's slots: e_slot[e_off[k] .. e_off[k+1]) ascending
+    int32_t e_slot[kSweepMaxSlots];
+};
+
 // Arguments of the batch kernels (expire_head / scan / resolve).
 struct EngineArgs {
     Cfg c;
@@ -564,6 +586,8 @@ struct EngineArgs {
     int32_t nblk;            // 256-node scan blocks (whole cluster; the lists' stride)
     int32_t blk_lo;          // this rank's scan range [blk_lo, blk_lo + blk_n) (node sharding)
     int32_t blk_n;
+    SweepWS* sw;             // sweep resolver workspace (nullptr unless allocated)
+    int32_t* e_idx;          // [n_pad] node -> index in the sweep's E, -1 otherwise
 };
 
 // Launchers and limits (defined in ks_kernels.hip).  The batch launchers take a device array of
@@ -593,6 +617,10 @@ int small_resolver_max_nodes();
 // pods, any cluster, when every total + 1 < 2^15 (its decision words carry a second total)
 hipError_t launch_resolve_pair(const EngineArgs* d, int S, int mode, hipStream_t st);
 int pair_resolver_max_batch();
+// the sweep resolver (ks_sweep.hip): parallel Jacobi sweeps to the sequential fixed point, one
+// engine (S = 1), batches of <= kSweepMaxB pods; `sweeps` kernels are queued, the ones after
+// convergence exit at once
+hipError_t launch_resolve_sweep(const EngineArgs* d, int mode, int sweeps, hipStream_t st);
 constexpr int64_t kPairTotalCap = 1LL << 15;
 struct BindSeg {
     const int32_t* node;

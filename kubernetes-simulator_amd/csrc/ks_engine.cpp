@@ -175,6 +175,9 @@ struct ks_engine {
     // scratch for queries
     uint8_t* d_mask = nullptr;
     int64_t* d_score = nullptr;
+    ks::SweepWS* d_sweep = nullptr;  // sweep resolver workspace and node -> E index (n_pad, -1)
+    int32_t* d_eidx = nullptr;
+    int sweeps = 12;                 // sweep kernels queued per batch (KS_SWEEPS overrides)
     unsigned long long* d_usage = nullptr;
     DVec<int32_t> d_blk;                  // usage query: candidate pod blocks
     std::vector<int32_t> h_blk;
@@ -230,6 +233,8 @@ ks::EngineArgs make_args(ks_engine* e) {
     a.ctr = e->d_ctr;
     a.B = e->B;
     a.PG = e->PG;
+    a.sw = e->d_sweep;
+    a.e_idx = e->d_eidx;
     return a;
 }
 
@@ -251,17 +256,27 @@ bool small_resolver(const ks_engine* e) {
 // second total, so it takes engines whose totals + 1 stay below 2^15 (weights and constant
 // values are >= 0).
 bool pair_resolver(const ks_engine* e) {
-    return !(e->flags & KS_ENGINE_ONE_POD_RESOLVER) &&
+    return (e->flags & KS_ENGINE_PAIR_RESOLVER) &&
            (int64_t)e->dc.const_total + 10 * ((int64_t)e->dc.w_lr + e->dc.w_ba) + 1 < ks::kPairTotalCap;
 }
-enum Resolver { kResolveRole = 0, kResolveSmall = 1, kResolvePair = 2 };
-int resolver_of(const ks_engine* e) {
-    return small_resolver(e) ? kResolveSmall : pair_resolver(e) ? kResolvePair : kResolveRole;
+// the sweep resolver (ks_sweep.hip): one engine per launch, batches of <= kSweepMaxB pods
+bool sweep_resolver(const ks_engine* e) {
+    return (e->flags & KS_ENGINE_SWEEP_RESOLVER) && e->B <= ks::kSweepMaxB;
 }
-hipError_t launch_resolver(const ks::EngineArgs* d, int S, int mode, int which, hipStream_t st) {
+enum Resolver { kResolveRole = 0, kResolveSmall = 1, kResolvePair = 2, kResolveSweep = 3 };
+// an explicit resolver flag wins over the size class (every resolver is exact on every engine
+// its limits admit; the flags exist to test them against each other)
+int resolver_of(const ks_engine* e) {
+    if (sweep_resolver(e)) return kResolveSweep;
+    if (pair_resolver(e)) return kResolvePair;
+    if (e->flags & KS_ENGINE_ONE_POD_RESOLVER) return kResolveRole;
+    return small_resolver(e) ? kResolveSmall : kResolveRole;
+}
+hipError_t launch_resolver(const ks::EngineArgs* d, int S, int mode, int which, hipStream_t st, int sweeps = 0) {
     return which == kResolveSmall ? ks::launch_resolve_small(d, S, mode, st)
          : which == kResolvePair ? ks::launch_resolve_pair(d, S, mode, st)
-                                 : ks::launch_resolve(d, S, mode, st);
+         : which == kResolveSweep ? ks::launch_resolve_sweep(d, mode, sweeps, st)
+                                  : ks::launch_resolve(d, S, mode, st);
 }
 void update_mode(ks_engine* e) {
     int64_t m[3];
@@ -298,7 +313,8 @@ ks_status engine_init(const ks_config* cfg, ks_engine** out) {
     if (cfg->n_scorers < 0 || cfg->n_scorers > 8) return KS_EINVAL;
     if (cfg->batch_pods < 0 || cfg->batch_pods > kMaxBatch) return KS_EINVAL;
     if (cfg->engine_flags &
-        ~(uint32_t)(KS_ENGINE_FORCE_WIDE | KS_ENGINE_NO_TINY | KS_ENGINE_NO_MICRO | KS_ENGINE_ONE_POD_RESOLVER))
+        ~(uint32_t)(KS_ENGINE_FORCE_WIDE | KS_ENGINE_NO_TINY | KS_ENGINE_NO_MICRO | KS_ENGINE_ONE_POD_RESOLVER |
+                    KS_ENGINE_PAIR_RESOLVER | KS_ENGINE_SWEEP_RESOLVER))
         return KS_EINVAL;
     int64_t const_total = 0, w_lr = 0, w_ba = 0;
     for (int i = 0; i < cfg->n_scorers; i++) {
@@ -382,6 +398,8 @@ void engine_free(ks_engine* e) {
     }
     if (e->d_mask) (void)hipFree(e->d_mask);
     if (e->d_score) (void)hipFree(e->d_score);
+    if (e->d_sweep) (void)hipFree(e->d_sweep);
+    if (e->d_eidx) (void)hipFree(e->d_eidx);
     if (e->d_usage) (void)hipFree(e->d_usage);
     for (auto ev : e->ev) if (ev) (void)hipEventDestroy(ev);
     for (auto ev : e->prof_ev) (void)hipEventDestroy(ev);
@@ -526,6 +544,10 @@ ks_status ks_load_nodes(ks_engine* e, int64_t n, const int64_t* alloc, const uin
     if (G > 1) HIPCHK(e, hipMalloc(&e->cand_all, sizeof(uint64_t) * (size_t)G * e->B * ks::kTopL));
     HIPCHK(e, hipMalloc(&e->d_mask, std::max<int64_t>(n, 1)));
     HIPCHK(e, hipMalloc(&e->d_score, sizeof(int64_t) * std::max<int64_t>(n, 1)));
+    if (const char* v = std::getenv("KS_SWEEPS")) e->sweeps = std::max(2, std::min(ks::kSweepMaxSweeps, std::atoi(v)));
+    HIPCHK(e, hipMalloc(&e->d_sweep, sizeof(ks::SweepWS)));
+    HIPCHK(e, hipMalloc(&e->d_eidx, sizeof(int32_t) * e->n_pad));
+    HIPCHK(e, hipMemsetAsync(e->d_eidx, 0xFF, sizeof(int32_t) * e->n_pad, e->st));
     HIPCHK(e, hipMalloc(&e->d_usage, sizeof(unsigned long long) * 3 * std::max<int64_t>(n, 1)));
     HIPCHK(e, hipStreamSynchronize(e->st));
     e->nodes_loaded = true;
@@ -862,7 +884,7 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
                 HIPCHK(e, ks::launch_merge(d, 1, e->B, e->cand_all, L, G, BL, e->cand, G, st));
             }
             if (ev[3]) HIPCHK(e, hipEventRecord(ev[3], st));
-            HIPCHK(e, launch_resolver(d, 1, e->mode, resolver_of(e), st));
+            HIPCHK(e, launch_resolver(d, 1, e->mode, resolver_of(e), st, e->sweeps));
             if (ev[4]) HIPCHK(e, hipEventRecord(ev[4], st));
             launches++;
         }
@@ -1027,7 +1049,7 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
         B = std::max(B, e->B);
         k16 = k16 && key16(e);
         small = small && small_resolver(e);
-        pair = pair && pair_resolver(e);
+        pair = pair && pair_resolver(e);  // (no sweep resolver in groups: it takes one engine)
     }
     const int which = small ? kResolveSmall : pair ? kResolvePair : kResolveRole;
     int64_t blocks = 0;

@@ -399,6 +399,11 @@ __device__ __forceinline__ Dec finish_b(Dec d, uint64_t wbw, uint64_t best, uint
 #ifndef KS_PR_PRE
 #define KS_PR_PRE 0
 #endif
+// KS_PR_LATE: owners do their decision-independent work (window deltas, prune, evaluations,
+// assuming both pods bind) before they wait for the bind wave's decision word, then commit
+#ifndef KS_PR_LATE
+#define KS_PR_LATE 0
+#endif
 __device__ __forceinline__ uint32_t dec_pack(const Dec& d, bool extra) {
     return (uint32_t)(d.ea + 1) | (uint32_t)(d.eb + 1) << 10 | (uint32_t)(d.na + d.nbw) << 20 |
            (uint32_t)d.stop_a << 22 | (uint32_t)d.stop_b << 25 | (extra ? 1u << 28 : 0u);
@@ -490,6 +495,10 @@ struct Dl {
 template <class T, class F>
 __device__ __forceinline__ void sub_dl(T& s, const Dl<F>& d) {
     s.rc -= d.c; s.rm -= d.m; s.rg -= d.g; s.nr -= d.n;
+}
+template <class T, class F>
+__device__ __forceinline__ void add_dl(T& s, const Dl<F>& d) {
+    s.rc += d.c; s.rm += d.m; s.rg += d.g; s.nr += d.n;
 }
 // the pod's own expiry slot within the batch window, or -1
 __device__ __forceinline__ int own_slot(const PodW& w) { return (int)(w.w0 >> 2) - 1; }
@@ -616,7 +625,7 @@ __device__ __forceinline__ LoopOut pair_loop(const EngineArgs& a, Shared& sh, co
             dc = finish_b(dc, wbw, p.best, fb, nt, su);
             if (KS_PR_PUB && kRole == 1 && lane == 0)
                 *reinterpret_cast<volatile uint64_t*>(&sh.dec_word) = (uint64_t)(2 * k + 1) << 32 | dec_pack(dc, false);
-        } else if (k >= 0) {
+        } else if (k >= 0 && !(kRole == 2 && KS_PR_LATE)) {
             uint32_t w = dec_wait(&sh.dec_word, k, 0);
             if (!(w >> 31)) {  // the extra fold round (phase 0 word): refold, barrier, final word
                 const Dec d0 = dec_unpack(w);
@@ -633,8 +642,8 @@ __device__ __forceinline__ LoopOut pair_loop(const EngineArgs& a, Shared& sh, co
         }
         PR_STAMP(sd);
         PR_ACC(2, sd - s0);
-        const bool have_b = k >= 0 && dc.stop_b == 0;
-        const bool prep = pcn < nb && (k < 0 || have_b);  // the next pair will be decided
+        bool have_b = k >= 0 && dc.stop_b == 0;
+        bool prep = pcn < nb && (k < 0 || have_b);  // the next pair will be decided
         // window ranges: b = [lo_b, hi_b), c = [hi_b, hi_c), d = [lo_d, hi_d) — adjacent; for the
         // prologue (k = -1) only window d (pod 1's) exists
         const PodW wpc = hd.w[2], wpd = hd.w[3];
@@ -843,6 +852,136 @@ __device__ __forceinline__ LoopOut pair_loop(const EngineArgs& a, Shared& sh, co
             }
         } else {
             // ================= owners =================
+#if KS_PR_LATE
+            // ---- speculative part (pods a and b both bind; otherwise the loop ends at this
+            // iteration and nothing of it is kept but what the commit below writes)
+            const int base = oslot * kWave;
+            if (r < nt) {
+                if (!loaded) {
+                    st = st_entry<St>(sh, r);
+                    st_node = sh.tnode[r];
+                    loaded = true;
+                    pf_stale = true;
+                } else if (sh.dirty[r] == k) {
+                    st_reload(sh, r, st);
+                    pf_stale = true;
+                }
+            }
+            const bool s_prep = pcn < nb;
+            const int s_hi_b = k >= 0 ? wpb.hi : wpd.lo;
+            const int s_hi_c = k >= 0 ? wpc.hi : wpd.lo;
+            const int s_hi_d = s_prep && pd < nb ? wpd.hi : s_hi_c;
+            Dl<DF> dwb{}, dwc{}, dd{};
+            bool has_b = false, has_c = false, has_dd = false, any_hit = false;
+            for (int x0 = lo_b; x0 < s_hi_d; x0 += kWave) {
+                const int x = x0 + lane;
+                int32_t te = -1;
+                bool hit = false;
+                if (x < s_hi_d) {
+                    te = sh.ex_entry[x];
+                    hit = sh.ex_ok[x] != 0 && te >= base && te < base + kWave;
+                }
+                uint64_t m = __ballot(hit);
+                any_hit |= m != 0;
+                while (m) {
+                    const int l = __ffsll((unsigned long long)m) - 1;
+                    m &= m - 1;
+                    const int xl = x0 + l;
+                    const int el = __builtin_amdgcn_readlane(te, l);
+                    if (r == el) {
+                        const DF q0 = (DF)sh.ex_req[xl][0], q1 = (DF)sh.ex_req[xl][1], q2 = (DF)sh.ex_req[xl][2];
+                        const int wsel = xl < s_hi_b ? 0 : (xl < s_hi_c ? 1 : 2);
+                        dwb.c += wsel == 0 ? q0 : 0; dwb.m += wsel == 0 ? q1 : 0; dwb.g += wsel == 0 ? q2 : 0; dwb.n += wsel == 0;
+                        dwc.c += wsel == 1 ? q0 : 0; dwc.m += wsel == 1 ? q1 : 0; dwc.g += wsel == 1 ? q2 : 0; dwc.n += wsel == 1;
+                        dd.c += wsel == 2 ? q0 : 0; dd.m += wsel == 2 ? q1 : 0; dd.g += wsel == 2 ? q2 : 0; dd.n += wsel == 2;
+                        has_b |= wsel == 0; has_c |= wsel == 1; has_dd |= wsel == 2;
+                    }
+                }
+            }
+            St sbc = st;  // the entry's state before pod c (windows b and c applied)
+            sub_dl(sbc, dwb);
+            sub_dl(sbc, dwc);
+            PR_STAMP(o1);
+            PR_ACC(3, o1 - sd);
+            bool pass_c = false, pass_d = false;
+            if (s_prep && r < nt) {
+                if (pf_stale || has_b || has_c) { pf = prune_prep_t<kMode>(a.c, sbc); pf_stale = has_b || has_c; }
+                const float qc0 = sh.podf[pcn][0], qc1 = sh.podf[pcn][1];
+                pass_c = pf.live && make_key(prune_tmax(a.c, pf, qc0, qc1) + 1u, (uint32_t)st_node) >= lbk_c;
+                if (pd < nb) {
+                    const float qd0 = sh.podf[pd][0], qd1 = sh.podf[pd][1];
+                    pass_d = has_dd ||
+                             (pf.live && make_key(prune_tmax(a.c, pf, qd0, qd1) + 1u, (uint32_t)st_node) >= lbk_d);
+                }
+            }
+            PR_STAMP(o2);
+            PR_ACC(4, o2 - o1);
+            uint64_t kc = 0, k1 = 0;
+            uint32_t t2 = 0;
+            if (__ballot(pass_c || pass_d)) {
+                St s1 = sbc;
+                sub_dl(s1, dd);
+                const PodRec p_c = pod_regs(&sh.pod[pcn]);
+                const PodRec p_d = pod_regs(&sh.pod[pd]);
+                const uint32_t tc = eval_t<kMode>(a.c, p_c, sbc);
+                const uint32_t t1 = eval_t<kMode>(a.c, p_d, s1);
+                kc = pass_c ? make_key(tc, (uint32_t)st_node) : 0ull;
+                k1 = pass_d ? make_key(t1, (uint32_t)st_node) : 0ull;
+                if (__ballot(kc != 0 && kc >= lbk_c) && pd < nb) {
+                    St s2 = s1;
+                    const int oc = own_slot(wpc);
+                    const bool okc = fits_t(p_c, sbc);
+                    if (okc && wpc.dur > 0) add_t(s2, p_c, 1);
+                    if (okc && oc >= s_hi_c && oc < s_hi_d) add_t(s2, p_c, -1);
+                    t2 = eval_t<kMode>(a.c, p_d, s2);
+                }
+            }
+            PR_STAMP(o3);
+            PR_ACC(5, o3 - o2);
+            // ---- the decision (the bind wave's word), then the commit
+            if (k >= 0) {
+                uint32_t w = dec_wait(&sh.dec_word, k, 0);
+                if (!(w >> 31)) {
+                    const Dec d0 = dec_unpack(w);
+                    if (mc_keep != 0 && dw_ent(mc_keep) != d0.ea) fold(&sh.pc[s_cur].mcx, mc_keep);
+                    __syncthreads();
+                    w = dec_wait(&sh.dec_word, k, 1);
+                }
+                dc = dec_unpack(w);
+                if (dc.stop_a) break;  // the walker holds committed / err for the launch
+                have_b = dc.stop_b == 0;
+                prep = pcn < nb && have_b;
+            }
+            const bool valid = r < nt && r != dc.ea && r != dc.eb;
+            // applied windows: b when pod a binds, c when pod b binds too
+            if (valid && (has_b || (have_b && has_c))) {
+                st = sbc;
+                if (!have_b) add_dl(st, dwc);
+                st_store(sh, r, st);
+                pf_stale = true;
+            }
+            if (any_hit) {  // mark the applied expiries (windows b, c) of this wave's valid entries
+                const int hc = have_b ? s_hi_c : s_hi_b;
+                for (int x0 = lo_b; x0 < hc; x0 += kWave) {
+                    const int x = x0 + lane;
+                    if (x < hc && sh.ex_ok[x] != 0) {
+                        const int32_t te = sh.ex_entry[x];
+                        if (te >= base && te < base + kWave && te < nt && te != dc.ea && te != dc.eb)
+                            gptr(a.expired)[sh.ex_q[x]] = 1;
+                    }
+                }
+            }
+            mc_keep = 0;
+            if (prep && valid) {
+                const bool cand = kc != 0 && kc >= lbk_c;
+                if (cand) fold(&sh.pc[s_nxt].best, dword_key(kc, (uint32_t)r, t2));
+                if (k1 != 0 && k1 >= lbk_d) {
+                    const uint64_t w1 = dword_key(k1, (uint32_t)r, 0);
+                    if (cand) { fold(&sh.pc[s_nxt].mc, w1); mc_keep = w1; }
+                    else fold(&sh.pc[s_nxt].m2, w1);
+                }
+            }
+#else
             const int base = oslot * kWave;
             const bool valid = r < nt && r != dc.ea && r != dc.eb;
             if (r < nt) {
@@ -936,6 +1075,7 @@ __device__ __forceinline__ LoopOut pair_loop(const EngineArgs& a, Shared& sh, co
             }
             PR_STAMP(o3);
             PR_ACC(5, o3 - o2);
+#endif
         }
         PR_STAMP(s1);
         __syncthreads();

@@ -1,0 +1,81 @@
+"""Every resolver against the oracle (kubesim/kubesim.go:90-225 restated in oracle/ks_oracle.c).
+
+The engine has four exact resolvers for step 4 of a batch: the role-split one-pod
+kernel, the register-table kernel (small clusters), the pair kernel (two pods per barrier) and
+the sweep kernel (parallel Jacobi sweeps to the sequential fixed point).  The engine picks one
+by size class; the KS_ENGINE_*_RESOLVER flags force one, and each forced resolver must give the
+oracle's binds, statuses and usage on every case below — all filter / scorer modes, batch sizes
+from 3 to 256, dense in-batch expiries, forced list exhaustion, and a C2 prefix.
+"""
+import numpy as np
+import pytest
+
+from harness import MODES, assert_same_binds, encoded, engine_run, make_engine, make_oracle, oracle_run, small_trace
+from kubesim_amd import _lib, tracegen
+
+pytestmark = pytest.mark.gpu
+RESOLVERS = {"one_pod": _lib.KS_ENGINE_ONE_POD_RESOLVER, "pair": _lib.KS_ENGINE_PAIR_RESOLVER,
+             "sweep": _lib.KS_ENGINE_SWEEP_RESOLVER}
+
+
+def _run(tr, mode, ticks, batch, flags, chunks):
+    enc = encoded(tr)
+    eng = make_engine(tr, enc, mode, batch, flags)
+    eng.submit(enc["pods"])
+    ora = make_oracle(tr, mode)
+    ora.submit(tr)
+    left = ticks
+    for c in chunks:
+        k = min(c, left)
+        if k <= 0:
+            break
+        eb, erc = engine_run(eng, k, k)
+        ob, orc = oracle_run(ora, k)
+        assert_same_binds(eb, ob)
+        assert erc == orc, (erc, orc)
+        left -= k
+        if erc:
+            return eng
+        np.testing.assert_array_equal(eng.usage(), ora.usage())
+    return eng
+
+
+@pytest.mark.parametrize("res", sorted(RESOLVERS))
+@pytest.mark.parametrize("mode", sorted(MODES))
+def test_modes(res, mode):
+    tr = small_trace(1, n_nodes=400, n_pods=600, arrival="stream")
+    _run(tr, mode, 800, 256, RESOLVERS[res], (1, 7, 100, 692))
+
+
+@pytest.mark.parametrize("res", sorted(RESOLVERS))
+@pytest.mark.parametrize("batch", [3, 64, 256])
+def test_batches(res, batch):
+    tr = small_trace(7, n_nodes=300, n_pods=2500, taints=False, selectors=False)
+    _run(tr, "literal_lrba_filters_ignored", 2500, batch, RESOLVERS[res], (1, 17, 500, 1982))
+
+
+@pytest.mark.parametrize("res", sorted(RESOLVERS))
+def test_dense_expiries(res):
+    tr = small_trace(11, n_nodes=2000, n_pods=6000, taints=False, selectors=False, tolerations=False)
+    p = tr["pods"]
+    p["phase_sec"][:] = 1 + (np.arange(len(p["phase_sec"])) % 12)
+    _run(tr, "feeds_all_lrba", 6000, 256, RESOLVERS[res], (1500,) * 4)
+
+
+@pytest.mark.parametrize("res", sorted(RESOLVERS))
+def test_list_exhaustion(res):
+    tr = small_trace(21, n_nodes=300, n_pods=900, taints=False, labels=False, tolerations=False,
+                     selectors=False)
+    nd, p = tr["nodes"], tr["pods"]
+    p["req"][:] = p["req"][0]
+    nd["alloc"][:, :3] = 4 * p["req"][0]
+    nd["alloc"][:, 3] = 110
+    nd["alloc_has"][:] = 15
+    _run(tr, "feeds_fit_lr", 900, 256, RESOLVERS[res], (900,))
+
+
+@pytest.mark.parametrize("res", sorted(RESOLVERS))
+@pytest.mark.parametrize("mode", ["feeds_all_lrba", "literal_lrba_filters_ignored"])
+def test_c2_prefix(res, mode):
+    tr = tracegen.c2_trace(n_pods=12_000)
+    _run(tr, mode, 12_000, 0, RESOLVERS[res], (4096, 7904))
