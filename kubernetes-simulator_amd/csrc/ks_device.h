@@ -549,6 +549,10 @@ enum : int64_t { kErrEinval = 1, kErrNotFound = 2 };
 constexpr int kSweepMaxB = 256;
 constexpr int kSweepMaxSlots = 1024;
 constexpr int kSweepMaxSweeps = 24;
+// chunk resolver (ks_chunk.hip): candidate lists of kChR entries per pod, windows of <= kChSlots
+constexpr int kChR = 24;
+constexpr int kChSlots = 512;
+enum : int32_t { kClTrunc = 1 << 8, kClFull = 1 << 9, kClOvf = 1 << 10 };
 struct SweepWS {
     int32_t nb, e_cnt, n_e, pad_;
     int32_t win_hi[kSweepMaxB];           // pod i: expiry slots < win_hi[i] are applied before it binds
@@ -564,6 +568,10 @@ struct SweepWS {
     int32_t e_node[kSweepMaxSlots];       // distinct nodes of the pre-batch expiries (E)
     int32_t e_off[kSweepMaxSlots + 1];    // E node k's slots: e_slot[e_off[k] .. e_off[k+1]) ascending
     int32_t e_slot[kSweepMaxSlots];
+    // chunk resolver: pod i's static candidates (chunk_cl_kernel), sorted descending
+    uint64_t cl_key[kSweepMaxB][kChR];
+    int32_t cl_info[kSweepMaxB];          // kept count | kClTrunc | kClFull | kClOvf
+    uint64_t cl_thr[kSweepMaxB];          // the list's last key when full, else 1
 };
 
 // Arguments of the batch kernels (expire_head / scan / resolve).
@@ -621,6 +629,9 @@ int pair_resolver_max_batch();
 // engine (S = 1), batches of <= kSweepMaxB pods; `sweeps` kernels are queued, the ones after
 // convergence exit at once
 hipError_t launch_resolve_sweep(const EngineArgs* d, int mode, int sweeps, hipStream_t st);
+// the chunk resolver (ks_chunk.hip): one engine (S = 1), batches of <= kSweepMaxB pods, evaluator
+// modes >= kEvalNarrow (node state in int32) and every total + 1 < 2^16
+hipError_t launch_resolve_chunk(const EngineArgs* d, int mode, hipStream_t st);
 constexpr int64_t kPairTotalCap = 1LL << 15;
 struct BindSeg {
     const int32_t* node;

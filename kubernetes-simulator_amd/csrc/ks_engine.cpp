@@ -263,10 +263,16 @@ bool pair_resolver(const ks_engine* e) {
 bool sweep_resolver(const ks_engine* e) {
     return (e->flags & KS_ENGINE_SWEEP_RESOLVER) && e->B <= ks::kSweepMaxB;
 }
-enum Resolver { kResolveRole = 0, kResolveSmall = 1, kResolvePair = 2, kResolveSweep = 3 };
+// the chunk resolver (ks_chunk.hip): one engine per launch, batches of <= kSweepMaxB pods, node
+// state in int32 (evaluator modes >= narrow), totals in 16 bits
+bool chunk_resolver(const ks_engine* e) {
+    return (e->flags & KS_ENGINE_CHUNK_RESOLVER) && e->B <= ks::kSweepMaxB && e->mode >= ks::kEvalNarrow && key16(e);
+}
+enum Resolver { kResolveRole = 0, kResolveSmall = 1, kResolvePair = 2, kResolveSweep = 3, kResolveChunk = 4 };
 // an explicit resolver flag wins over the size class (every resolver is exact on every engine
 // its limits admit; the flags exist to test them against each other)
 int resolver_of(const ks_engine* e) {
+    if (chunk_resolver(e)) return kResolveChunk;
     if (sweep_resolver(e)) return kResolveSweep;
     if (pair_resolver(e)) return kResolvePair;
     if (e->flags & KS_ENGINE_ONE_POD_RESOLVER) return kResolveRole;
@@ -276,6 +282,7 @@ hipError_t launch_resolver(const ks::EngineArgs* d, int S, int mode, int which, 
     return which == kResolveSmall ? ks::launch_resolve_small(d, S, mode, st)
          : which == kResolvePair ? ks::launch_resolve_pair(d, S, mode, st)
          : which == kResolveSweep ? ks::launch_resolve_sweep(d, mode, sweeps, st)
+         : which == kResolveChunk ? ks::launch_resolve_chunk(d, mode, st)
                                   : ks::launch_resolve(d, S, mode, st);
 }
 void update_mode(ks_engine* e) {
@@ -314,7 +321,7 @@ ks_status engine_init(const ks_config* cfg, ks_engine** out) {
     if (cfg->batch_pods < 0 || cfg->batch_pods > kMaxBatch) return KS_EINVAL;
     if (cfg->engine_flags &
         ~(uint32_t)(KS_ENGINE_FORCE_WIDE | KS_ENGINE_NO_TINY | KS_ENGINE_NO_MICRO | KS_ENGINE_ONE_POD_RESOLVER |
-                    KS_ENGINE_PAIR_RESOLVER | KS_ENGINE_SWEEP_RESOLVER))
+                    KS_ENGINE_PAIR_RESOLVER | KS_ENGINE_SWEEP_RESOLVER | KS_ENGINE_CHUNK_RESOLVER))
         return KS_EINVAL;
     int64_t const_total = 0, w_lr = 0, w_ba = 0;
     for (int i = 0; i < cfg->n_scorers; i++) {

@@ -102,7 +102,7 @@ __device__ int replay(const EngineArgs& a, const SweepWS& ws, int32_t n, int e_i
 }
 
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kPrepThreads) void sweep_prep_kernel(const EngineArgs* __restrict__ A) {
+__global__ __launch_bounds__(kPrepThreads) void sweep_prep_kernel(const EngineArgs* __restrict__ A, int max_slots) {
     const EngineArgs& a = A[0];
     SweepWS& ws = *a.sw;
     const int tid = threadIdx.x;
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(kPrepThreads) void sweep_prep_kernel(const EngineAr
         return;
     }
     const int64_t e_base = a.exp_off[start + 1];
-    const bool fits_win = tid < nb && a.exp_off[start + tid + 1] - e_base <= kSweepMaxSlots;
+    const bool fits_win = tid < nb && a.exp_off[start + tid + 1] - e_base <= max_slots;
     for (int h = tid; h < kEHash; h += kPrepThreads) hk[h] = -1;
     if (tid == 0) s_ne = 0;
     nb = __syncthreads_count(fits_win);  // exp_off is non-decreasing: a prefix of the pods
@@ -409,7 +409,7 @@ hipError_t launch_resolve_sweep(const EngineArgs* d, int mode, int sweeps, hipSt
     // at least two sweeps: sweep 0 starts from "no binds", so only from sweep 1 on is a prefix
     // (pod 0 at least) stable and committable
     sweeps = sweeps < 2 ? 2 : (sweeps > kSweepMaxSweeps ? kSweepMaxSweeps : sweeps);
-    hipLaunchKernelGGL(sw::sweep_prep_kernel, dim3(1), dim3(sw::kPrepThreads), 0, st, d);
+    hipLaunchKernelGGL(sw::sweep_prep_kernel, dim3(1), dim3(sw::kPrepThreads), 0, st, d, kSweepMaxSlots);
     for (int s = 0; s < sweeps; ++s) {
         switch (mode) {
             case kEvalMicro: hipLaunchKernelGGL(sw::sweep_kernel<kEvalMicro>, dim3(kSweepMaxB), dim3(sw::kThreads), 0, st, d, s); break;
@@ -419,6 +419,11 @@ hipError_t launch_resolve_sweep(const EngineArgs* d, int mode, int sweeps, hipSt
         }
     }
     hipLaunchKernelGGL(sw::sweep_commit_kernel<kEvalWide>, dim3(1), dim3(sw::kPrepThreads), 0, st, d, sweeps);
+    return hipGetLastError();
+}
+
+hipError_t launch_sweep_prep(const EngineArgs* d, int max_slots, hipStream_t st) {
+    hipLaunchKernelGGL(sw::sweep_prep_kernel, dim3(1), dim3(sw::kPrepThreads), 0, st, d, max_slots);
     return hipGetLastError();
 }
 

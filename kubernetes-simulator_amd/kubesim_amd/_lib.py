@@ -24,6 +24,7 @@ KS_ENGINE_NO_MICRO = 4
 KS_ENGINE_ONE_POD_RESOLVER = 8
 KS_ENGINE_PAIR_RESOLVER = 16
 KS_ENGINE_SWEEP_RESOLVER = 32
+KS_ENGINE_CHUNK_RESOLVER = 64
 KS_SELFTEST_LR_MICRO = 0
 
 STATUS_NAMES = {KS_OK: "OK", KS_EINVAL: "InvalidArgument", KS_ENOTFOUND: "NotFound",

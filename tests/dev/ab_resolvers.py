@@ -13,7 +13,7 @@ from kubesim_amd.engine import Engine
 args = [x for x in sys.argv[1:] if not x.startswith("--")]
 c5 = "--c5" in sys.argv
 names = args or ["one_pod", "pair", "sweep"]
-FLAGS = {"one_pod": 8, "pair": 16, "sweep": 32}
+FLAGS = {"one_pod": 8, "pair": 16, "sweep": 32, "chunk": 64}
 tr = tracegen.c5_trace(n_pods=120_000) if c5 else tracegen.c3_trace(n_pods=200_000)
 enc = encode.encode_trace(tr)
 for rep in range(2):

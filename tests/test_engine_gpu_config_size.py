@@ -105,12 +105,12 @@ def test_c3_40k_pods_bit_exact_with_usage_samples(c3):
     assert_same_binds(eb, ob)
 
 
-@pytest.mark.parametrize("flags", [0, 16, 32], ids=["default", "pair", "sweep"])
+@pytest.mark.parametrize("flags", [0, 16, 32, 64], ids=["default", "pair", "sweep", "chunk"])
 def test_c3_whole_trace_matches_oracle_golden(c3, flags):
     """Every pod of the 1M-pod trace — the whole range bench.py times — bind-for-bind against the
     oracle's committed digests (tests/golden/full_run.json, tests/golden/make_full_run.py), at
     the bench's batch (the engine default), with usage at every other window end; the engine's
-    default resolver and the forced pair / sweep resolvers."""
+    default resolver and the forced pair / sweep / chunk resolvers."""
     tr, enc = c3
     g = full_run_digest.load("c3")
     assert g is not None and g["pods"] == tr["pods"]["m"] and g["nodes"] == tr["nodes"]["n"]

@@ -2,7 +2,8 @@
 
 The engine has four exact resolvers for step 4 of a batch: the role-split one-pod
 kernel, the register-table kernel (small clusters), the pair kernel (two pods per barrier) and
-the sweep kernel (parallel Jacobi sweeps to the sequential fixed point).  The engine picks one
+the sweep kernel (parallel Jacobi sweeps to the sequential fixed point), and the chunk kernel
+(chunked Jacobi sweeps in one workgroup's LDS).  The engine picks one
 by size class; the KS_ENGINE_*_RESOLVER flags force one, and each forced resolver must give the
 oracle's binds, statuses and usage on every case below — all filter / scorer modes, batch sizes
 from 3 to 256, dense in-batch expiries, forced list exhaustion, and a C2 prefix.
@@ -15,7 +16,7 @@ from kubesim_amd import _lib, tracegen
 
 pytestmark = pytest.mark.gpu
 RESOLVERS = {"one_pod": _lib.KS_ENGINE_ONE_POD_RESOLVER, "pair": _lib.KS_ENGINE_PAIR_RESOLVER,
-             "sweep": _lib.KS_ENGINE_SWEEP_RESOLVER}
+             "sweep": _lib.KS_ENGINE_SWEEP_RESOLVER, "chunk": _lib.KS_ENGINE_CHUNK_RESOLVER}
 
 
 def _run(tr, mode, ticks, batch, flags, chunks):
