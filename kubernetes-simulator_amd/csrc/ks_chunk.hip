@@ -26,7 +26,8 @@
 namespace ks {
 namespace chk {
 
-constexpr int kThreads = 1024;
+constexpr int kThreads = 512;   // 8 waves: 256 VGPRs per lane (no spills)
+constexpr int kLanesPerPod = kThreads / 64;  // sweep phases: 64 chunk pods x 8 lanes
 constexpr int kB = kSweepMaxB;  // pods per batch
 constexpr int kC = 64;          // pods per chunk: one lane each
 constexpr int kR = kChR;        // static candidates kept per pod
@@ -39,6 +40,8 @@ constexpr int kL = kTopL;
 constexpr int kClBuf = 256;
 constexpr int kWaves = kThreads / kWave;
 constexpr int16_t kNoSeg = INT16_MAX;
+constexpr int kMOvf = kSeg, kMCid = kSeg + 1;
+static_assert(kSeg + 2 <= 8, "slot row");
 static_assert(kB <= 256 && kB % kC == 0, "chunks of one wave");
 static_assert(kR <= 32, "two entries per lane of a 16-lane pod group");
 
@@ -54,7 +57,12 @@ __device__ __forceinline__ uint64_t dstamp() {
 }
 #define DG(...) __VA_ARGS__
 #else
+#undef KS_CHUNK_ABL
 #define DG(...)
+#endif
+
+#ifndef KS_CHUNK_ABL
+#define KS_CHUNK_ABL 0  // diagnostic ablations (timing only, results invalid): 1 no D pairs, 2 no replays
 #endif
 
 // A node's state in int32 (evaluator modes >= narrow: capacities < 2^29; `ap` clamped)
@@ -142,10 +150,12 @@ enum : uint8_t { kFlRun = 1, kFlTrunc = 2, kFlFull = 4, kFlOvf = 8 };
 struct ChShared {
     PodRec pod[kB];
     uint32_t cl[kB][kR];          // (cid << 16) | total + 1, descending
-    uint64_t thr[kB];
     int32_t cnode[kCid];          // cid -> node (cids 0 .. n_e - 1 are E, in ws order)
     int32_t rs[4][kCid];          // ac am ag ap
-    int32_t rd[4][kCid];          // rc rm rg nr at the batch start
+    int32_t rd[4][kCid];          // rc rm rg nr at the base: binds < tb, events effective < tb
+    uint16_t ecur[kCid];          // first E slot (eslot index) not yet applied; bit 15: pending own expiries
+    int16_t fcur[kCid];           // first final bind >= tb (fnext list), -1 none
+    uint8_t dirty[kCid];          // chunk binds changed since the node's last replay
     uint64_t rt[kCid], rl[kCid];  // taint label
     uint64_t cmask[kCid];         // this sweep's chunk binds of the cid (bit = pod - c0)
     int16_t fhead[kCid], ftail[kCid];  // final binds of the cid, ascending (fnext links)
@@ -159,9 +169,11 @@ struct ChShared {
     int32_t xreq[3][kSlots];
     int16_t xeff[kSlots];         // slot x is applied from pod xeff[x] on
     int16_t eoff[kSlots + 1], eslot[kSlots];
-    int16_t seff[kB][kSeg];       // replayed node (slot = its first binder pod): segment start pods
-    int32_t sst[kB][kSeg][4];     // and states rc rm rg nr
-    int16_t sovf[kB];             // first pod whose state the slot does not hold
+    // replayed node (slot = its first binder pod, one 16-byte row): [0, kSeg) segment start pods,
+    // [kMOvf] the first pod whose state the slot does not hold, [kMCid] the node's cid (-1: the pod
+    // is not a first binder)
+    alignas(16) int16_t smeta[kB][8];
+    int32_t sst[kB][kSeg][4];     // segment states rc rm rg nr
     uint64_t cd1[kC], cd2[kC];    // top two keys of pre-chunk nodes per chunk pod
     int16_t cd1c[kC], cd2c[kC];
     uint8_t cdbad[kC];
@@ -181,113 +193,163 @@ struct ChShared {
 };
 static_assert(sizeof(ChShared) <= 160 * 1024, "LDS");
 
-// Replays cid k: its final binds (pods < c0), then — `chunk` — the current sweep's chunk binds,
-// with the pre-batch expiry slots of k (E cids) and each admitted running bind's own expiry, in
-// pod order.  Stores the state segments for pods [from, i_end) in slot sl (sl < 0: none), writes
-// adm[] of every bind (`wadm`), returns the state before pod i_end binds.
-__device__ NS32 replay(ChShared& sh, int k, int n_e, bool chunk, int c0, int from, int sl, int i_end, bool wadm) {
+// Replays cid k from its base (state before pod tb: binds < tb, events effective < tb): its final
+// binds >= tb (admission known, adm[]), then — `chunk` — the current sweep's chunk binds (admission
+// evaluated, written to adm[]), with the pre-batch expiry slots of k (E cids) and each admitted
+// running bind's own expiry, in pod order.  Stores the state segments for pods [from, i_end) in
+// slot sl (sl < 0: none); returns the state before pod i_end binds (events effective < i_end);
+// *ecur_out / *hp_out (optional): the E cursor and whether own expiries remain pending after it.
+// A bind whose own expiry cannot be tracked (more than kPend pending) makes the state unknown
+// from the next pod on: the slot's ovf, adm 2 for later binds, *lost_at.
+struct Replayed {
     NS32 v;
-    v.ac = sh.rs[0][k]; v.am = sh.rs[1][k]; v.ag = sh.rs[2][k]; v.ap = sh.rs[3][k];
-    v.rc = sh.rd[0][k]; v.rm = sh.rd[1][k]; v.rg = sh.rd[2][k]; v.nr = sh.rd[3][k];
-    v.taint = 0; v.label = 0;
-    int e_u = 0, e_end = 0;
-    if (k < n_e) { e_u = sh.eoff[k]; e_end = sh.eoff[k + 1]; }
-    // pending own expiries: fixed register slots (eff INT_MAX = empty), no dynamic indexing
-    int pe[kPend], pj[kPend];
-#pragma unroll
-    for (int q = 0; q < kPend; ++q) { pe[q] = INT_MAX; pj[q] = 0; }
+    int ecur;     // E cursor after the replay
+    bool hp;      // own expiries still pending
+    int lost_at;  // INT_MAX, or the first pod whose state is unknown
+};
+__device__ __forceinline__ Replayed replay(ChShared& sh, int k, int n_e, int tb, bool chunk, int c0, int from, int sl, int i_end) {
+    // (no lambdas: their by-reference closures kept the state in scratch memory)
+    int32_t vrc = sh.rd[0][k], vrm = sh.rd[1][k], vrg = sh.rd[2][k], vnr = sh.rd[3][k];
+    const uint16_t ec = sh.ecur[k];
+    int e_u = ec & 0x7FFF;
+    const int e_end = k < n_e ? sh.eoff[k + 1] : 0;
+    // pending own expiries: four named slots (eff INT_MAX = empty), updated by value selects only
+    static_assert(kPend == 4, "four pending slots");
+    int pe0 = INT_MAX, pe1 = INT_MAX, pe2 = INT_MAX, pe3 = INT_MAX, pj0 = 0, pj1 = 0, pj2 = 0, pj3 = 0;
     bool lost = false;
-    int ns = 0, last_t = -1, ovf = kNoSeg;
-    auto store = [&](int t) {
-        if (sl < 0) return;
-        t = t < from ? from : t;
-        if (t >= i_end || t >= ovf) return;
-        if (t != last_t) {
-            if (ns == kSeg) { ovf = t; return; }
-            sh.seff[sl][ns] = (int16_t)t;
-            ++ns;
-            last_t = t;
+    int ovf = kNoSeg, lost_at = INT_MAX;
+#define KS_PUSH(EX, JB)                                                                              \
+    do {                                                                                             \
+        const int ex_ = (EX), jb_ = (JB);                                                            \
+        const bool s0 = pe0 == INT_MAX, s1 = !s0 && pe1 == INT_MAX, s2 = !s0 && !s1 && pe2 == INT_MAX, \
+                   s3 = !s0 && !s1 && !s2 && pe3 == INT_MAX;                                          \
+        pe0 = s0 ? ex_ : pe0; pj0 = s0 ? jb_ : pj0;                                                  \
+        pe1 = s1 ? ex_ : pe1; pj1 = s1 ? jb_ : pj1;                                                  \
+        pe2 = s2 ? ex_ : pe2; pj2 = s2 ? jb_ : pj2;                                                  \
+        pe3 = s3 ? ex_ : pe3; pj3 = s3 ? jb_ : pj3;                                                  \
+        if (!(s0 || s1 || s2 || s3)) { /* untracked: the state is unknown from the next pod on */   \
+            lost = true;                                                                             \
+            ovf = jb_ + 1 < ovf ? jb_ + 1 : ovf;                                                     \
+            lost_at = jb_ + 1 < lost_at ? jb_ + 1 : lost_at;                                         \
+        }                                                                                            \
+    } while (0)
+    if (ec & 0x8000) {  // own expiries of binds before the base that have not fired by it
+        for (int j = sh.fhead[k]; j >= 0 && j < tb; j = sh.fnext[j]) {
+            const int x = sh.own[j];
+            if (sh.adm[j] == 1 && (sh.clfl[j] & kFlRun) && x >= 0 && sh.xeff[x] >= tb) KS_PUSH(sh.xeff[x], j);
         }
-        int32_t* d = sh.sst[sl][ns - 1];
-        d[0] = v.rc; d[1] = v.rm; d[2] = v.rg; d[3] = v.nr;
-    };
-    if (sl >= 0) {
-        for (int q = 0; q < kSeg; ++q) sh.seff[sl][q] = kNoSeg;
-        store(from);
     }
-    auto advance = [&](int t) {  // apply every event effective at pods <= t
-        for (;;) {
-            const int ne = e_u < e_end ? sh.xeff[sh.eslot[e_u]] : INT_MAX;
-            int pq = 0, pm = INT_MAX;
-#pragma unroll
-            for (int q = 0; q < kPend; ++q)
-                if (pe[q] < pm) { pm = pe[q]; pq = q; }
-            const int nx = ne < pm ? ne : pm;
-            if (nx > t) break;
+    int ns = 0, last_t = -1;
+#define KS_STORE(T)                                                                                  \
+    do {                                                                                             \
+        int t_ = (T);                                                                                \
+        t_ = t_ < from ? from : t_;                                                                  \
+        if (sl >= 0 && t_ < i_end && t_ < ovf) {                                                     \
+            bool ok_ = true;                                                                         \
+            if (t_ != last_t) {                                                                      \
+                if (ns == kSeg) { ovf = t_; ok_ = false; }                                           \
+                else { sh.smeta[sl][ns] = (int16_t)t_; ++ns; last_t = t_; }                          \
+            }                                                                                        \
+            if (ok_) *reinterpret_cast<int4*>(&sh.sst[sl][ns - 1][0]) = make_int4(vrc, vrm, vrg, vnr); \
+        }                                                                                            \
+    } while (0)
+    if (sl >= 0) {
+        for (int q = 0; q < kSeg; ++q) sh.smeta[sl][q] = kNoSeg;
+        sh.smeta[sl][kMCid] = (int16_t)k;
+        KS_STORE(from);
+    }
+    const int32_t ac = sh.rs[0][k], am = sh.rs[1][k], ag = sh.rs[2][k], ap = sh.rs[3][k];
+    int j = sh.fcur[k];
+    uint64_t m = chunk ? sh.cmask[k] : 0ull;
+    // one event loop: the next bind (final list, then the chunk mask) against the next expiry
+    for (;;) {
+        int jb = j >= 0 ? j : (m ? c0 + __builtin_ctzll(m) : INT_MAX);
+        if (jb >= i_end) jb = INT_MAX;
+        const int ne = e_u < e_end ? sh.xeff[sh.eslot[e_u]] : INT_MAX;
+        const int pm01 = pe0 < pe1 ? pe0 : pe1, pm23 = pe2 < pe3 ? pe2 : pe3;
+        const int pm = pm01 < pm23 ? pm01 : pm23;
+        const int nx = ne < pm ? ne : pm;
+        const int lim = jb != INT_MAX ? jb : i_end - 1;
+        if (nx <= lim) {  // an expiry effective before the next bind (or before i_end)
             if (ne == nx) {
                 const int x = sh.eslot[e_u++];
-                v.rc -= sh.xreq[0][x]; v.rm -= sh.xreq[1][x]; v.rg -= sh.xreq[2][x]; v.nr -= 1;
+                vrc -= sh.xreq[0][x]; vrm -= sh.xreq[1][x]; vrg -= sh.xreq[2][x]; vnr -= 1;
             } else {
-                int jq = 0;
-#pragma unroll
-                for (int q = 0; q < kPend; ++q)
-                    if (q == pq) { jq = pj[q]; pe[q] = INT_MAX; }
+                const bool h0 = pe0 == pm, h1 = !h0 && pe1 == pm, h2 = !h0 && !h1 && pe2 == pm,
+                           h3 = !h0 && !h1 && !h2;
+                const int jq = h0 ? pj0 : (h1 ? pj1 : (h2 ? pj2 : pj3));
+                pe0 = h0 ? INT_MAX : pe0; pe1 = h1 ? INT_MAX : pe1;
+                pe2 = h2 ? INT_MAX : pe2; pe3 = h3 ? INT_MAX : pe3;
                 const PodRec& p = sh.pod[jq];
-                v.rc -= (int32_t)p.req[0]; v.rm -= (int32_t)p.req[1]; v.rg -= (int32_t)p.req[2]; v.nr -= 1;
+                vrc -= (int32_t)p.req[0]; vrm -= (int32_t)p.req[1]; vrg -= (int32_t)p.req[2]; vnr -= 1;
             }
-            store(nx);
+            KS_STORE(nx);
+            continue;
         }
-    };
-    int j = sh.fhead[k];
-    uint64_t m = chunk ? sh.cmask[k] : 0ull;
-    for (;;) {
-        int jb;
-        if (j >= 0) { jb = j; j = sh.fnext[j]; }
-        else if (m) { jb = c0 + __builtin_ctzll(m); m &= m - 1; }
-        else break;
-        if (jb >= i_end) break;
-        advance(jb);
+        if (jb == INT_MAX) break;
+        const bool fin = j >= 0;
+        if (fin) j = sh.fnext[j];
+        else m &= m - 1;
         const PodRec& p = sh.pod[jb];
-        const bool ok = !lost && fits32(p, v);
-        if (wadm) sh.adm[jb] = lost ? 2 : (ok ? 1 : 0);
+        bool ok;
+        if (fin) {
+            ok = sh.adm[jb] == 1;
+        } else {  // CreatePod admission (kubesim/node/node.go:44-47)
+            ok = !lost && vnr < ap;
+            if (p.keymask & 1) ok &= (int64_t)vrc + p.req[0] <= ac;
+            if (p.keymask & 2) ok &= (int64_t)vrm + p.req[1] <= am;
+            if (p.keymask & 4) ok &= (int64_t)vrg + p.req[2] <= ag;
+            sh.adm[jb] = lost ? 2 : (ok ? 1 : 0);
+        }
         if (ok && (sh.clfl[jb] & kFlRun)) {
-            v.rc += (int32_t)p.req[0]; v.rm += (int32_t)p.req[1]; v.rg += (int32_t)p.req[2]; v.nr += 1;
-            store(jb + 1);
+            vrc += (int32_t)p.req[0]; vrm += (int32_t)p.req[1]; vrg += (int32_t)p.req[2]; vnr += 1;
+            KS_STORE(jb + 1);
             const int x = sh.own[jb];
-            if (x >= 0) {
-                const int ex = sh.xeff[x];
-                bool placed = false;
-#pragma unroll
-                for (int q = 0; q < kPend; ++q)
-                    if (!placed && pe[q] == INT_MAX) { pe[q] = ex; pj[q] = jb; placed = true; }
-                if (!placed) {  // untracked: the state is unknown from the next pod on
-                    lost = true;
-                    if (jb + 1 < ovf) ovf = jb + 1;
-                }
-            }
+            if (x >= 0) KS_PUSH(sh.xeff[x], jb);
         }
     }
-    advance(i_end - 1);
-    if (sl >= 0) sh.sovf[sl] = (int16_t)ovf;
-    return v;
+#undef KS_STORE
+#undef KS_PUSH
+    if (sl >= 0) sh.smeta[sl][kMOvf] = (int16_t)ovf;
+    Replayed out;
+    out.v.ac = ac; out.v.am = am; out.v.ag = ag; out.v.ap = ap;
+    out.v.rc = vrc; out.v.rm = vrm; out.v.rg = vrg; out.v.nr = vnr;
+    out.v.taint = 0; out.v.label = 0;
+    out.ecur = e_u;
+    out.hp = (pe0 & pe1 & pe2 & pe3) != INT_MAX;  // any slot holds a (non-negative) pod index
+    out.lost_at = lost_at;
+    return out;
 }
 
-// state of slot sl's node at pod i (i >= the slot's first segment)
-__device__ __forceinline__ int seg_of(const ChShared& sh, int sl, int i) {
+// a slot's 16-byte row
+struct SRow {
+    uint4 v;
+    __device__ __forceinline__ int m(int q) const {  // q: a compile-time constant after unrolling
+        const uint32_t w = q < 2 ? v.x : (q < 4 ? v.y : (q < 6 ? v.z : v.w));
+        return (int)(int16_t)(uint16_t)((q & 1) ? (w >> 16) : (w & 0xFFFFu));
+    }
+    __device__ __forceinline__ void clear_cid() { v.w |= 0xFFFFu; }  // kMCid = 6: low half of v.w
+};
+static_assert(kMCid == 6, "SRow::clear_cid");
+__device__ __forceinline__ SRow srow(const ChShared& sh, int sl) {
+    SRow r;
+    r.v = *reinterpret_cast<const uint4*>(&sh.smeta[sl][0]);
+    return r;
+}
+
+// Pod i's key on slot sl's node (cid k) from its row: the segment holding pod i
+template <int kMode>
+__device__ __forceinline__ uint64_t key_at(const EngineArgs& a, const ChShared& sh, const PodRec& p, int i, int k,
+                                           int sl, const SRow& r) {
     int s = 0;
 #pragma unroll
-    for (int q = 1; q < kSeg; ++q) s += sh.seff[sl][q] <= i;
-    return s;
-}
-
-template <int kMode>
-__device__ __forceinline__ uint64_t key_on(const EngineArgs& a, const ChShared& sh, int i, int k, int sl) {
-    const int s = seg_of(sh, sl, i);
+    for (int q = 1; q < kSeg; ++q) s += r.m(q) <= i;
+    const int4 st = *reinterpret_cast<const int4*>(&sh.sst[sl][s][0]);
     NS32 n;
     n.ac = sh.rs[0][k]; n.am = sh.rs[1][k]; n.ag = sh.rs[2][k]; n.ap = sh.rs[3][k];
-    n.rc = sh.sst[sl][s][0]; n.rm = sh.sst[sl][s][1]; n.rg = sh.sst[sl][s][2]; n.nr = sh.sst[sl][s][3];
+    n.rc = st.x; n.rm = st.y; n.rg = st.z; n.nr = st.w;
     n.taint = sh.rt[k]; n.label = sh.rl[k];
-    return make_key(eval_t<kMode>(a.c, sh.pod[i], n), (uint32_t)sh.cnode[k]);
+    return make_key(eval_t<kMode>(a.c, p, n), (uint32_t)sh.cnode[k]);
 }
 
 __device__ __forceinline__ uint64_t cl_key(const ChShared& sh, uint32_t e) {
@@ -306,7 +368,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
     const int n_e = ws.n_e, e_cnt = ws.e_cnt;
 
     // ---- setup: pods, window, candidate ids, records
-    DG(uint64_t t_setup = dstamp(); uint64_t acc_cd = 0, acc_sw = 0, acc_fin = 0, acc_ph[4] = {0, 0, 0, 0}; int n_sweeps = 0, n_chunks = 0;)
+    DG(uint64_t t_setup = dstamp(); uint64_t acc_cd = 0, acc_sw = 0, acc_fin = 0, acc_ph[4] = {0, 0, 0, 0}; int n_sweeps = 0, n_sonly = 0, n_chunks = 0;)
     if (tid == 0) { sh.ncid = n_e; sh.nbc = nb; sh.cut = INT_MAX; sh.fc[0] = sh.fc[1] = INT_MAX; sh.fs[0] = sh.fs[1] = INT_MAX; }
     for (int h = tid; h < kHash; h += kThreads) sh.u.h.hk[h] = -1;
     if (tid < nb) {
@@ -317,10 +379,10 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
         sh.clcnt[tid] = (uint8_t)(info & 0xFF);
         sh.clfl[tid] = (a.dur[start + tid] > 0 ? kFlRun : 0) | ((info & kClTrunc) ? kFlTrunc : 0) |
                        ((info & kClFull) ? kFlFull : 0) | ((info & kClOvf) ? kFlOvf : 0);
-        sh.thr[tid] = ws.cl_thr[tid];
         sh.adm[tid] = 0;
         sh.wf[tid] = -1;
         sh.w[0][tid] = -1; sh.w[1][tid] = -1;
+        sh.smeta[tid][kMCid] = -1;
         sh.code[0][tid] = 0; sh.code[1][tid] = 0;
     }
     for (int x = tid; x < e_cnt; x += kThreads) {
@@ -331,76 +393,100 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
     }
     for (int k = tid; k <= n_e; k += kThreads) sh.eoff[k] = (int16_t)ws.e_off[k];
     __syncthreads();
+    DG(uint64_t ts1 = dstamp();)
     // slot x is applied from the first pod i >= 1 with win_hi[i] > x
     for (int i = tid + 1; i < nb; i += kThreads)
         for (int x = sh.win_hi[i - 1]; x < sh.win_hi[i]; ++x) sh.xeff[x] = (int16_t)i;
     // candidate ids: E nodes are cids 0 .. n_e - 1; then every list node, claimed by CAS
-    auto insert = [&](int32_t node, int32_t val, int32_t* slot_out) -> bool {
+    // Candidate ids: E nodes are cids 0 .. n_e - 1; list nodes are numbered in (pod, entry) order,
+    // 64 pods per phase (claim by CAS, exclusive prefix of the claims over the threads, which run
+    // in pod order), so the batch is cut exactly before the first pod whose nodes do not fit
+    // kCid — pod 0 always fits (its <= L entries beside <= kSlots E nodes).  A phase starts only
+    // when the hash has room for all its entries.
+    if (tid < n_e) {  // distinct (the prep kernel's E)
+        const int32_t node = ws.e_node[tid];
         uint32_t h = hslot(node);
-        for (int t = 0; t < kHash; ++t) {
-            const int32_t prev = atomicCAS(&sh.u.h.hk[h], -1, node);
-            if (prev == -1) { if (val >= 0) sh.u.h.hv[h] = val; *slot_out = (int)h; return true; }
-            if (prev == node) { *slot_out = (int)h; return false; }
-            h = (h + 1) & (kHash - 1);
-        }
-        *slot_out = -1;
-        return false;
-    };
-    if (tid < n_e) {
-        int32_t s;
-        insert(ws.e_node[tid], tid, &s);
-        sh.cnode[tid] = ws.e_node[tid];
+        while (atomicCAS(&sh.u.h.hk[h], -1, node) != -1) h = (h + 1) & (kHash - 1);  // < kHash keys
+        sh.u.h.hv[h] = tid;
+        sh.cnode[tid] = node;
     }
-    __syncthreads();
-    // each thread: pod i = tid / 4, entries (tid % 4) + 4 r
-    int32_t eslot_of[kR / 4 + 1];
-    bool claim[kR / 4 + 1];
+    __shared__ int32_t wsum[kWaves];
     {
-        const int i = tid >> 2;
-        const int nc = i < nb ? sh.clcnt[i] : 0;
+        constexpr int kPP = 64, kTPP = kThreads / kPP, kEPT = (kR + kTPP - 1) / kTPP;  // 8 threads, 3 entries
+        static_assert(kTPP * kPP == kThreads, "threads per phase pod");
+        const int pl = tid / kTPP, sub = tid % kTPP;
+        // phases: pod 0 alone (always fits), then 64 pods at a time
+        for (int p0 = 0, pn = 1; p0 < nb; p0 = pn, pn = p0 + kPP) {
+            const int i = p0 + pl;
+            const bool mine = i < pn && i < nb;
+            const int nc = mine ? sh.clcnt[i] : 0;
+            uint64_t key[kEPT];
 #pragma unroll
-        for (int q = 0; q < kR / 4; ++q) {
-            const int r = (tid & 3) + 4 * q;
-            eslot_of[q] = -1;
-            claim[q] = false;
-            if (r < nc) {
-                const int32_t node = key_node(ws.cl_key[i][r]);
-                int32_t s;
-                claim[q] = insert(node, -1, &s);
-                eslot_of[q] = s;
-                if (s < 0) atomicMin(&sh.nbc, i);  // hash full: cut the batch before this pod
+            for (int q = 0; q < kEPT; ++q) {
+                const int r = sub + kTPP * q;
+                key[q] = r < nc ? ws.cl_key[i][r] : 0ull;
             }
+            // room check (uniform): the keys so far + every entry of this phase
+            if (tid == 0) sh.cut = 0;
+            __syncthreads();
+            if (sub == 0 && nc) atomicAdd(&sh.cut, nc);
+            __syncthreads();
+            const bool room = sh.ncid + sh.cut <= kHash - kWave;
+            __syncthreads();
+            if (!room) { if (tid == 0) atomicMin(&sh.nbc, p0); break; }
+            int slot[kEPT];
+            int claims = 0;
+#pragma unroll
+            for (int q = 0; q < kEPT; ++q) {
+                slot[q] = -1;
+                if (key[q] == 0) continue;
+                const int32_t node = key_node(key[q]);
+                uint32_t h = hslot(node);
+                for (;;) {  // the room check keeps the table below kHash keys: terminates
+                    const int32_t prev = atomicCAS(&sh.u.h.hk[h], -1, node);
+                    if (prev == -1) { slot[q] = (int)h | (1 << 30); ++claims; break; }
+                    if (prev == node) { slot[q] = (int)h; break; }
+                    h = (h + 1) & (kHash - 1);
+                }
+            }
+            // exclusive prefix of the claims in thread (= pod, entry) order
+            int incl = claims;
+#pragma unroll
+            for (int o = 1; o < kWave; o <<= 1) {
+                const int v = __shfl_up(incl, o);
+                if (lane >= o) incl += v;
+            }
+            if (lane == kWave - 1) wsum[wave] = incl;
+            __syncthreads();
+            int base = sh.ncid;
+            for (int g = 0; g < wave; ++g) base += wsum[g];
+            int c = base + incl - claims;
+#pragma unroll
+            for (int q = 0; q < kEPT; ++q)
+                if (slot[q] >= 0 && (slot[q] & (1 << 30))) {
+                    const int h = slot[q] & ~(1 << 30);
+                    sh.u.h.hv[h] = c;
+                    if (c < kCid) sh.cnode[c] = key_node(key[q]);
+                    ++c;
+                }
+            __syncthreads();
+            if (tid == kThreads - 1) sh.ncid = c;  // the last thread's next id is the phase total
+#pragma unroll
+            for (int q = 0; q < kEPT; ++q) {
+                if (slot[q] < 0) continue;
+                const int cid = sh.u.h.hv[slot[q] & ~(1 << 30)];
+                if (cid >= kCid) atomicMin(&sh.nbc, i);
+                else sh.cl[i][sub + kTPP * q] = ((uint32_t)cid << 16) | (uint32_t)(key[q] >> 32);
+            }
+            __syncthreads();
+            if (sh.nbc < pn) break;
         }
-    }
-    __syncthreads();
-    {
-        const int i = tid >> 2;
-#pragma unroll
-        for (int q = 0; q < kR / 4; ++q)
-            if (claim[q]) {
-                const int c = atomicAdd(&sh.ncid, 1);
-                sh.u.h.hv[eslot_of[q]] = c;
-                if (c < kCid) sh.cnode[c] = sh.u.h.hk[eslot_of[q]];
-                else atomicMin(&sh.nbc, i);
-            }
-    }
-    __syncthreads();
-    {
-        const int i = tid >> 2;
-        const int nc = i < nb ? sh.clcnt[i] : 0;
-#pragma unroll
-        for (int q = 0; q < kR / 4; ++q) {
-            const int r = (tid & 3) + 4 * q;
-            if (r < nc && eslot_of[q] >= 0) {
-                const int c = sh.u.h.hv[eslot_of[q]];
-                if (c >= kCid) atomicMin(&sh.nbc, i);
-                else sh.cl[i][r] = ((uint32_t)c << 16) | (uint32_t)(ws.cl_key[i][r] >> 32);
-            }
-        }
+        if (tid == 0) sh.cut = INT_MAX;
     }
     __syncthreads();
     nb = sh.nbc < nb ? sh.nbc : nb;
     const int ncid = sh.ncid < kCid ? sh.ncid : kCid;
+    DG(uint64_t ts2 = dstamp();)
     for (int k = tid; k < ncid; k += kThreads) {
         const int32_t n = sh.cnode[k];
         const NodeV v = load_node(a.s, n);
@@ -408,40 +494,71 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
         sh.rd[0][k] = (int32_t)v.rc; sh.rd[1][k] = (int32_t)v.rm; sh.rd[2][k] = (int32_t)v.rg; sh.rd[3][k] = (int32_t)v.nr;
         sh.rt[k] = v.taint; sh.rl[k] = v.label;
         sh.cmask[k] = 0;
-        sh.fhead[k] = -1; sh.ftail[k] = -1;
+        sh.fhead[k] = -1; sh.ftail[k] = -1; sh.fcur[k] = -1;
+        sh.ecur[k] = k < n_e ? (uint16_t)sh.eoff[k] : 0;
+        sh.dirty[k] = 0;
     }
     __syncthreads();
 
     // ---- chunks
-    DG(t_setup = dstamp() - t_setup;)
-    int committed = nb, stop_code = 0;
+    DG(uint64_t ts3 = dstamp(); uint64_t sub1 = ts1 - t_setup, sub2 = ts2 - ts1, sub3 = ts3 - ts2; t_setup = ts3 - t_setup;)
+    int committed = nb, stop_code = 0, tb = 0;
     for (int c0 = 0; c0 < nb; c0 += kC) {
         const int c1 = nb < c0 + kC ? nb : c0 + kC;
         DG(uint64_t t0 = dstamp(); ++n_chunks;)
         // (1) pre-chunk nodes: replay each over [c0, c1) into its first final binder's slot, then
         // per chunk pod the top two keys (lane = pod, waves over nodes)
         if (c0 > 0) {
-            if (tid < c0) {
-                const int k = sh.wf[tid];
-                if (k >= 0 && sh.fhead[k] == tid) (void)replay(sh, k, n_e, false, c0, c0, tid, c1, false);
+            // rebase every node with events to c0 (binds < c0, events effective < c0)
+            for (int k = tid; k < ncid; k += kThreads) {
+                if (k < n_e || sh.fhead[k] >= 0) {
+                    const Replayed r = replay(sh, k, n_e, tb, false, c0, c0, -1, c0);
+                    if (r.lost_at != INT_MAX) atomicMin(&sh.cut, c0);
+                    sh.rd[0][k] = r.v.rc; sh.rd[1][k] = r.v.rm; sh.rd[2][k] = r.v.rg; sh.rd[3][k] = r.v.nr;
+                    sh.ecur[k] = (uint16_t)(r.ecur | (r.hp ? 0x8000 : 0));
+                    sh.fcur[k] = -1;
+                }
+            }
+            __syncthreads();
+            tb = c0;
+            if (sh.cut <= c0) {  // an own expiry could not be tracked: commit the pods before c0
+                committed = c0;
+                stop_code = 1;
+                break;
+            }
+            // replays spread over the waves: pod j's thread is 2 j
+            if ((tid & 1) == 0 && (tid >> 1) < c0) {
+                const int j = tid >> 1;
+                const int k = sh.wf[j];
+                if (k >= 0 && sh.fhead[k] == j) (void)replay(sh, k, n_e, tb, false, c0, c0, j, c1);
+                else sh.smeta[j][kMCid] = -1;
             }
             __syncthreads();
             {
                 const int i = c0 + lane;
+                const bool li = i < c1;
+                const PodRec p = sh.pod[li ? i : c0];
                 uint64_t k1 = 0, k2 = 0;
                 int16_t q1 = -1, q2 = -1;
                 bool bad = false;
-                for (int j = wave; j < c0; j += kWaves) {
-                    const int k = sh.wf[j];
-                    if (k < 0 || sh.fhead[k] != j) continue;
-                    if (i < c1) {
-                        if (sh.sovf[j] <= i) {
-                            bad = true;
-                        } else {
-                            const uint64_t key = key_on<kMode>(a, sh, i, k, j);
-                            if (key > k1) { k2 = k1; q2 = q1; k1 = key; q1 = (int16_t)k; }
-                            else if (key > k2) { k2 = key; q2 = (int16_t)k; }
-                        }
+                // four slots per step (j = wave + 16 (4 t + q)), their loads issued together
+                for (int j0 = wave; j0 < c0; j0 += 4 * kWaves) {
+                    SRow r[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int j = j0 + q * kWaves;
+                        r[q] = srow(sh, j < c0 ? j : 0);
+                        if (j >= c0) r[q].clear_cid();
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int j = j0 + q * kWaves;
+                        const int k = r[q].m(kMCid);
+                        if (k < 0 || !li) continue;
+                        if (r[q].m(kMOvf) <= i) { bad = true; continue; }
+                        const uint64_t key = key_at<kMode>(a, sh, p, i, k, j, r[q]);
+                        if (key > k1) { k2 = k1; q2 = q1; k1 = key; q1 = (int16_t)k; }
+                        else if (key > k2) { k2 = key; q2 = (int16_t)k; }
                     }
                 }
                 sh.u.x.k[wave][lane][0] = k1; sh.u.x.k[wave][lane][1] = bad ? ~0ull : k2;
@@ -452,6 +569,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                 uint64_t k1 = 0, k2 = 0;
                 int16_t q1 = -1, q2 = -1;
                 bool bad = false;
+#pragma unroll 4
                 for (int g = 0; g < kWaves; ++g) {
                     if (sh.u.x.k[g][lane][1] == ~0ull) { bad = true; continue; }
 #pragma unroll
@@ -471,61 +589,95 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
 
         // (2) sweeps
         DG(uint64_t t1 = dstamp(); acc_cd += t1 - t0;)
+        // Rounds in two modes.  First exclusion-only rounds (w_i = the first static candidate no
+        // earlier pod takes; no evaluation, no replay) to their fixed point — a guess without the
+        // piles a cold start makes (every pod on its own best node) — then full sweeps from it.
         int par = 0, lo = c0, fsv = INT_MAX;
+        bool sonly = true;
         for (;;) {
-            DG(++n_sweeps; uint64_t q0 = dstamp();)
-            // A: the guesses' chunk binds
-            int wold = -1;
-            if (tid < kC) {
-                const int i = c0 + tid;
-                if (i < c1) {
-                    wold = sh.w[par][i];
-                    if (wold >= 0) atomicOr((unsigned long long*)&sh.cmask[wold], 1ull << tid);
+            DG(if (sonly) ++n_sonly; else ++n_sweeps; uint64_t q0 = dstamp();)
+            // A: the guesses' chunk binds (pod c0 + jr on thread 16 jr: spread over the waves)
+            // incrementally: a pod whose guess changed moves its bit and marks both nodes dirty
+            int wcur = -1;
+            const int jr = tid / kLanesPerPod;
+            const bool jlead = tid % kLanesPerPod == 0;
+            if (jlead && c0 + jr < c1) {
+                wcur = sh.w[par][c0 + jr];
+                const int wprv = sh.w[par ^ 1][c0 + jr];
+                if (wcur != wprv) {
+                    if (wprv >= 0) { atomicAnd((unsigned long long*)&sh.cmask[wprv], ~(1ull << jr)); sh.dirty[wprv] = 1; }
+                    if (wcur >= 0) { atomicOr((unsigned long long*)&sh.cmask[wcur], 1ull << jr); sh.dirty[wcur] = 1; }
                 }
             }
             __syncthreads();
             DG(uint64_t q1 = dstamp(); acc_ph[0] += q1 - q0;)
             // B: replay each chunk node (its first chunk binder's thread) into that pod's slot
-            if (wold >= 0 && __builtin_ctzll(sh.cmask[wold]) == tid)
-                (void)replay(sh, wold, n_e, true, c0, c0, c0 + tid, c1, true);
+            // B: replay each changed chunk node (or one whose first binder moved) into its first
+            // chunk binder's slot
+            if (!sonly && jlead && c0 + jr < c1) {
+                const int j = c0 + jr;
+                if (wcur >= 0 && __builtin_ctzll(sh.cmask[wcur]) == jr) {
+                    if (!(KS_CHUNK_ABL & 2) && (sh.dirty[wcur] || sh.smeta[j][kMCid] != wcur)) {
+                        sh.dirty[wcur] = 0;
+                        (void)replay(sh, wcur, n_e, tb, true, c0, c0, j, c1);
+                    }
+                } else {
+                    sh.smeta[j][kMCid] = -1;
+                }
+            }
             __syncthreads();
             DG(uint64_t q2 = dstamp(); acc_ph[1] += q2 - q1;)
-            // C: pod i = c0 + tid / 16, 16 lanes each
+            // C: pod i = c0 + tid / 8, 8 lanes each
             {
-                const int pi = tid >> 4, sub = tid & 15, rowsh = lane & ~15;
+                constexpr int G = kLanesPerPod;
+                static_assert(G == 8 && kR <= 3 * G, "three entries per lane of an 8-lane pod group");
+                const int pi = tid / G, sub = tid % G, rowsh = lane & ~(G - 1);
                 const int i = c0 + pi;
                 const bool act = i < c1 && i >= lo;
                 const uint64_t below = (1ull << pi) - 1ull;
-                bool f0 = false, f1 = false;
-                uint32_t e0 = 0, e1 = 0;
+                bool f[3] = {false, false, false};
+                uint32_t e[3] = {0u, 0u, 0u};
                 if (act) {
                     const int nc = sh.clcnt[i];
-                    if (sub < nc) {
-                        e0 = sh.cl[i][sub];
-                        const int c = e0 >> 16;
-                        f0 = sh.fhead[c] < 0 && (sh.cmask[c] & below) == 0;
-                    }
-                    if (sub + 16 < nc) {
-                        e1 = sh.cl[i][sub + 16];
-                        const int c = e1 >> 16;
-                        f1 = sh.fhead[c] < 0 && (sh.cmask[c] & below) == 0;
-                    }
+#pragma unroll
+                    for (int q = 0; q < 3; ++q)
+                        if (sub + G * q < nc) e[q] = sh.cl[i][sub + G * q];
+#pragma unroll
+                    for (int q = 0; q < 3; ++q)
+                        if (sub + G * q < nc) {
+                            const int c = e[q] >> 16;
+                            f[q] = sh.fhead[c] < 0 && (sh.cmask[c] & below) == 0;
+                        }
                 }
-                const uint32_t r0 = (uint32_t)(__ballot(f0) >> rowsh) & 0xFFFFu;
-                const uint32_t r1 = (uint32_t)(__ballot(f1) >> rowsh) & 0xFFFFu;
-                const int rfree = r0 ? __builtin_ctz(r0) : (r1 ? 16 + __builtin_ctz(r1) : kR);
-                const uint32_t efree = r0 ? (uint32_t)__shfl((int)e0, rowsh + rfree)
-                                          : (r1 ? (uint32_t)__shfl((int)e1, rowsh + rfree - 16) : 0u);
+                int rfree = kR;
+                uint32_t efree = 0u;
+#pragma unroll
+                for (int q = 2; q >= 0; --q) {  // the lowest free entry wins
+                    const uint32_t rq = (uint32_t)(__ballot(f[q]) >> rowsh) & 0xFFu;
+                    const uint32_t eq = (uint32_t)__shfl((int)e[q], rowsh + (rq ? __builtin_ctz(rq) : 0));
+                    if (rq) { rfree = G * q + __builtin_ctz(rq); efree = eq; }
+                }
                 uint64_t dk = 0;
                 int dc = -1;
                 bool bad = false;
-                if (act) {
-                    for (int jj = sub; jj < pi; jj += 16) {
-                        const int j = c0 + jj;
-                        const int k = sh.w[par][j];
-                        if (k < 0 || __builtin_ctzll(sh.cmask[k]) != jj) continue;
-                        if (sh.sovf[j] <= i) { bad = true; continue; }
-                        const uint64_t key = key_on<kMode>(a, sh, i, k, j);
+                if (act && !sonly) {
+                    // the chunk's first binders j = c0 + sub + 16 q before pod i: rows together
+                    const PodRec p = sh.pod[i];
+                    constexpr int NQ = kC / G;
+                    SRow r[NQ];
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        const int jj = sub + G * q;
+                        r[q] = srow(sh, c0 + (jj < pi ? jj : 0));
+                        if (jj >= pi) r[q].clear_cid();
+                    }
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        const int k = r[q].m(kMCid);
+                        if (k < 0) continue;
+                        if (r[q].m(kMOvf) <= i) { bad = true; continue; }
+                        if (KS_CHUNK_ABL & 1) continue;
+                        const uint64_t key = key_at<kMode>(a, sh, p, i, k, c0 + sub + G * q, r[q]);
                         if (key > dk) { dk = key; dc = k; }
                     }
                     if (sub == 0) {  // pre-chunk nodes: the best one not rebound before pod i
@@ -544,13 +696,20 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                     }
                 }
 #pragma unroll
-                for (int o = 1; o < 16; o <<= 1) {
+                for (int o = 1; o < G; o <<= 1) {
                     const uint64_t ok = shfl_xor64(dk, o);
                     const int oc = __shfl_xor(dc, o);
                     if (ok > dk) { dk = ok; dc = oc; }
                 }
-                bad = ((__ballot(bad) >> rowsh) & 0xFFFFu) != 0;
-                if (sub == 0 && i < c1) {
+                bad = ((__ballot(bad) >> rowsh) & 0xFFu) != 0;
+                if (sonly) {
+                    if (sub == 0 && i < c1) {
+                        const int nw = act ? (rfree < kR ? (int)(efree >> 16) : -1) : sh.w[par][i];
+                        if (act && nw != sh.w[par][i]) atomicMin(&sh.fc[par], i);
+                        sh.w[par ^ 1][i] = (int16_t)nw;
+                        sh.code[par ^ 1][i] = 0;
+                    }
+                } else if (sub == 0 && i < c1) {
                     int code;
                     int nw;
                     if (act) {
@@ -569,7 +728,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                             if (dk > cl_key(sh, sh.cl[i][kR - 1])) { win = dk; wc = dc; }
                             else { code = 1; DG(sh.why[i] = 2;) }
                         } else if (fl & kFlFull) {   // exhausted list: D must beat the list's last key
-                            if (dk > sh.thr[i]) { win = dk; wc = dc; }
+                            if (dk > ws.cl_thr[i]) { win = dk; wc = dc; }
                             else { code = 1; DG(sh.why[i] = 3;) }
                         } else {
                             win = dk; wc = dc;
@@ -594,11 +753,15 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
             // D: convergence; clear this sweep's masks and the next sweep's accumulators
             const int fcv = sh.fc[par];
             fsv = sh.fs[par];
-            if (wold >= 0) sh.cmask[wold] = 0;
             if (tid == 0) { sh.fc[par ^ 1] = INT_MAX; sh.fs[par ^ 1] = INT_MAX; }
             __syncthreads();
             DG(acc_ph[3] += dstamp() - q3;)
             par ^= 1;
+            if (sonly) {
+                if (fcv == INT_MAX) { sonly = false; lo = c0; }  // full sweeps recompute every pod
+                else lo = fcv + 1;
+                continue;
+            }
             if (fcv == INT_MAX || fcv >= fsv) break;
             lo = fcv + 1;
         }
@@ -614,19 +777,18 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
         __syncthreads();
         const bool cut = sh.cut < cend;
         if (cut) cend = sh.cut;
+        // the masks hold the last sweep's guesses (= the final winners before cend)
+        const uint64_t keep = cend - c0 >= 64 ? ~0ull : ((1ull << (cend - c0)) - 1ull);
         int wk = -1;
         if (tid < kC) {
             const int i = c0 + tid;
-            if (i < cend) {
-                wk = sh.w[par][i];
-                sh.wf[i] = (int16_t)wk;
-                if (wk >= 0) atomicOr((unsigned long long*)&sh.cmask[wk], 1ull << tid);
-            }
+            if (i < c1) wk = sh.w[par ^ 1][i];
+            if (i < cend) sh.wf[i] = (int16_t)sh.w[par][i];
         }
-        __syncthreads();
         if (wk >= 0 && __builtin_ctzll(sh.cmask[wk]) == tid) {
-            uint64_t m = sh.cmask[wk];
+            uint64_t m = sh.cmask[wk] & keep;
             int tail = sh.ftail[wk];
+            if (m && sh.fcur[wk] < 0) sh.fcur[wk] = (int16_t)(c0 + __builtin_ctzll(m));
             while (m) {
                 const int j = c0 + __builtin_ctzll(m);
                 m &= m - 1;
@@ -638,7 +800,8 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
             sh.ftail[wk] = (int16_t)tail;
         }
         __syncthreads();
-        if (wk >= 0) sh.cmask[wk] = 0;
+        if (wk >= 0) { sh.cmask[wk] = 0; sh.dirty[wk] = 0; }
+        if (tid < kC && c0 + tid < c1) { sh.w[0][c0 + tid] = -1; sh.w[1][c0 + tid] = -1; }
         __syncthreads();
         DG(acc_fin += dstamp() - t2;)
         if (cend < c1) {
@@ -672,7 +835,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
         if (ws.ex_ok[x]) gptr(a.expired)[ws.ex_q[x]] = 1;
     for (int k = tid; k < ncid; k += kThreads) {
         if (k < n_e || sh.fhead[k] >= 0) {
-            const NS32 v = replay(sh, k, n_e, false, 0, 0, -1, c, false);
+            const NS32 v = replay(sh, k, n_e, tb, false, 0, 0, -1, c).v;
             const int32_t n = sh.cnode[k];
             a.s.rc[n] = v.rc; a.s.rm[n] = v.rm; a.s.rg[n] = v.rg; a.s.nr[n] = v.nr;
         }
@@ -704,6 +867,8 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
         atomicAdd(&d[22], (unsigned long long)n_e);
         atomicAdd(&d[23], (unsigned long long)nb);
         for (int q = 0; q < 4; ++q) atomicAdd(&d[24 + q], acc_ph[q]);
+        atomicAdd(&d[28], (unsigned long long)n_sonly);
+        atomicAdd(&d[29], sub1); atomicAdd(&d[30], sub2); atomicAdd(&d[31], sub3);
     }
 #endif
 }

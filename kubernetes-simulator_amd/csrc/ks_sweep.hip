@@ -168,11 +168,25 @@ __global__ __launch_bounds__(kPrepThreads) void sweep_prep_kernel(const EngineAr
         atomicAdd(&cnt[k_of], 1);
     }
     __syncthreads();
-    if (tid == 0) {  // prefix of the counts (n_e <= 1024: serial is fine once per batch)
-        int acc = 0;
-        for (int k = 0; k < n_e; ++k) { ws.e_off[k] = acc; acc += cnt[k]; }
-        ws.e_off[n_e] = acc;
+    {  // exclusive prefix of the counts (n_e <= kPrepThreads: one per thread; wave scans + wave sums)
+        __shared__ int32_t wsum[kPrepThreads / 64];
+        const int lane = tid & 63, wv = tid >> 6;
+        const int v = tid < n_e ? cnt[tid] : 0;
+        int incl = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int u = __shfl_up(incl, o);
+            if (lane >= o) incl += u;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        int base = 0;
+        for (int g = 0; g < wv; ++g) base += wsum[g];
+        if (tid < n_e) ws.e_off[tid] = base + incl - v;
+        if (tid == n_e - 1) ws.e_off[n_e] = base + incl;
+        if (n_e == 0 && tid == 0) ws.e_off[0] = 0;
     }
+    static_assert(kSweepMaxSlots <= kPrepThreads, "one E node per thread");
     __syncthreads();
     if (my_node >= 0) ws.e_slot[ws.e_off[k_of] + atomicAdd(&fill[k_of], 1)] = tid;  // slot x == tid here
     __syncthreads();

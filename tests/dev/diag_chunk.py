@@ -28,6 +28,7 @@ print(f"launches {L}, pods/launch {d[6] / L:.1f} (batch {d[23] / L:.1f}), sweeps
 print("early stops by reason (unknown/rebound, buf ovf, trunc, exhausted, adm unknown, notfound/bad):", [int(x) for x in d[9:15]])
 print("cycles per launch: setup %.0f, cache %.0f, sweeps %.0f (%.0f per sweep), finalize %.0f, commit %.0f" % (
     d[16] / L, d[17] / L, d[18] / L, d[18] / max(d[7], 1), d[19] / L, d[20] / L))
-print("sweep phases, cycles per sweep: A marks %.0f, B replay %.0f, C decide %.0f, D converge %.0f" % tuple(d[24 + q] / max(d[7], 1) for q in range(4)))
+print("exclusion-only rounds/launch %.1f; phases, cycles per round (both kinds): A marks %.0f, B replay %.0f, C decide %.0f, D converge %.0f" % ((d[28] / L,) + tuple(d[24 + q] / max(d[7] + d[28], 1) for q in range(4))))
+print("setup split: loads %.0f, candidate ids %.0f, records %.0f" % (d[29] / L, d[30] / L, d[31] / L))
 nl = max(st["launches"], 1)
 print(f"resolve {st['resolve_ms'] / nl * 1e3:.1f} us/launch (prep + cl + chunk kernels), scan {st['scan_ms'] / nl * 1e3:.1f}, other {st['other_ms'] / nl * 1e3:.1f}")
