@@ -415,17 +415,32 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
         constexpr int kPP = 64, kTPP = kThreads / kPP, kEPT = (kR + kTPP - 1) / kTPP;  // 8 threads, 3 entries
         static_assert(kTPP * kPP == kThreads, "threads per phase pod");
         const int pl = tid / kTPP, sub = tid % kTPP;
+        // every phase's keys loaded up front (one global round instead of one per phase); phase
+        // f covers pods [f ? 64 f - 63 : 0, 64 f + 1)
+        constexpr int kPh = (kB + kPP - 1) / kPP + 1;
+        uint64_t keys[kPh][kEPT];
+#pragma unroll
+        for (int f = 0; f < kPh; ++f) {
+            const int i = f ? kPP * (f - 1) + 1 + pl : pl;
+            const int pn = f ? kPP * f + 1 : 1;
+            const int nc = i < pn && i < nb ? sh.clcnt[i] : 0;
+#pragma unroll
+            for (int q = 0; q < kEPT; ++q) {
+                const int r = sub + kTPP * q;
+                keys[f][q] = r < nc ? ws.cl_key[i][r] : 0ull;
+            }
+        }
         // phases: pod 0 alone (always fits), then 64 pods at a time
-        for (int p0 = 0, pn = 1; p0 < nb; p0 = pn, pn = p0 + kPP) {
+#pragma unroll
+        for (int f = 0; f < kPh; ++f) {
+            const int p0 = f ? kPP * (f - 1) + 1 : 0, pn = f ? kPP * f + 1 : 1;
+            if (p0 >= nb) break;
             const int i = p0 + pl;
             const bool mine = i < pn && i < nb;
             const int nc = mine ? sh.clcnt[i] : 0;
             uint64_t key[kEPT];
 #pragma unroll
-            for (int q = 0; q < kEPT; ++q) {
-                const int r = sub + kTPP * q;
-                key[q] = r < nc ? ws.cl_key[i][r] : 0ull;
-            }
+            for (int q = 0; q < kEPT; ++q) key[q] = keys[f][q];
             // room check (uniform): the keys so far + every entry of this phase
             if (tid == 0) sh.cut = 0;
             __syncthreads();
@@ -487,16 +502,25 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
     nb = sh.nbc < nb ? sh.nbc : nb;
     const int ncid = sh.ncid < kCid ? sh.ncid : kCid;
     DG(uint64_t ts2 = dstamp();)
-    for (int k = tid; k < ncid; k += kThreads) {
-        const int32_t n = sh.cnode[k];
-        const NodeV v = load_node(a.s, n);
-        sh.rs[0][k] = (int32_t)v.ac; sh.rs[1][k] = (int32_t)v.am; sh.rs[2][k] = (int32_t)v.ag; sh.rs[3][k] = clamp32(v.ap);
-        sh.rd[0][k] = (int32_t)v.rc; sh.rd[1][k] = (int32_t)v.rm; sh.rd[2][k] = (int32_t)v.rg; sh.rd[3][k] = (int32_t)v.nr;
-        sh.rt[k] = v.taint; sh.rl[k] = v.label;
-        sh.cmask[k] = 0;
-        sh.fhead[k] = -1; sh.ftail[k] = -1; sh.fcur[k] = -1;
-        sh.ecur[k] = k < n_e ? (uint16_t)sh.eoff[k] : 0;
-        sh.dirty[k] = 0;
+    static_assert(kCid <= 2 * kThreads, "two records per thread");
+    {  // both records' loads issued before either is stored
+        const int k0 = tid, k1 = tid + kThreads;
+        NodeV v0{}, v1{};
+        if (k0 < ncid) v0 = load_node(a.s, sh.cnode[k0]);
+        if (k1 < ncid) v1 = load_node(a.s, sh.cnode[k1]);
+#pragma unroll
+        for (int z = 0; z < 2; ++z) {
+            const int k = z ? k1 : k0;
+            const NodeV& v = z ? v1 : v0;
+            if (k >= ncid) continue;
+            sh.rs[0][k] = (int32_t)v.ac; sh.rs[1][k] = (int32_t)v.am; sh.rs[2][k] = (int32_t)v.ag; sh.rs[3][k] = clamp32(v.ap);
+            sh.rd[0][k] = (int32_t)v.rc; sh.rd[1][k] = (int32_t)v.rm; sh.rd[2][k] = (int32_t)v.rg; sh.rd[3][k] = (int32_t)v.nr;
+            sh.rt[k] = v.taint; sh.rl[k] = v.label;
+            sh.cmask[k] = 0;
+            sh.fhead[k] = -1; sh.ftail[k] = -1; sh.fcur[k] = -1;
+            sh.ecur[k] = k < n_e ? (uint16_t)sh.eoff[k] : 0;
+            sh.dirty[k] = 0;
+        }
     }
     __syncthreads();
 
