@@ -352,6 +352,25 @@ __device__ __forceinline__ uint64_t key_at(const EngineArgs& a, const ChShared& 
     return make_key(eval_t<kMode>(a.c, p, n), (uint32_t)sh.cnode[k]);
 }
 
+// The same, 0 when the float upper bound of the total (prune_tmax: filters ignored, exact slack)
+// says the key stays below lb — most (pod, node) pairs: the full evaluator runs only for the rest.
+template <int kMode>
+__device__ __forceinline__ uint64_t key_at_lb(const EngineArgs& a, const ChShared& sh, const PodRec& p, int i, int k,
+                                              int sl, const SRow& r, uint64_t lb) {
+    int s = 0;
+#pragma unroll
+    for (int q = 1; q < kSeg; ++q) s += r.m(q) <= i;
+    const int4 st = *reinterpret_cast<const int4*>(&sh.sst[sl][s][0]);
+    NS32 n;
+    n.ac = sh.rs[0][k]; n.am = sh.rs[1][k]; n.ag = sh.rs[2][k]; n.ap = sh.rs[3][k];
+    n.rc = st.x; n.rm = st.y; n.rg = st.z; n.nr = st.w;
+    const uint32_t node = (uint32_t)sh.cnode[k];
+    const PruneF f = prune_prep_t<kMode>(a.c, n);
+    if (!f.live || make_key(prune_tmax(a.c, f, (float)p.req[0], (float)p.req[1]) + 1u, node) < lb) return 0;
+    n.taint = sh.rt[k]; n.label = sh.rl[k];
+    return make_key(eval_t<kMode>(a.c, p, n), node);
+}
+
 __device__ __forceinline__ uint64_t cl_key(const ChShared& sh, uint32_t e) {
     return ((uint64_t)(e & 0xFFFFu) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)sh.cnode[e >> 16]);
 }
@@ -562,6 +581,9 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                 const int i = c0 + lane;
                 const bool li = i < c1;
                 const PodRec p = sh.pod[li ? i : c0];
+                // a cached key below thr_i never decides pod i: a winner from the static list is
+                // >= thr_i, and without one D must beat thr_i (or the last kept entry, >= thr_i)
+                const uint64_t lbc = li ? ws.cl_thr[i] : 0ull;
                 uint64_t k1 = 0, k2 = 0;
                 int16_t q1 = -1, q2 = -1;
                 bool bad = false;
@@ -580,7 +602,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                         const int k = r[q].m(kMCid);
                         if (k < 0 || !li) continue;
                         if (r[q].m(kMOvf) <= i) { bad = true; continue; }
-                        const uint64_t key = key_at<kMode>(a, sh, p, i, k, j, r[q]);
+                        const uint64_t key = key_at_lb<kMode>(a, sh, p, i, k, j, r[q], lbc);
                         if (key > k1) { k2 = k1; q2 = q1; k1 = key; q1 = (int16_t)k; }
                         else if (key > k2) { k2 = key; q2 = (int16_t)k; }
                     }
@@ -685,7 +707,9 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                 int dc = -1;
                 bool bad = false;
                 if (act && !sonly) {
-                    // the chunk's first binders j = c0 + sub + 16 q before pod i: rows together
+                    // the chunk's first binders j = c0 + sub + 8 q before pod i: rows together
+                    // (no float-bound pruning here: measured slower — in SIMT the exact
+                    // evaluation still runs whenever one lane of the wave passes the bound)
                     const PodRec p = sh.pod[i];
                     constexpr int NQ = kC / G;
                     SRow r[NQ];
