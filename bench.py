@@ -125,10 +125,12 @@ def stream_copy_gbs(device: int, mib: int = 2048, reps: int = 10):
 
 
 # the kernels of one batch round (ks_step: expire_head -> scan -> merge -> resolve); every
-# resolver variant counts as "resolve"
+# resolver variant counts as "resolve" (the chunk resolver is three kernels: window prep,
+# candidate lists, the resolver proper)
 BATCH_KERNELS = {"ks::expire_head_kernel": "expire_head", "ks::scan_kernel": "scan", "ks::merge_kernel": "merge",
                  "ks::resolve_kernel": "resolve", "ks::pr::resolve_pair_kernel": "resolve",
-                 "ks::resolve_pair_kernel": "resolve"}
+                 "ks::resolve_pair_kernel": "resolve", "ks::sw::sweep_prep_kernel": "resolve",
+                 "ks::chk::chunk_cl_kernel": "resolve", "ks::chk::resolve_chunk_kernel": "resolve"}
 
 
 def load_traffic(config: str = "c3"):
@@ -144,7 +146,7 @@ def load_traffic(config: str = "c3"):
     for k, v in d.get("per_kernel", {}).items():
         role = BATCH_KERNELS.get(k)
         if role and "FETCH_SIZE_KB_avg" in v and "WRITE_SIZE_KB_avg" in v:
-            per[role] = int((2 * v["FETCH_SIZE_KB_avg"] + v["WRITE_SIZE_KB_avg"]) * 1024)
+            per[role] = per.get(role, 0) + int((2 * v["FETCH_SIZE_KB_avg"] + v["WRITE_SIZE_KB_avg"]) * 1024)
     if "scan" not in per:
         return None
     return {"per_kernel": per, "per_batch": sum(per.values()), "source": d.get("source", p),
@@ -167,7 +169,8 @@ def roofline_block(value, st, nodes, config, stream_gbs=None):
     res_ns_pod = st["resolve_ms"] * 1e6 / max(st["pods"], 1)
     per = tr["per_kernel"] if tr else {}
     return {
-        "bound": "latency (resolve kernel: one workgroup per batch walks its pods in FIFO order)",
+        "bound": "latency (resolver: one workgroup per batch reaches the FIFO-sequential binds by chunked "
+                 "Jacobi sweeps, barrier-separated rounds)",
         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": achieved / HBM_PEAK_GBS if achieved is not None else None,
         "traffic": tr["per_batch"] if tr else None,
@@ -188,7 +191,8 @@ def roofline_block(value, st, nodes, config, stream_gbs=None):
             "resolve": {"ms": res_ms, "hbm_bytes": per.get("resolve"), "ns_per_pod": res_ns_pod,
                         "cycles_per_pod_at_2_4ghz": res_ns_pod * 2.4,
                         "share_of_device_time": res_ms / dev_ms if dev_ms > 0 else None,
-                        "bound": "latency: dependent per-pair decision chain in one workgroup"},
+                        "bound": "latency: barrier-separated sweep rounds in one workgroup (window prep + "
+                                 "candidate lists + chunk kernel)"},
             "merge_and_expire_head": {"ms": st["other_ms"] / launches,
                                       "hbm_bytes": (per.get("merge") or 0) + (per.get("expire_head") or 0) or None},
         },

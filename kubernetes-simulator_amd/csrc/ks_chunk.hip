@@ -671,7 +671,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                     sh.smeta[j][kMCid] = -1;
                 }
             }
-            __syncthreads();
+            if (!sonly) __syncthreads();  // (exclusion-only rounds replay nothing)
             DG(uint64_t q2 = dstamp(); acc_ph[1] += q2 - q1;)
             // C: pod i = c0 + tid / 8, 8 lanes each
             {
@@ -801,8 +801,10 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
             // D: convergence; clear this sweep's masks and the next sweep's accumulators
             const int fcv = sh.fc[par];
             fsv = sh.fs[par];
+            // No barrier here: the next round's accumulators (par ^ 1) are only written after its
+            // phase-A barrier, which tid 0 reaches after this reset; this round's (par) are reset
+            // two rounds on, after every thread has passed the next phase-A barrier.
             if (tid == 0) { sh.fc[par ^ 1] = INT_MAX; sh.fs[par ^ 1] = INT_MAX; }
-            __syncthreads();
             DG(acc_ph[3] += dstamp() - q3;)
             par ^= 1;
             if (sonly) {
@@ -813,7 +815,6 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
             if (fcv == INT_MAX || fcv >= fsv) break;
             lo = fcv + 1;
         }
-        if (tid == 0) { sh.fc[0] = sh.fc[1] = INT_MAX; sh.fs[0] = sh.fs[1] = INT_MAX; }
         DG(uint64_t t2 = dstamp(); acc_sw += t2 - t1;)
 
         // (3) finalize the chunk's prefix [c0, cend): admissions known, final bind lists
@@ -823,6 +824,8 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
             if (i < cend && sh.adm[i] == 2) atomicMin(&sh.cut, i);
         }
         __syncthreads();
+        // every thread has read this chunk's last accumulators (before the barrier above)
+        if (tid == 0) { sh.fc[0] = sh.fc[1] = INT_MAX; sh.fs[0] = sh.fs[1] = INT_MAX; }
         const bool cut = sh.cut < cend;
         if (cut) cend = sh.cut;
         // the masks hold the last sweep's guesses (= the final winners before cend)

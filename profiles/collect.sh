@@ -11,6 +11,10 @@ ROOT=$(pwd)
 DB=/tmp/ks_prof   # result databases (large): scratch, summaries go to OUT
 mkdir -p "$OUT" "$DB"
 export TMPDIR=/tmp
+# heartbeat under OUT (a profiled run prints nothing for minutes; gpurun takes silence for a hang)
+( while true; do date +%T >> "$OUT/heartbeat.txt"; sleep 30; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 B="$ROOT/bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-c5"
 cd /tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$DB/c3" -o run -- python3 $B > "$ROOT/$OUT/c3_bench.json"
