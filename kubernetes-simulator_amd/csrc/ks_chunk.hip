@@ -375,6 +375,17 @@ __device__ __forceinline__ uint64_t cl_key(const ChShared& sh, uint32_t e) {
     return ((uint64_t)(e & 0xFFFFu) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)sh.cnode[e >> 16]);
 }
 
+// candidate id k's record (int32 state, taint, label) and its per-batch bookkeeping
+__device__ __forceinline__ void store_rec(ChShared& sh, int k, int n_e, const NodeV& v) {
+    sh.rs[0][k] = (int32_t)v.ac; sh.rs[1][k] = (int32_t)v.am; sh.rs[2][k] = (int32_t)v.ag; sh.rs[3][k] = clamp32(v.ap);
+    sh.rd[0][k] = (int32_t)v.rc; sh.rd[1][k] = (int32_t)v.rm; sh.rd[2][k] = (int32_t)v.rg; sh.rd[3][k] = (int32_t)v.nr;
+    sh.rt[k] = v.taint; sh.rl[k] = v.label;
+    sh.cmask[k] = 0;
+    sh.fhead[k] = -1; sh.ftail[k] = -1; sh.fcur[k] = -1;
+    sh.ecur[k] = k < n_e ? (uint16_t)sh.eoff[k] : 0;
+    sh.dirty[k] = 0;
+}
+
 template <int kMode>
 __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArgs* __restrict__ A) {
     __shared__ ChShared sh;
@@ -387,7 +398,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
     const int n_e = ws.n_e, e_cnt = ws.e_cnt;
 
     // ---- setup: pods, window, candidate ids, records
-    DG(uint64_t t_setup = dstamp(); uint64_t acc_cd = 0, acc_sw = 0, acc_fin = 0, acc_ph[4] = {0, 0, 0, 0}; int n_sweeps = 0, n_sonly = 0, n_chunks = 0;)
+    DG(uint64_t t_setup = dstamp(); uint64_t acc_cd = 0, acc_sw = 0, acc_fin = 0, acc_ph[4] = {0, 0, 0, 0}, acc_cs = 0, acc_rb = 0, acc_cdp = 0; int n_sweeps = 0, n_sonly = 0, n_chunks = 0;)
     if (tid == 0) { sh.ncid = n_e; sh.nbc = nb; sh.cut = INT_MAX; sh.fc[0] = sh.fc[1] = INT_MAX; sh.fs[0] = sh.fs[1] = INT_MAX; }
     for (int h = tid; h < kHash; h += kThreads) sh.u.h.hk[h] = -1;
     if (tid < nb) {
@@ -422,6 +433,11 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
     // in pod order), so the batch is cut exactly before the first pod whose nodes do not fit
     // kCid — pod 0 always fits (its <= L entries beside <= kSlots E nodes).  A phase starts only
     // when the hash has room for all its entries.
+    // records are loaded by the thread that claims the id and stored once the id is known, so
+    // their HBM round trips overlap the id phases (E: one per thread, stored after the phases)
+    static_assert(kSlots <= kThreads, "one E node per thread");
+    NodeV erec{};
+    if (tid < n_e) erec = load_node(a.s, ws.e_node[tid]);
     if (tid < n_e) {  // distinct (the prep kernel's E)
         const int32_t node = ws.e_node[tid];
         uint32_t h = hslot(node);
@@ -470,6 +486,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
             if (!room) { if (tid == 0) atomicMin(&sh.nbc, p0); break; }
             int slot[kEPT];
             int claims = 0;
+            NodeV rec[kEPT];
 #pragma unroll
             for (int q = 0; q < kEPT; ++q) {
                 slot[q] = -1;
@@ -483,6 +500,9 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                     h = (h + 1) & (kHash - 1);
                 }
             }
+#pragma unroll
+            for (int q = 0; q < kEPT; ++q)
+                if (slot[q] >= 0 && (slot[q] & (1 << 30))) rec[q] = load_node(a.s, key_node(key[q]));
             // exclusive prefix of the claims in thread (= pod, entry) order
             int incl = claims;
 #pragma unroll
@@ -500,7 +520,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                 if (slot[q] >= 0 && (slot[q] & (1 << 30))) {
                     const int h = slot[q] & ~(1 << 30);
                     sh.u.h.hv[h] = c;
-                    if (c < kCid) sh.cnode[c] = key_node(key[q]);
+                    if (c < kCid) { sh.cnode[c] = key_node(key[q]); store_rec(sh, c, n_e, rec[q]); }
                     ++c;
                 }
             __syncthreads();
@@ -521,26 +541,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
     nb = sh.nbc < nb ? sh.nbc : nb;
     const int ncid = sh.ncid < kCid ? sh.ncid : kCid;
     DG(uint64_t ts2 = dstamp();)
-    static_assert(kCid <= 2 * kThreads, "two records per thread");
-    {  // both records' loads issued before either is stored
-        const int k0 = tid, k1 = tid + kThreads;
-        NodeV v0{}, v1{};
-        if (k0 < ncid) v0 = load_node(a.s, sh.cnode[k0]);
-        if (k1 < ncid) v1 = load_node(a.s, sh.cnode[k1]);
-#pragma unroll
-        for (int z = 0; z < 2; ++z) {
-            const int k = z ? k1 : k0;
-            const NodeV& v = z ? v1 : v0;
-            if (k >= ncid) continue;
-            sh.rs[0][k] = (int32_t)v.ac; sh.rs[1][k] = (int32_t)v.am; sh.rs[2][k] = (int32_t)v.ag; sh.rs[3][k] = clamp32(v.ap);
-            sh.rd[0][k] = (int32_t)v.rc; sh.rd[1][k] = (int32_t)v.rm; sh.rd[2][k] = (int32_t)v.rg; sh.rd[3][k] = (int32_t)v.nr;
-            sh.rt[k] = v.taint; sh.rl[k] = v.label;
-            sh.cmask[k] = 0;
-            sh.fhead[k] = -1; sh.ftail[k] = -1; sh.fcur[k] = -1;
-            sh.ecur[k] = k < n_e ? (uint16_t)sh.eoff[k] : 0;
-            sh.dirty[k] = 0;
-        }
-    }
+    if (tid < n_e) store_rec(sh, tid, n_e, erec);
     __syncthreads();
 
     // ---- chunks
@@ -577,6 +578,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                 else sh.smeta[j][kMCid] = -1;
             }
             __syncthreads();
+            DG(uint64_t tr1 = dstamp(); acc_rb += tr1 - t0;)
             {
                 const int i = c0 + lane;
                 const bool li = i < c1;
@@ -611,6 +613,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                 sh.u.x.c[wave][lane][0] = q1; sh.u.x.c[wave][lane][1] = q2;
             }
             __syncthreads();
+            DG(acc_cdp += dstamp() - tr1;)
             if (wave == 0) {
                 uint64_t k1 = 0, k2 = 0;
                 int16_t q1 = -1, q2 = -1;
@@ -797,7 +800,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                 }
             }
             __syncthreads();
-            DG(uint64_t q3 = dstamp(); acc_ph[2] += q3 - q2;)
+            DG(uint64_t q3 = dstamp(); if (sonly) acc_cs += q3 - q2; else acc_ph[2] += q3 - q2;)
             // D: convergence; clear this sweep's masks and the next sweep's accumulators
             const int fcv = sh.fc[par];
             fsv = sh.fs[par];
@@ -861,7 +864,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
 #ifdef KS_CHUNK_DIAG
             if (tid == 0) {
                 unsigned long long* d = (unsigned long long*)a.ctr;
-                const int r = cut ? 4 : (stop_code == 1 ? sh.why[cend] : 5);
+                const int r = cut ? 4 : (stop_code == 1 ? sh.why[cend] : 4);  // (4: adm unknown or NotFound/bad)
                 atomicAdd(&d[9 + r], 1ull);
             }
 #endif
@@ -915,10 +918,12 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
         atomicAdd(&d[19], acc_fin);
         atomicAdd(&d[20], dstamp() - t3);
         atomicAdd(&d[21], (unsigned long long)ncid);
-        atomicAdd(&d[22], (unsigned long long)n_e);
+        atomicAdd(&d[22], acc_cdp);
+        atomicAdd(&d[14], acc_rb);
         atomicAdd(&d[23], (unsigned long long)nb);
         for (int q = 0; q < 4; ++q) atomicAdd(&d[24 + q], acc_ph[q]);
         atomicAdd(&d[28], (unsigned long long)n_sonly);
+        atomicAdd(&d[15], acc_cs);
         atomicAdd(&d[29], sub1); atomicAdd(&d[30], sub2); atomicAdd(&d[31], sub3);
     }
 #endif

@@ -18,7 +18,10 @@ trap 'kill $HB 2>/dev/null' EXIT
 B="$ROOT/bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-c5"
 cd /tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$DB/c3" -o run -- python3 $B > "$ROOT/$OUT/c3_bench.json"
+if [ -z "${SKIP_C4:-}" ]; then
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$DB/c4" -o run -- python3 "$ROOT/bench.py" --config c4 --steps 2 --warmup 1 > "$ROOT/$OUT/c4_bench.json"
+fi
+echo "c3/c4 traces done"
 timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE -d "$DB/fetch" -o run -- python3 $B --steps 2 > /dev/null
 timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE -d "$DB/write" -o run -- python3 $B --steps 2 > /dev/null
 timeout -k 10 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$DB/sq" -o run -- python3 $B --steps 2 > /dev/null
@@ -31,7 +34,7 @@ python3 profiles/db_summary.py stats "$DB/c5/run_results.db" "$OUT/c5_kernel_sta
 python3 profiles/db_summary.py pmc "$DB/c5fetch/run_results.db" "$DB/c5write/run_results.db" "" \
     "$OUT/pmc_c5.json" "rocprofv3 --pmc passes over bench.py --config c5 --steps 2 --warmup 1 (C5, 1M nodes), MI355X"
 python3 profiles/db_summary.py stats "$DB/c3/run_results.db" "$OUT/c3_kernel_stats.csv"
-python3 profiles/db_summary.py stats "$DB/c4/run_results.db" "$OUT/c4_kernel_stats.csv"
+[ -z "${SKIP_C4:-}" ] && python3 profiles/db_summary.py stats "$DB/c4/run_results.db" "$OUT/c4_kernel_stats.csv"
 python3 profiles/db_summary.py pmc "$DB/fetch/run_results.db" "$DB/write/run_results.db" "$DB/sq/run_results.db" \
     "$OUT/pmc_c3.json" "rocprofv3 --pmc passes over bench.py --steps 2 --warmup 1 (C3), MI355X"
 rm -rf "$DB"
