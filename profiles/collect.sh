@@ -22,13 +22,20 @@ if [ -z "${SKIP_C4:-}" ]; then
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$DB/c4" -o run -- python3 "$ROOT/bench.py" --config c4 --steps 2 --warmup 1 > "$ROOT/$OUT/c4_bench.json"
 fi
 echo "c3/c4 traces done"
-timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE -d "$DB/fetch" -o run -- python3 $B --steps 2 > /dev/null
-timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE -d "$DB/write" -o run -- python3 $B --steps 2 > /dev/null
-timeout -k 10 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$DB/sq" -o run -- python3 $B --steps 2 > /dev/null
+# PMC passes serialise every dispatch: a short step (8,192 pods, ~40 batch rounds) keeps each pass
+# within its limit; the summaries are per-launch averages
+P="$B --steps 1 --pods-per-step 8192"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$DB/fetch" -o run -- python3 $P > /dev/null
+echo "fetch pass done"
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$DB/write" -o run -- python3 $P > /dev/null
+echo "write pass done"
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$DB/sq" -o run -- python3 $P > /dev/null
+echo "sq pass done"
 C5="$ROOT/bench.py --config c5 --steps 2 --warmup 1"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$DB/c5" -o run -- python3 $C5 > "$ROOT/$OUT/c5_bench.json"
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$DB/c5fetch" -o run -- python3 $C5 > /dev/null
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$DB/c5write" -o run -- python3 $C5 > /dev/null
+echo "c5 trace done"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$DB/c5fetch" -o run -- python3 $C5 --steps 1 --warmup 0 > /dev/null
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$DB/c5write" -o run -- python3 $C5 --steps 1 --warmup 0 > /dev/null
 cd "$ROOT"
 python3 profiles/db_summary.py stats "$DB/c5/run_results.db" "$OUT/c5_kernel_stats.csv"
 python3 profiles/db_summary.py pmc "$DB/c5fetch/run_results.db" "$DB/c5write/run_results.db" "" \
