@@ -15,7 +15,7 @@ export TMPDIR=/tmp
 ( while true; do date +%T >> "$OUT/heartbeat.txt"; sleep 30; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
-B="$ROOT/bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-c5"
+B="$ROOT/bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-c5 --no-dropin"
 cd /tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$DB/c3" -o run -- python3 $B > "$ROOT/$OUT/c3_bench.json"
 if [ -z "${SKIP_C4:-}" ]; then
@@ -32,17 +32,21 @@ echo "write pass done"
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$DB/sq" -o run -- python3 $P > /dev/null
 echo "sq pass done"
 C5="$ROOT/bench.py --config c5 --steps 2 --warmup 1"
+if [ -z "${SKIP_C5:-}" ]; then
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$DB/c5" -o run -- python3 $C5 > "$ROOT/$OUT/c5_bench.json"
 echo "c5 trace done"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$DB/c5fetch" -o run -- python3 $C5 --steps 1 --warmup 0 > /dev/null
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$DB/c5write" -o run -- python3 $C5 --steps 1 --warmup 0 > /dev/null
+fi
 cd "$ROOT"
+if [ -z "${SKIP_C5:-}" ]; then
 python3 profiles/db_summary.py stats "$DB/c5/run_results.db" "$OUT/c5_kernel_stats.csv"
 python3 profiles/db_summary.py pmc "$DB/c5fetch/run_results.db" "$DB/c5write/run_results.db" "" \
-    "$OUT/pmc_c5.json" "rocprofv3 --pmc passes over bench.py --config c5 --steps 2 --warmup 1 (C5, 1M nodes), MI355X"
+    "$OUT/pmc_c5.json" "rocprofv3 --pmc passes over bench.py --config c5 --steps 1 --warmup 0 (C5, 1M nodes), MI355X"
+fi
 python3 profiles/db_summary.py stats "$DB/c3/run_results.db" "$OUT/c3_kernel_stats.csv"
 [ -z "${SKIP_C4:-}" ] && python3 profiles/db_summary.py stats "$DB/c4/run_results.db" "$OUT/c4_kernel_stats.csv"
 python3 profiles/db_summary.py pmc "$DB/fetch/run_results.db" "$DB/write/run_results.db" "$DB/sq/run_results.db" \
-    "$OUT/pmc_c3.json" "rocprofv3 --pmc passes over bench.py --steps 2 --warmup 1 (C3), MI355X"
+    "$OUT/pmc_c3.json" "rocprofv3 --pmc passes over bench.py --steps 1 --warmup 1 --pods-per-step 8192 --no-c5 --no-dropin (C3), MI355X"
 rm -rf "$DB"
 echo "profiles collected in $OUT"
