@@ -207,7 +207,7 @@ def main():
     ap.add_argument("--pods-per-step", type=int, default=32768)
     ap.add_argument("--nodes", type=int, default=50_000)
     ap.add_argument("--pods", type=int, default=1_000_000)
-    ap.add_argument("--batch", type=int, default=0, help="pods per scan/resolve batch (0 = engine default)")
+    ap.add_argument("--batch", type=int, default=0, help="pods per scan/resolve batch (0 = engine default: 192 on the chunk resolver)")
     ap.add_argument("--cpu-sample-pods", type=int, default=40000)
     ap.add_argument("--cpu-budget-s", type=float, default=12.0, help="per CPU-baseline leg (multi-core, single-thread)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -341,7 +341,7 @@ def main():
                                    " -> Score(LR+BA) -> argmax -> bind, 1 pod/tick",
                        "nodes": nodes, "pods_per_step": S, "trace_pods": n_pods,
                        "parallelism": "replicas" if world > 1 else "single-gpu",
-                       "batch_pods": args.batch or 256},
+                       "batch_pods": args.batch or 192},
             "pods_per_s": pods_per_s,
             "roofline": roofline_block(value, st, nodes, "c3", stream_copy_gbs(local)),
             "kernels": {"launches_per_step": launches, "pods_per_launch": pods_per_launch,
@@ -606,7 +606,7 @@ def _c5_leg_body(args, rank, world, local, dist, steps=None, warmup=1):
                                "argmax -> bind, node-sharded scan, per-batch RCCL candidate all-gather",
                    "nodes": nodes, "pods_per_step": S, "trace_pods": n_pods,
                    "parallelism": f"node-shards/{world}" + (f"x{args.vshards}v" if args.vshards > 1 else ""),
-                   "batch_pods": args.batch or 256},
+                   "batch_pods": args.batch or 192},
         "kernels": {"launches_per_step": launches, "pods_per_launch": st["pods"] / launches,
                     "scan_avg_ms": st["scan_ms"] / launches, "resolve_avg_ms": st["resolve_ms"] / launches,
                     "other_avg_ms": st["other_ms"] / launches, "profiled_step_ms": st["step_ms"]},

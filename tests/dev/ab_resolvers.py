@@ -1,6 +1,6 @@
 """A/B of the resolvers on the C3 bench workload (and C5 with --c5): per-launch resolve / scan /
 other device time (HIP events), pods per launch, wall pods/s and a CRC of the binds (must agree).
-    python tests/dev/ab_resolvers.py [--c5] [one_pod pair sweep sweep:8 ...]   (sweep:N = KS_SWEEPS=N)"""
+    python tests/dev/ab_resolvers.py [--c5] [one_pod pair sweep sweep:8 chunk@224 ...]   (sweep:N = KS_SWEEPS=N, @B = batch)"""
 import os, sys, time, zlib
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -18,12 +18,14 @@ tr = tracegen.c5_trace(n_pods=120_000) if c5 else tracegen.c3_trace(n_pods=200_0
 enc = encode.encode_trace(tr)
 for rep in range(2):
     for nm in names:
-        base, _, sw = nm.partition(":")
+        nm0, _, bp = nm.partition("@")  # name@B: batch of B pods
+        base, _, sw = nm0.partition(":")
         if sw:
             os.environ["KS_SWEEPS"] = sw
         else:
             os.environ.pop("KS_SWEEPS", None)
-        eng = Engine(tick_seconds=10, filter_mode=1, filters=7, scorers=((1, 1, 0), (2, 1, 0)), engine_flags=FLAGS[base])
+        eng = Engine(tick_seconds=10, filter_mode=1, filters=7, scorers=((1, 1, 0), (2, 1, 0)), engine_flags=FLAGS[base],
+                     batch_pods=int(bp) if bp else 0)
         eng.load_nodes(enc["alloc"], enc["taint"], enc["label"])
         eng.submit(enc["pods"])
         eng.step(32768)

@@ -10,4 +10,4 @@ timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" || exit 
 timeout -k 10 400 python -u bench.py > gpurun_out/b_r3.json 2> gpurun_out/b_r3.log
 rc=$?; echo "bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
 python3 -c "import json; d=json.load(open('gpurun_out/b_r3.json')); print(d['value'], d['pods_per_s'], d['ms_per_step'], d['c5_sharded']['value'])"
-bash profiles/collect.sh gpurun_out/prof_r03
+SKIP_C4=1 bash profiles/collect.sh gpurun_out/prof_r03
