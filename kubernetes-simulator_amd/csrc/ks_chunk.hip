@@ -136,7 +136,16 @@ __global__ __launch_bounds__(256) void chunk_cl_kernel(const EngineArgs* __restr
         const uint64_t me = buf[tid];
         int r = 0;
         for (int u = 0; u < n; ++u) r += buf[u] > me;
-        if (r < kR) ws.cl_key[i][r] = me;
+        if (r < kR) {
+            // the chunk kernel reads its candidate records from here: one coalesced row per id
+            // instead of ten scattered gathers on one CU
+            ws.cl_key[i][r] = me;
+            const NodeV v = load_node(a.s, key_node(me));
+            uint4* o = ws.cl_rec[i][r];
+            o[0] = make_uint4((uint32_t)(int32_t)v.ac, (uint32_t)(int32_t)v.am, (uint32_t)(int32_t)v.ag, (uint32_t)clamp32(v.ap));
+            o[1] = make_uint4((uint32_t)(int32_t)v.rc, (uint32_t)(int32_t)v.rm, (uint32_t)(int32_t)v.rg, (uint32_t)(int32_t)v.nr);
+            o[2] = make_uint4((uint32_t)v.taint, (uint32_t)(v.taint >> 32), (uint32_t)v.label, (uint32_t)(v.label >> 32));
+        }
     }
     if (tid == 0) {
         ws.cl_info[i] = (c < kR ? c : kR) | (c > kR ? kClTrunc : 0) | (full ? kClFull : 0) | (c > kClBuf ? kClOvf : 0);
@@ -375,15 +384,28 @@ __device__ __forceinline__ uint64_t cl_key(const ChShared& sh, uint32_t e) {
     return ((uint64_t)(e & 0xFFFFu) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)sh.cnode[e >> 16]);
 }
 
-// candidate id k's record (int32 state, taint, label) and its per-batch bookkeeping
-__device__ __forceinline__ void store_rec(ChShared& sh, int k, int n_e, const NodeV& v) {
-    sh.rs[0][k] = (int32_t)v.ac; sh.rs[1][k] = (int32_t)v.am; sh.rs[2][k] = (int32_t)v.ag; sh.rs[3][k] = clamp32(v.ap);
-    sh.rd[0][k] = (int32_t)v.rc; sh.rd[1][k] = (int32_t)v.rm; sh.rd[2][k] = (int32_t)v.rg; sh.rd[3][k] = (int32_t)v.nr;
-    sh.rt[k] = v.taint; sh.rl[k] = v.label;
+// candidate id k's per-batch bookkeeping
+__device__ __forceinline__ void store_book(ChShared& sh, int k, int n_e) {
     sh.cmask[k] = 0;
     sh.fhead[k] = -1; sh.ftail[k] = -1; sh.fcur[k] = -1;
     sh.ecur[k] = k < n_e ? (uint16_t)sh.eoff[k] : 0;
     sh.dirty[k] = 0;
+}
+
+// candidate id k's record (int32 state, taint, label) and its bookkeeping
+__device__ __forceinline__ void store_rec(ChShared& sh, int k, int n_e, const NodeV& v) {
+    sh.rs[0][k] = (int32_t)v.ac; sh.rs[1][k] = (int32_t)v.am; sh.rs[2][k] = (int32_t)v.ag; sh.rs[3][k] = clamp32(v.ap);
+    sh.rd[0][k] = (int32_t)v.rc; sh.rd[1][k] = (int32_t)v.rm; sh.rd[2][k] = (int32_t)v.rg; sh.rd[3][k] = (int32_t)v.nr;
+    sh.rt[k] = v.taint; sh.rl[k] = v.label;
+    store_book(sh, k, n_e);
+}
+
+// the same from a packed candidate-list record (chunk_cl_kernel)
+__device__ __forceinline__ void store_prec(ChShared& sh, int k, int n_e, const uint4* r) {
+    sh.rs[0][k] = (int32_t)r[0].x; sh.rs[1][k] = (int32_t)r[0].y; sh.rs[2][k] = (int32_t)r[0].z; sh.rs[3][k] = (int32_t)r[0].w;
+    sh.rd[0][k] = (int32_t)r[1].x; sh.rd[1][k] = (int32_t)r[1].y; sh.rd[2][k] = (int32_t)r[1].z; sh.rd[3][k] = (int32_t)r[1].w;
+    sh.rt[k] = r[2].x | ((uint64_t)r[2].y << 32); sh.rl[k] = r[2].z | ((uint64_t)r[2].w << 32);
+    store_book(sh, k, n_e);
 }
 
 template <int kMode>
@@ -427,14 +449,12 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
     // slot x is applied from the first pod i >= 1 with win_hi[i] > x
     for (int i = tid + 1; i < nb; i += kThreads)
         for (int x = sh.win_hi[i - 1]; x < sh.win_hi[i]; ++x) sh.xeff[x] = (int16_t)i;
-    // candidate ids: E nodes are cids 0 .. n_e - 1; then every list node, claimed by CAS
     // Candidate ids: E nodes are cids 0 .. n_e - 1; list nodes are numbered in (pod, entry) order,
     // 64 pods per phase (claim by CAS, exclusive prefix of the claims over the threads, which run
     // in pod order), so the batch is cut exactly before the first pod whose nodes do not fit
     // kCid — pod 0 always fits (its <= L entries beside <= kSlots E nodes).  A phase starts only
     // when the hash has room for all its entries.
-    // records are loaded by the thread that claims the id and stored once the id is known, so
-    // their HBM round trips overlap the id phases (E: one per thread, stored after the phases)
+    // records are loaded after the phases (E: one per thread, issued before them)
     static_assert(kSlots <= kThreads, "one E node per thread");
     NodeV erec{};
     if (tid < n_e) erec = load_node(a.s, ws.e_node[tid]);
@@ -486,7 +506,6 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
             if (!room) { if (tid == 0) atomicMin(&sh.nbc, p0); break; }
             int slot[kEPT];
             int claims = 0;
-            NodeV rec[kEPT];
 #pragma unroll
             for (int q = 0; q < kEPT; ++q) {
                 slot[q] = -1;
@@ -500,9 +519,6 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                     h = (h + 1) & (kHash - 1);
                 }
             }
-#pragma unroll
-            for (int q = 0; q < kEPT; ++q)
-                if (slot[q] >= 0 && (slot[q] & (1 << 30))) rec[q] = load_node(a.s, key_node(key[q]));
             // exclusive prefix of the claims in thread (= pod, entry) order
             int incl = claims;
 #pragma unroll
@@ -520,7 +536,10 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                 if (slot[q] >= 0 && (slot[q] & (1 << 30))) {
                     const int h = slot[q] & ~(1 << 30);
                     sh.u.h.hv[h] = c;
-                    if (c < kCid) { sh.cnode[c] = key_node(key[q]); store_rec(sh, c, n_e, rec[q]); }
+                    if (c < kCid) {  // fhead holds the (pod, entry) of the id's record until store_prec
+                        sh.cnode[c] = key_node(key[q]);
+                        sh.fhead[c] = (int16_t)(i * kR + sub + kTPP * q);
+                    }
                     ++c;
                 }
             __syncthreads();
@@ -542,6 +561,19 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
     const int ncid = sh.ncid < kCid ? sh.ncid : kCid;
     DG(uint64_t ts2 = dstamp();)
     if (tid < n_e) store_rec(sh, tid, n_e, erec);
+    // list-node records: one pass after the id phases over the packed rows chunk_cl_kernel wrote
+    // (two ids per thread, 48 contiguous bytes each), so the phases carry no HBM round trip
+    static_assert(kCid <= 2 * kThreads, "two list records per thread");
+    static_assert(kB * kR <= 32767, "(pod, entry) index in int16");
+    {
+        const int k1 = n_e + tid, k2 = k1 + kThreads;
+        const uint4* rows = &ws.cl_rec[0][0][0];
+        uint4 r1[3], r2[3];
+        if (k1 < ncid) { const uint4* q = rows + 3 * sh.fhead[k1]; r1[0] = q[0]; r1[1] = q[1]; r1[2] = q[2]; }
+        if (k2 < ncid) { const uint4* q = rows + 3 * sh.fhead[k2]; r2[0] = q[0]; r2[1] = q[1]; r2[2] = q[2]; }
+        if (k1 < ncid) store_prec(sh, k1, n_e, r1);
+        if (k2 < ncid) store_prec(sh, k2, n_e, r2);
+    }
     __syncthreads();
 
     // ---- chunks

@@ -572,6 +572,8 @@ struct SweepWS {
     uint64_t cl_key[kSweepMaxB][kChR];
     int32_t cl_info[kSweepMaxB];          // kept count | kClTrunc | kClFull | kClOvf
     uint64_t cl_thr[kSweepMaxB];          // the list's last key when full, else 1
+    // entry r's node record, packed: {ac am ag ap} {rc rm rg nr} as int32, {taint label} as u64 pairs
+    uint4 cl_rec[kSweepMaxB][kChR][3];
 };
 
 // Arguments of the batch kernels (expire_head / scan / resolve).
