@@ -471,39 +471,41 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
         static_assert(kTPP * kPP == kThreads, "threads per phase pod");
         const int pl = tid / kTPP, sub = tid % kTPP;
         // every phase's keys loaded up front (one global round instead of one per phase); phase
-        // f covers pods [f ? 64 f - 63 : 0, 64 f + 1)
-        constexpr int kPh = (kB + kPP - 1) / kPP + 1;
+        // f covers pods [64 f, 64 f + 64)
+        constexpr int kPh = (kB + kPP - 1) / kPP;
         uint64_t keys[kPh][kEPT];
 #pragma unroll
         for (int f = 0; f < kPh; ++f) {
-            const int i = f ? kPP * (f - 1) + 1 + pl : pl;
-            const int pn = f ? kPP * f + 1 : 1;
-            const int nc = i < pn && i < nb ? sh.clcnt[i] : 0;
+            const int i = kPP * f + pl;
+            const int nc = i < nb ? sh.clcnt[i] : 0;
 #pragma unroll
             for (int q = 0; q < kEPT; ++q) {
                 const int r = sub + kTPP * q;
                 keys[f][q] = r < nc ? ws.cl_key[i][r] : 0ull;
             }
         }
-        // phases: pod 0 alone (always fits), then 64 pods at a time
+        // phases of 64 pods; when the first lacks hash room, pod 0 alone (always fits:
+        // n_e <= kSlots plus <= kR entries) and the batch is cut after it
+        static_assert(kSlots + kR <= kHash - kWave, "pod 0 alone always fits the hash");
 #pragma unroll
         for (int f = 0; f < kPh; ++f) {
-            const int p0 = f ? kPP * (f - 1) + 1 : 0, pn = f ? kPP * f + 1 : 1;
+            const int p0 = kPP * f, pn0 = p0 + kPP;
             if (p0 >= nb) break;
             const int i = p0 + pl;
-            const bool mine = i < pn && i < nb;
-            const int nc = mine ? sh.clcnt[i] : 0;
-            uint64_t key[kEPT];
-#pragma unroll
-            for (int q = 0; q < kEPT; ++q) key[q] = keys[f][q];
             // room check (uniform): the keys so far + every entry of this phase
             if (tid == 0) sh.cut = 0;
             __syncthreads();
-            if (sub == 0 && nc) atomicAdd(&sh.cut, nc);
+            if (sub == 0 && i < nb) atomicAdd(&sh.cut, (int)sh.clcnt[i]);
             __syncthreads();
             const bool room = sh.ncid + sh.cut <= kHash - kWave;
             __syncthreads();
-            if (!room) { if (tid == 0) atomicMin(&sh.nbc, p0); break; }
+            if (!room && f > 0) { if (tid == 0) atomicMin(&sh.nbc, p0); break; }
+            const int pn = room ? pn0 : 1;
+            if (!room && tid == 0) atomicMin(&sh.nbc, 1);
+            const bool mine = i < pn && i < nb;
+            uint64_t key[kEPT];
+#pragma unroll
+            for (int q = 0; q < kEPT; ++q) key[q] = mine ? keys[f][q] : 0ull;
             int slot[kEPT];
             int claims = 0;
 #pragma unroll
@@ -552,7 +554,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                 else sh.cl[i][sub + kTPP * q] = ((uint32_t)cid << 16) | (uint32_t)(key[q] >> 32);
             }
             __syncthreads();
-            if (sh.nbc < pn) break;
+            if (sh.nbc < pn0) break;
         }
         if (tid == 0) sh.cut = INT_MAX;
     }
