@@ -466,6 +466,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
         sh.cnode[tid] = node;
     }
     __shared__ int32_t wsum[kWaves];
+    DG(uint64_t sub_k = 0;)
     {
         constexpr int kPP = 64, kTPP = kThreads / kPP, kEPT = (kR + kTPP - 1) / kTPP;  // 8 threads, 3 entries
         static_assert(kTPP * kPP == kThreads, "threads per phase pod");
@@ -484,6 +485,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                 keys[f][q] = r < nc ? ws.cl_key[i][r] : 0ull;
             }
         }
+        DG(__syncthreads(); sub_k = dstamp() - ts1;)
         // phases of 64 pods; when the first lacks hash room, pod 0 alone (always fits:
         // n_e <= kSlots plus <= kR entries) and the batch is cut after it
         static_assert(kSlots + kR <= kHash - kWave, "pod 0 alone always fits the hash");
@@ -958,7 +960,8 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
         for (int q = 0; q < 4; ++q) atomicAdd(&d[24 + q], acc_ph[q]);
         atomicAdd(&d[28], (unsigned long long)n_sonly);
         atomicAdd(&d[15], acc_cs);
-        atomicAdd(&d[29], sub1); atomicAdd(&d[30], sub2); atomicAdd(&d[31], sub3);
+        // d[29] low: loads, high: E inserts + list keys
+        atomicAdd(&d[29], sub1 + (sub_k << 32)); atomicAdd(&d[30], sub2); atomicAdd(&d[31], sub3);
     }
 #endif
 }
