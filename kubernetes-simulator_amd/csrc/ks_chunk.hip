@@ -421,7 +421,9 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
 
     // ---- setup: pods, window, candidate ids, records
     DG(uint64_t t_setup = dstamp(); uint64_t acc_cd = 0, acc_sw = 0, acc_fin = 0, acc_ph[4] = {0, 0, 0, 0}, acc_cs = 0, acc_rb = 0, acc_cdp = 0; int n_sweeps = 0, n_sonly = 0, n_chunks = 0;)
+    __shared__ int32_t fcnt[4];  // list entries per 64-pod id phase
     if (tid == 0) { sh.ncid = n_e; sh.nbc = nb; sh.cut = INT_MAX; sh.fc[0] = sh.fc[1] = INT_MAX; sh.fs[0] = sh.fs[1] = INT_MAX; }
+    if (tid < 4) fcnt[tid] = 0;
     for (int h = tid; h < kHash; h += kThreads) sh.u.h.hk[h] = -1;
     if (tid < nb) {
         sh.pod[tid] = a.pods[start + tid];
@@ -474,18 +476,21 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
         // every phase's keys loaded up front (one global round instead of one per phase); phase
         // f covers pods [64 f, 64 f + 64)
         constexpr int kPh = (kB + kPP - 1) / kPP;
+        static_assert(kPh <= 4, "fcnt");
         uint64_t keys[kPh][kEPT];
 #pragma unroll
         for (int f = 0; f < kPh; ++f) {
             const int i = kPP * f + pl;
             const int nc = i < nb ? sh.clcnt[i] : 0;
+            if (sub == 0 && nc) atomicAdd(&fcnt[f], nc);
 #pragma unroll
             for (int q = 0; q < kEPT; ++q) {
                 const int r = sub + kTPP * q;
                 keys[f][q] = r < nc ? ws.cl_key[i][r] : 0ull;
             }
         }
-        DG(__syncthreads(); sub_k = dstamp() - ts1;)
+        __syncthreads();  // fcnt complete; the E inserts precede every list insert
+        DG(sub_k = dstamp() - ts1;)
         // phases of 64 pods; when the first lacks hash room, pod 0 alone (always fits:
         // n_e <= kSlots plus <= kR entries) and the batch is cut after it
         static_assert(kSlots + kR <= kHash - kWave, "pod 0 alone always fits the hash");
@@ -494,13 +499,9 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
             const int p0 = kPP * f, pn0 = p0 + kPP;
             if (p0 >= nb) break;
             const int i = p0 + pl;
-            // room check (uniform): the keys so far + every entry of this phase
-            if (tid == 0) sh.cut = 0;
-            __syncthreads();
-            if (sub == 0 && i < nb) atomicAdd(&sh.cut, (int)sh.clcnt[i]);
-            __syncthreads();
-            const bool room = sh.ncid + sh.cut <= kHash - kWave;
-            __syncthreads();
+            // room check (uniform): the keys so far + every entry of this phase (ncid is rewritten
+            // only after this phase's first barrier)
+            const bool room = sh.ncid + fcnt[f] <= kHash - kWave;
             if (!room && f > 0) { if (tid == 0) atomicMin(&sh.nbc, p0); break; }
             const int pn = room ? pn0 : 1;
             if (!room && tid == 0) atomicMin(&sh.nbc, 1);
