@@ -100,11 +100,10 @@ typedef struct {
 enum { KS_ENGINE_FORCE_WIDE = 1, KS_ENGINE_NO_TINY = 2, KS_ENGINE_NO_MICRO = 4,
        /* resolvers for batches of clusters above the small class (all give the same binds; the
         * flags exist to test them against each other): ONE_POD = the role-split one-pod-per-
-        * barrier resolver; PAIR = two pods per barrier (when every total + 1 < 2^15); SWEEP =
-        * parallel Jacobi sweeps to the sequential fixed point (ks_step only, not groups); CHUNK =
-        * chunked Jacobi sweeps in one workgroup's LDS (ks_step only, evaluator modes >= narrow) */
-       KS_ENGINE_ONE_POD_RESOLVER = 8, KS_ENGINE_PAIR_RESOLVER = 16, KS_ENGINE_SWEEP_RESOLVER = 32,
-       KS_ENGINE_CHUNK_RESOLVER = 64 };
+        * barrier resolver; CHUNK = chunked Jacobi sweeps in one workgroup's LDS (ks_step only,
+        * evaluator modes >= narrow); SEQ = the one-wave FIFO loop over static candidate lists
+        * (ks_step only).  Bits 16 and 32 (the retired pair and sweep resolvers) are rejected. */
+       KS_ENGINE_ONE_POD_RESOLVER = 8, KS_ENGINE_CHUNK_RESOLVER = 64, KS_ENGINE_SEQ_RESOLVER = 128 };
 
 typedef struct {
     int64_t pod;    /* FIFO index (submission order) */

@@ -28,11 +28,11 @@ namespace chk {
 
 constexpr int kThreads = 512;   // 8 waves: 256 VGPRs per lane (no spills)
 constexpr int kLanesPerPod = kThreads / 64;  // sweep phases: 64 chunk pods x 8 lanes
-constexpr int kB = kSweepMaxB;  // pods per batch
+constexpr int kB = kWinMaxB;  // pods per batch
 constexpr int kC = 64;          // pods per chunk: one lane each
 constexpr int kR = kChR;        // static candidates kept per pod
 constexpr int kCid = 1024;      // distinct candidate nodes per batch (E nodes first)
-constexpr int kSlots = kChSlots;
+constexpr int kSlots = kWinSlots;
 constexpr int kSeg = 5;         // stored state segments per replayed node within a chunk
 constexpr int kPend = 4;        // pending own expiries per replayed node
 constexpr int kHashLog2 = 11, kHash = 1 << kHashLog2;
@@ -96,7 +96,7 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
 template <int kMode>
 __global__ __launch_bounds__(256) void chunk_cl_kernel(const EngineArgs* __restrict__ A) {
     const EngineArgs& a = A[0];
-    SweepWS& ws = *a.sw;
+    WinWS& ws = *a.sw;
     const int i = blockIdx.x, tid = threadIdx.x;
     if (i >= ws.nb) return;
     const int64_t start = a.ctr[kCtrStart];
@@ -412,7 +412,7 @@ template <int kMode>
 __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArgs* __restrict__ A) {
     __shared__ ChShared sh;
     const EngineArgs& a = A[0];
-    const SweepWS& ws = *a.sw;
+    const WinWS& ws = *a.sw;
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid >> 6;
     const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
     int nb = ws.nb;
@@ -969,22 +969,20 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
 
 }  // namespace chk
 
-hipError_t launch_sweep_prep(const EngineArgs* d, int max_slots, hipStream_t st);
-
 hipError_t launch_resolve_chunk(const EngineArgs* d, int mode, hipStream_t st) {
-    hipError_t r = launch_sweep_prep(d, kChSlots, st);
+    hipError_t r = launch_window_prep(d, st);
     if (r != hipSuccess) return r;
     switch (mode) {
         case kEvalMicro:
-            hipLaunchKernelGGL(chk::chunk_cl_kernel<kEvalMicro>, dim3(kSweepMaxB), dim3(256), 0, st, d);
+            hipLaunchKernelGGL(chk::chunk_cl_kernel<kEvalMicro>, dim3(kWinMaxB), dim3(256), 0, st, d);
             hipLaunchKernelGGL(chk::resolve_chunk_kernel<kEvalMicro>, dim3(1), dim3(chk::kThreads), 0, st, d);
             break;
         case kEvalTiny:
-            hipLaunchKernelGGL(chk::chunk_cl_kernel<kEvalTiny>, dim3(kSweepMaxB), dim3(256), 0, st, d);
+            hipLaunchKernelGGL(chk::chunk_cl_kernel<kEvalTiny>, dim3(kWinMaxB), dim3(256), 0, st, d);
             hipLaunchKernelGGL(chk::resolve_chunk_kernel<kEvalTiny>, dim3(1), dim3(chk::kThreads), 0, st, d);
             break;
         default:
-            hipLaunchKernelGGL(chk::chunk_cl_kernel<kEvalNarrow>, dim3(kSweepMaxB), dim3(256), 0, st, d);
+            hipLaunchKernelGGL(chk::chunk_cl_kernel<kEvalNarrow>, dim3(kWinMaxB), dim3(256), 0, st, d);
             hipLaunchKernelGGL(chk::resolve_chunk_kernel<kEvalNarrow>, dim3(1), dim3(chk::kThreads), 0, st, d);
             break;
     }

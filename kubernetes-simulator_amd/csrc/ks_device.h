@@ -544,36 +544,32 @@ enum : int64_t { kCtrStart = 0, kCtrEnd = 1, kCtrErr = 2, kCtrErrPod = 3, kCtrEa
 enum : uint32_t { kFlagBadKey = 1, kFlagBadSpec = 2 };
 enum : int64_t { kErrEinval = 1, kErrNotFound = 2 };
 
-// Workspace of the sweep resolver (ks_sweep.hip), one per engine, in HBM.  Sized for batches of
-// up to kSweepMaxB pods whose expiry window holds up to kSweepMaxSlots slots.
-constexpr int kSweepMaxB = 256;
-constexpr int kSweepMaxSlots = 1024;
-constexpr int kSweepMaxSweeps = 24;
-// chunk resolver (ks_chunk.hip): candidate lists of kChR entries per pod, windows of <= kChSlots
-constexpr int kChR = 24;
-constexpr int kChSlots = 512;
+// Batch window workspace, one per engine, in HBM: the expiry window and the static candidate lists
+// of a batch (window_prep_kernel and the candidate-list kernels, ks_seq.hip), read by the chunk and
+// sequential resolvers.  Batches of up to kWinMaxB pods whose expiry window holds up to kWinSlots
+// slots.
+constexpr int kWinMaxB = 256;
+constexpr int kWinSlots = 512;
+constexpr int kChR = 24;    // static candidates kept per pod
+constexpr int kRecDw = 24;  // a static candidate's staged record, dwords (the widest format, ks_seq.hip)
 enum : int32_t { kClTrunc = 1 << 8, kClFull = 1 << 9, kClOvf = 1 << 10 };
-struct SweepWS {
+struct WinWS {
     int32_t nb, e_cnt, n_e, pad_;
-    int32_t win_hi[kSweepMaxB];           // pod i: expiry slots < win_hi[i] are applied before it binds
-    int32_t own[kSweepMaxB];              // pod i's own expiry slot in the window, or -1
-    int32_t w[2][kSweepMaxB];             // winners of the last two sweeps (node, -1 none)
-    int32_t code[2][kSweepMaxB];          // 0 ok, 1 list exhausted, 2 NotFound, 3 bad pod key / spec
-    int32_t fc[kSweepMaxSweeps];          // sweep s: first pod whose result changed (INT32_MAX: none)
-    int32_t fs[kSweepMaxSweeps];          // sweep s: first pod with a stop code (INT32_MAX: none)
-    int32_t ran[kSweepMaxSweeps];         // sweep s executed
-    int32_t ex_q[kSweepMaxSlots];         // slot -> expiring pod
-    int32_t ex_ok[kSweepMaxSlots];        // pre-batch pod bound Ok and not expired yet
-    int64_t ex_req[kSweepMaxSlots][3];
-    int32_t e_node[kSweepMaxSlots];       // distinct nodes of the pre-batch expiries (E)
-    int32_t e_off[kSweepMaxSlots + 1];    // E node k's slots: e_slot[e_off[k] .. e_off[k+1]) ascending
-    int32_t e_slot[kSweepMaxSlots];
-    // chunk resolver: pod i's static candidates (chunk_cl_kernel), sorted descending
-    uint64_t cl_key[kSweepMaxB][kChR];
-    int32_t cl_info[kSweepMaxB];          // kept count | kClTrunc | kClFull | kClOvf
-    uint64_t cl_thr[kSweepMaxB];          // the list's last key when full, else 1
+    int32_t win_hi[kWinMaxB];             // pod i: expiry slots < win_hi[i] are applied before it binds
+    int32_t own[kWinMaxB];                // pod i's own expiry slot in the window, or -1
+    int32_t ex_q[kWinSlots];              // slot -> expiring pod
+    int32_t ex_ok[kWinSlots];             // pre-batch pod bound Ok and not expired yet
+    int64_t ex_req[kWinSlots][3];
+    int32_t e_node[kWinSlots];            // distinct nodes of the pre-batch expiries (E)
+    int32_t e_off[kWinSlots + 1];         // E node k's slots: e_slot[e_off[k] .. e_off[k+1]) ascending
+    int32_t e_slot[kWinSlots];
+    // pod i's static candidates, sorted descending
+    uint64_t cl_key[kWinMaxB][kChR];
+    int32_t cl_info[kWinMaxB];            // kept count | kClTrunc | kClFull | kClOvf
+    uint64_t cl_thr[kWinMaxB];            // the list's last key when full, else 1
     // entry r's node record, packed: {ac am ag ap} {rc rm rg nr} as int32, {taint label} as u64 pairs
-    uint4 cl_rec[kSweepMaxB][kChR][3];
+    uint4 cl_rec[kWinMaxB][kChR][3];      // (chunk resolver)
+    uint32_t sq_rec[kWinMaxB][kChR][kRecDw];  // (sequential resolver, ks_seq.hip)
 };
 
 // Arguments of the batch kernels (expire_head / scan / resolve).
@@ -596,8 +592,8 @@ struct EngineArgs {
     int32_t nblk;            // 256-node scan blocks (whole cluster; the lists' stride)
     int32_t blk_lo;          // this rank's scan range [blk_lo, blk_lo + blk_n) (node sharding)
     int32_t blk_n;
-    SweepWS* sw;             // sweep resolver workspace (nullptr unless allocated)
-    int32_t* e_idx;          // [n_pad] node -> index in the sweep's E, -1 otherwise
+    WinWS* sw;               // batch window workspace (nullptr unless allocated)
+    int32_t* e_idx;          // [n_pad] node -> index in the window's E, -1 otherwise
 };
 
 // Launchers and limits (defined in ks_kernels.hip).  The batch launchers take a device array of
@@ -623,18 +619,14 @@ hipError_t launch_resolve(const EngineArgs* d, int S, int mode, hipStream_t st);
 hipError_t launch_resolve_small(const EngineArgs* d, int S, int mode, hipStream_t st);
 int small_resolver_max_batch();
 int small_resolver_max_nodes();
-// the pair resolver (ks_pair.hip): two pods per barrier, batches of <= pair_resolver_max_batch()
-// pods, any cluster, when every total + 1 < 2^15 (its decision words carry a second total)
-hipError_t launch_resolve_pair(const EngineArgs* d, int S, int mode, hipStream_t st);
-int pair_resolver_max_batch();
-// the sweep resolver (ks_sweep.hip): parallel Jacobi sweeps to the sequential fixed point, one
-// engine (S = 1), batches of <= kSweepMaxB pods; `sweeps` kernels are queued, the ones after
-// convergence exit at once
-hipError_t launch_resolve_sweep(const EngineArgs* d, int mode, int sweeps, hipStream_t st);
-// the chunk resolver (ks_chunk.hip): one engine (S = 1), batches of <= kSweepMaxB pods, evaluator
+// the chunk resolver (ks_chunk.hip): one engine (S = 1), batches of <= kWinMaxB pods, evaluator
 // modes >= kEvalNarrow (node state in int32) and every total + 1 < 2^16
 hipError_t launch_resolve_chunk(const EngineArgs* d, int mode, hipStream_t st);
-constexpr int64_t kPairTotalCap = 1LL << 15;
+// the sequential resolver (ks_seq.hip): one engine (S = 1), batches of <= kWinMaxB pods, any
+// evaluator mode
+hipError_t launch_resolve_seq(const EngineArgs* d, int mode, hipStream_t st);
+// the batch window (expiries of the batch's pods, the node set E): the resolvers' first kernel
+hipError_t launch_window_prep(const EngineArgs* d, hipStream_t st);
 struct BindSeg {
     const int32_t* node;
     const int32_t* status;
@@ -643,6 +635,51 @@ struct BindSeg {
 hipError_t launch_gather_binds(const BindSeg* segs, int S, int64_t max_n, int32_t* node, int32_t* status,
                                hipStream_t st);
 hipError_t launch_rescale(const NodeSoA& s, int64_t n_pad, PodRec* pods, int64_t P, const int64_t f[3], hipStream_t st);
+
+// Host-staged submits (ks_engine.cpp): copy `bytes` from device-visible pinned host memory to dst.
+struct CopySeg {
+    uint8_t* dst;
+    const uint8_t* src;
+    int64_t bytes;
+};
+hipError_t launch_scatter(const CopySeg* segs, int n, hipStream_t st);
+
+// The per-tick path (ks_tick.hip): one pod, one launch.
+constexpr int kTickMaxExp = 16;  // expiries due before the pod, passed by value
+struct TickExp {
+    int32_t node, q;    // the expiring pod q and its node
+    int64_t req[3];
+};
+struct TickScratch {    // device, zero between launches (the last workgroup resets it)
+    uint64_t best;
+    uint32_t count, pad_;
+};
+struct TickOut {        // host-mapped
+    int32_t node, status, code, pad_;
+};
+struct TickArgs {
+    Cfg c;
+    NodeSoA s;
+    PodRec pod;
+    int64_t j;          // the pod's FIFO index
+    int32_t run;        // bound Ok, it counts toward the node's totals (dur > 0)
+    int32_t n_exp;
+    TickExp exp[kTickMaxExp];
+    int32_t* b_node;
+    int32_t* b_status;
+    uint8_t* expired;
+    TickScratch* scr;
+    TickOut* out;
+    const CopySeg* segs;  // host-staged submits applied by the last workgroup first
+    int32_t n_seg, pad_;
+};
+hipError_t launch_tick(const TickArgs& a, int mode, hipStream_t st);
+struct ExpList {
+    int32_t n, pad_;
+    TickExp x[kTickMaxExp];
+};
+// apply the listed expiries to the node state and mark them expired (ks_filter / ks_score's flush)
+hipError_t launch_apply_exp(const NodeSoA& s, uint8_t* expired, const ExpList& l, hipStream_t st);
 hipError_t launch_eval_pod(const Cfg& c, const NodeSoA& s, const PodRec* pod, uint32_t filters, uint8_t* mask,
                            int64_t* score, int mode, hipStream_t st);
 hipError_t launch_flush(const NodeSoA& s, const PodRec* pods, const int64_t* fin, int64_t t, int64_t n_done,

@@ -52,6 +52,7 @@ constexpr int64_t kMaxValue = 1LL << 59;
 constexpr int kMaxBatch = 256;
 constexpr int kDefaultBatch = 256;
 constexpr int kChunkBatch = 192;  // default batch of engines on the chunk resolver (ks_load_nodes)
+constexpr int64_t kStageMaxPods = 4096;  // submits of up to this many pods are host-staged
 #ifndef KS_PG_MIN_WG
 #define KS_PG_MIN_WG 2048  // scan workgroups to keep when raising the pods per workgroup
 #endif
@@ -139,6 +140,25 @@ struct ks_engine {
     // host mirror of the binds (name-keyed queries): node (-1 = not bound) and status
     std::vector<int32_t> h_node;
     std::vector<int8_t> h_status;
+    // host mirrors the per-tick path passes by value: device-unit pod records, the expiry CSR's
+    // pods, the device's expired flags (exact while err == KS_OK: every expiry attached to a pod
+    // < done has been applied, plus the ones a flush applied)
+    std::vector<ks::PodRec> h_pods;
+    std::vector<int32_t> h_exp_pod;
+    std::vector<uint8_t> h_expired;
+    // host-staged submits: rows for the device arrays in a pinned, device-visible arena, applied by
+    // one scatter (or by the per-tick kernel) before any device work reads them
+    uint8_t* stage = nullptr;           // pinned host arena
+    uint8_t* stage_dev = nullptr;       // its device address
+    int64_t stage_cap = 0, stage_used = 0;
+    ks::CopySeg* segs = nullptr;        // pinned segment table
+    ks::CopySeg* segs_dev = nullptr;
+    int seg_cap = 0, nseg = 0, seg_done = 0;
+    hipEvent_t stage_ev = nullptr;      // recorded after the launch that consumed the last segments
+    // per-tick path (ks_tick.hip)
+    ks::TickScratch* d_tick = nullptr;
+    ks::TickOut* h_tick = nullptr;      // pinned, device-visible
+    ks::TickOut* h_tick_dev = nullptr;
     // name-keyed index over binds [0, idx_upto), extended on each query
     int64_t idx_upto = 0;
     std::vector<std::vector<int64_t>> node_pods;      // per node: every pod bound there, FIFO
@@ -176,9 +196,8 @@ struct ks_engine {
     // scratch for queries
     uint8_t* d_mask = nullptr;
     int64_t* d_score = nullptr;
-    ks::SweepWS* d_sweep = nullptr;  // sweep resolver workspace and node -> E index (n_pad, -1)
+    ks::WinWS* d_sweep = nullptr;    // batch window workspace and node -> E index (n_pad, -1)
     int32_t* d_eidx = nullptr;
-    int sweeps = 12;                 // sweep kernels queued per batch (KS_SWEEPS overrides)
     unsigned long long* d_usage = nullptr;
     DVec<int32_t> d_blk;                  // usage query: candidate pod blocks
     std::vector<int32_t> h_blk;
@@ -239,6 +258,74 @@ ks::EngineArgs make_args(ks_engine* e) {
     return a;
 }
 
+// ---- host-staged submits ---------------------------------------------------------------------
+// Staged rows are applied in submission order by one scatter launch (stage_flush) or by the
+// per-tick kernel, always before the device work that reads them (stream order).  The arena is
+// reused once the launch that consumed its last segment has completed.
+hipError_t stage_flush(ks_engine* e) {
+    if (e->seg_done >= e->nseg) return hipSuccess;
+    hipError_t r = ks::launch_scatter(e->segs_dev + e->seg_done, e->nseg - e->seg_done, e->st);
+    if (r == hipSuccess) r = hipEventRecord(e->stage_ev, e->st);
+    e->seg_done = e->nseg;
+    return r;
+}
+
+// room for `bytes` more in the arena and one more segment
+hipError_t stage_room(ks_engine* e, int64_t bytes) {
+    if (e->nseg > 0 && e->seg_done == e->nseg && hipEventQuery(e->stage_ev) == hipSuccess) {
+        e->stage_used = 0;
+        e->nseg = e->seg_done = 0;
+    }
+    const int64_t need = e->stage_used + bytes + 16;
+    if (need <= e->stage_cap && e->nseg < e->seg_cap) return hipSuccess;
+    hipError_t r = stage_flush(e);
+    if (r == hipSuccess) r = hipStreamSynchronize(e->st);
+    if (r != hipSuccess) return r;
+    e->stage_used = 0;
+    e->nseg = e->seg_done = 0;
+    if (bytes + 16 > e->stage_cap) {
+        if (e->stage) (void)hipHostFree(e->stage);
+        e->stage = nullptr;
+        e->stage_cap = std::max<int64_t>(bytes + 16, std::max<int64_t>(2 * e->stage_cap, 1 << 20));
+        r = hipHostMalloc(&e->stage, e->stage_cap, hipHostMallocMapped);
+        if (r == hipSuccess) r = hipHostGetDevicePointer((void**)&e->stage_dev, e->stage, 0);
+        if (r != hipSuccess) { e->stage = nullptr; e->stage_cap = 0; return r; }
+    }
+    if (e->seg_cap == 0) {
+        e->seg_cap = 1 << 16;
+        r = hipHostMalloc(&e->segs, sizeof(ks::CopySeg) * e->seg_cap, hipHostMallocMapped);
+        if (r == hipSuccess) r = hipHostGetDevicePointer((void**)&e->segs_dev, e->segs, 0);
+        if (r == hipSuccess && !e->stage_ev) r = hipEventCreateWithFlags(&e->stage_ev, hipEventDisableTiming);
+        if (r != hipSuccess) { e->seg_cap = 0; return r; }
+    }
+    return hipSuccess;
+}
+
+// one staged copy of `bytes` host bytes to device address dst
+hipError_t stage_copy(ks_engine* e, void* dst, const void* src, int64_t bytes) {
+    if (bytes <= 0) return hipSuccess;
+    hipError_t r = stage_room(e, bytes);
+    if (r != hipSuccess) return r;
+    std::memcpy(e->stage + e->stage_used, src, bytes);
+    e->segs[e->nseg++] = ks::CopySeg{(uint8_t*)dst, e->stage_dev + e->stage_used, bytes};
+    e->stage_used += (bytes + 15) / 16 * 16;
+    return hipSuccess;
+}
+
+// DVec::append through the arena (growth flushes first: the copy of the old contents must
+// follow the staged rows written into them)
+template <typename T>
+hipError_t stage_append(ks_engine* e, DVec<T>& v, const T* h, int64_t k) {
+    if (v.n + k > v.cap) {
+        hipError_t r = stage_flush(e);
+        if (r == hipSuccess) r = v.reserve(v.n + k, e->st);
+        if (r != hipSuccess) return r;
+    }
+    hipError_t r = stage_copy(e, v.p + v.n, h, sizeof(T) * k);
+    v.n += k;
+    return r;
+}
+
 // every total + 1 fits the scan's 16-bit key table (weights and constant values are >= 0)
 bool key16(const ks_engine* e) {
     return (int64_t)e->dc.const_total + 10 * ((int64_t)e->dc.w_lr + e->dc.w_ba) + 1 < (1 << 16);
@@ -249,34 +336,22 @@ bool small_resolver(const ks_engine* e) {
     return e->B <= ks::small_resolver_max_batch() && e->dc.n_nodes <= ks::small_resolver_max_nodes();
 }
 
-// Two resolvers, the same binds: the role-split resolve_kernel (16 waves, ks_kernels.hip) has the
-// shortest per-pod chain and takes big batches; the register-table resolver (4 waves,
-// ks_resolve.hip) is lighter — four per CU, so a what-if group's resolvers run side by side (C4
-// 2.29e11 against 2.16e11 evals/s with the role-split kernel's half-size class).
-// The pair resolver (ks_pair.hip) decides two pods per barrier; its decision words carry a
-// second total, so it takes engines whose totals + 1 stay below 2^15 (weights and constant
-// values are >= 0).
-bool pair_resolver(const ks_engine* e) {
-    return (e->flags & KS_ENGINE_PAIR_RESOLVER) &&
-           (int64_t)e->dc.const_total + 10 * ((int64_t)e->dc.w_lr + e->dc.w_ba) + 1 < ks::kPairTotalCap;
-}
-// the sweep resolver (ks_sweep.hip): one engine per launch, batches of <= kSweepMaxB pods
-bool sweep_resolver(const ks_engine* e) {
-    return (e->flags & KS_ENGINE_SWEEP_RESOLVER) && e->B <= ks::kSweepMaxB;
-}
-// the chunk resolver (ks_chunk.hip): one engine per launch, batches of <= kSweepMaxB pods, node
-// state in int32 (evaluator modes >= narrow), totals in 16 bits
+// Resolvers, the same binds: the role-split resolve_kernel (16 waves, ks_kernels.hip) takes any
+// engine; the register-table resolver (4 waves, ks_resolve.hip) is lighter — four per CU, so a
+// what-if group's resolvers run side by side (C4 2.29e11 against 2.16e11 evals/s with the
+// role-split kernel's half-size class); the chunk resolver (ks_chunk.hip) and the
+// sequential resolver (ks_seq.hip) take one engine per launch, batches of <= kWinMaxB pods.
+// the chunk resolver: node state in int32 (evaluator modes >= narrow), totals in 16 bits
 bool chunk_eligible(const ks_engine* e) {
-    return e->B <= ks::kSweepMaxB && e->mode >= ks::kEvalNarrow && key16(e);
+    return e->B <= ks::kWinMaxB && e->mode >= ks::kEvalNarrow && key16(e);
 }
-bool chunk_resolver(const ks_engine* e) { return (e->flags & KS_ENGINE_CHUNK_RESOLVER) && chunk_eligible(e); }
-enum Resolver { kResolveRole = 0, kResolveSmall = 1, kResolvePair = 2, kResolveSweep = 3, kResolveChunk = 4 };
+bool seq_eligible(const ks_engine* e) { return e->B <= ks::kWinMaxB; }
+enum Resolver { kResolveRole = 0, kResolveSmall = 1, kResolveChunk = 4, kResolveSeq = 5 };
 // an explicit resolver flag wins over the size class (every resolver is exact on every engine
 // its limits admit; the flags exist to test them against each other)
 int resolver_of(const ks_engine* e) {
-    if (chunk_resolver(e)) return kResolveChunk;
-    if (sweep_resolver(e)) return kResolveSweep;
-    if (pair_resolver(e)) return kResolvePair;
+    if ((e->flags & KS_ENGINE_SEQ_RESOLVER) && seq_eligible(e)) return kResolveSeq;
+    if ((e->flags & KS_ENGINE_CHUNK_RESOLVER) && chunk_eligible(e)) return kResolveChunk;
     if (e->flags & KS_ENGINE_ONE_POD_RESOLVER) return kResolveRole;
     // default: the register-table resolver for the small class, else the chunk resolver where
     // its limits admit the engine (C3: 8.8e5 vs 7.2e5 pods/s with the one-pod kernel), else
@@ -284,12 +359,11 @@ int resolver_of(const ks_engine* e) {
     if (small_resolver(e)) return kResolveSmall;
     return chunk_eligible(e) ? kResolveChunk : kResolveRole;
 }
-hipError_t launch_resolver(const ks::EngineArgs* d, int S, int mode, int which, hipStream_t st, int sweeps = 0) {
+hipError_t launch_resolver(const ks::EngineArgs* d, int S, int mode, int which, hipStream_t st) {
     return which == kResolveSmall ? ks::launch_resolve_small(d, S, mode, st)
-         : which == kResolvePair ? ks::launch_resolve_pair(d, S, mode, st)
-         : which == kResolveSweep ? ks::launch_resolve_sweep(d, mode, sweeps, st)
          : which == kResolveChunk ? ks::launch_resolve_chunk(d, mode, st)
-                                  : ks::launch_resolve(d, S, mode, st);
+         : which == kResolveSeq ? ks::launch_resolve_seq(d, mode, st)
+                                : ks::launch_resolve(d, S, mode, st);
 }
 void update_mode(ks_engine* e) {
     int64_t m[3];
@@ -327,7 +401,7 @@ ks_status engine_init(const ks_config* cfg, ks_engine** out) {
     if (cfg->batch_pods < 0 || cfg->batch_pods > kMaxBatch) return KS_EINVAL;
     if (cfg->engine_flags &
         ~(uint32_t)(KS_ENGINE_FORCE_WIDE | KS_ENGINE_NO_TINY | KS_ENGINE_NO_MICRO | KS_ENGINE_ONE_POD_RESOLVER |
-                    KS_ENGINE_PAIR_RESOLVER | KS_ENGINE_SWEEP_RESOLVER | KS_ENGINE_CHUNK_RESOLVER))
+                    KS_ENGINE_CHUNK_RESOLVER | KS_ENGINE_SEQ_RESOLVER))
         return KS_EINVAL;
     int64_t const_total = 0, w_lr = 0, w_ba = 0;
     for (int i = 0; i < cfg->n_scorers; i++) {
@@ -414,6 +488,11 @@ void engine_free(ks_engine* e) {
     if (e->d_sweep) (void)hipFree(e->d_sweep);
     if (e->d_eidx) (void)hipFree(e->d_eidx);
     if (e->d_usage) (void)hipFree(e->d_usage);
+    if (e->stage) (void)hipHostFree(e->stage);
+    if (e->segs) (void)hipHostFree(e->segs);
+    if (e->stage_ev) (void)hipEventDestroy(e->stage_ev);
+    if (e->d_tick) (void)hipFree(e->d_tick);
+    if (e->h_tick) (void)hipHostFree(e->h_tick);
     for (auto ev : e->ev) if (ev) (void)hipEventDestroy(ev);
     for (auto ev : e->prof_ev) (void)hipEventDestroy(ev);
     if (e->st && !e->group) (void)hipStreamDestroy(e->st);
@@ -550,7 +629,7 @@ ks_status ks_load_nodes(ks_engine* e, int64_t n, const int64_t* alloc, const uin
     // (~215 pods committed): 192 pods binds more per second on C3 (9.96e5 vs 9.12e5 pods/s,
     // 224: 9.53e5, 176: 9.64e5, 128: 9.49e5) and C5 (3.67e5 vs 3.19e5; tests/dev/ab_resolvers.py)
     if (!e->cfg.batch_pods && !small_resolver(e) && chunk_eligible(e) &&
-        !(e->flags & (KS_ENGINE_ONE_POD_RESOLVER | KS_ENGINE_PAIR_RESOLVER | KS_ENGINE_SWEEP_RESOLVER)))
+        !(e->flags & (KS_ENGINE_ONE_POD_RESOLVER | KS_ENGINE_SEQ_RESOLVER)))
         e->B = kChunkBatch;
     // pods per scan workgroup: the most pod reuse per node load that still leaves >= ~2048
     // workgroups (8 per CU) per scan
@@ -564,8 +643,7 @@ ks_status ks_load_nodes(ks_engine* e, int64_t n, const int64_t* alloc, const uin
     if (G > 1) HIPCHK(e, hipMalloc(&e->cand_all, sizeof(uint64_t) * (size_t)G * e->B * ks::kTopL));
     HIPCHK(e, hipMalloc(&e->d_mask, std::max<int64_t>(n, 1)));
     HIPCHK(e, hipMalloc(&e->d_score, sizeof(int64_t) * std::max<int64_t>(n, 1)));
-    if (const char* v = std::getenv("KS_SWEEPS")) e->sweeps = std::max(2, std::min(ks::kSweepMaxSweeps, std::atoi(v)));
-    HIPCHK(e, hipMalloc(&e->d_sweep, sizeof(ks::SweepWS)));
+    HIPCHK(e, hipMalloc(&e->d_sweep, sizeof(ks::WinWS)));
     HIPCHK(e, hipMalloc(&e->d_eidx, sizeof(int32_t) * e->n_pad));
     HIPCHK(e, hipMemsetAsync(e->d_eidx, 0xFF, sizeof(int32_t) * e->n_pad, e->st));
     HIPCHK(e, hipMalloc(&e->d_usage, sizeof(unsigned long long) * 3 * std::max<int64_t>(n, 1)));
@@ -652,8 +730,11 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
         }
         if (any) {
             HIPCHK(e, hipSetDevice(e->device));
+            HIPCHK(e, stage_flush(e));
             HIPCHK(e, ks::launch_rescale(e->s, e->n_pad, e->pods.p, e->P, f, e->st));
             HIPCHK(e, hipStreamSynchronize(e->st));
+            for (ks::PodRec& r : e->h_pods)
+                for (int k = 0; k < 3; k++) r.req[k] *= f[k];
             update_mode(e);
         }
     }
@@ -712,37 +793,64 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
         eoff[i] = e->h_exp_off.back() + (int64_t)epod.size();
         if (d > 0) e->pending.push({fin[i], j});
     }
-    // device uploads
+    // device uploads: small submits (a drop-in's per-tick calls) are staged in pinned memory and
+    // applied by the next launch (no copy call, no synchronisation here); large ones are copied
     hipStream_t st = e->st;
     HIPCHK(e, hipSetDevice(e->device));
-    HIPCHK(e, e->pods.append(recs.data(), m, st));
-    HIPCHK(e, e->dur.append(dur.data(), m, st));
-    HIPCHK(e, e->t0.append(t0.data(), m, st));
-    HIPCHK(e, e->fin.append(fin.data(), m, st));
     std::vector<int32_t> neg(m, -1);
-    HIPCHK(e, e->b_node.append(neg.data(), m, st));
-    HIPCHK(e, e->b_status.append(neg.data(), m, st));
     std::vector<uint8_t> zero(m, 0);
-    HIPCHK(e, e->expired.append(zero.data(), m, st));
-    HIPCHK(e, e->preg.append(reg.data(), m, st));
-    // phase_off holds P+1 entries: overwrite the trailing sentinel
-    if (e->phase_off.n) e->phase_off.n -= 1;
-    HIPCHK(e, e->phase_off.append(poff.data(), m, st));
     const int32_t tail = (int32_t)(e->F + nf);
-    HIPCHK(e, e->phase_off.append(&tail, 1, st));
-    HIPCHK(e, e->cum_sec.append(cum.data(), nf, st));
-    HIPCHK(e, e->use.append(phase_use, nf * 3, st));
-    if (e->exp_off.n == 0) {
-        const int64_t z = 0;
-        HIPCHK(e, e->exp_off.append(&z, 1, st));
+    const int64_t z0 = 0;
+    if (!e->group && m <= kStageMaxPods) {
+        HIPCHK(e, stage_append(e, e->pods, recs.data(), m));
+        HIPCHK(e, stage_append(e, e->dur, dur.data(), m));
+        HIPCHK(e, stage_append(e, e->t0, t0.data(), m));
+        HIPCHK(e, stage_append(e, e->fin, fin.data(), m));
+        HIPCHK(e, stage_append(e, e->b_node, neg.data(), m));
+        HIPCHK(e, stage_append(e, e->b_status, neg.data(), m));
+        HIPCHK(e, stage_append(e, e->expired, zero.data(), m));
+        HIPCHK(e, stage_append(e, e->preg, reg.data(), m));
+        if (e->phase_off.n) e->phase_off.n -= 1;  // phase_off holds P+1 entries: overwrite the sentinel
+        HIPCHK(e, stage_append(e, e->phase_off, poff.data(), m));
+        HIPCHK(e, stage_append(e, e->phase_off, &tail, 1));
+        HIPCHK(e, stage_append(e, e->cum_sec, cum.data(), nf));
+        HIPCHK(e, stage_append(e, e->use, phase_use, nf * 3));
+        if (e->exp_off.n == 0) HIPCHK(e, stage_append(e, e->exp_off, &z0, 1));
+        HIPCHK(e, stage_append(e, e->exp_off, eoff.data(), m));
+        HIPCHK(e, stage_append(e, e->exp_pod, epod.data(), (int64_t)epod.size()));
+        if (e->exp_pos.cap < e->P + m) {
+            HIPCHK(e, stage_flush(e));
+            HIPCHK(e, e->exp_pos.reserve(e->P + m, st));
+        }
+        HIPCHK(e, stage_copy(e, e->exp_pos.p + pos_lo, e->h_exp_pos.data() + pos_lo, sizeof(int64_t) * (e->P + m - pos_lo)));
+        e->exp_pos.n = e->P + m;
+    } else {
+        HIPCHK(e, stage_flush(e));
+        HIPCHK(e, e->pods.append(recs.data(), m, st));
+        HIPCHK(e, e->dur.append(dur.data(), m, st));
+        HIPCHK(e, e->t0.append(t0.data(), m, st));
+        HIPCHK(e, e->fin.append(fin.data(), m, st));
+        HIPCHK(e, e->b_node.append(neg.data(), m, st));
+        HIPCHK(e, e->b_status.append(neg.data(), m, st));
+        HIPCHK(e, e->expired.append(zero.data(), m, st));
+        HIPCHK(e, e->preg.append(reg.data(), m, st));
+        if (e->phase_off.n) e->phase_off.n -= 1;  // phase_off holds P+1 entries: overwrite the sentinel
+        HIPCHK(e, e->phase_off.append(poff.data(), m, st));
+        HIPCHK(e, e->phase_off.append(&tail, 1, st));
+        HIPCHK(e, e->cum_sec.append(cum.data(), nf, st));
+        HIPCHK(e, e->use.append(phase_use, nf * 3, st));
+        if (e->exp_off.n == 0) HIPCHK(e, e->exp_off.append(&z0, 1, st));
+        HIPCHK(e, e->exp_off.append(eoff.data(), m, st));
+        HIPCHK(e, e->exp_pod.append(epod.data(), (int64_t)epod.size(), st));
+        HIPCHK(e, e->exp_pos.reserve(e->P + m, st));
+        HIPCHK(e, hipMemcpyAsync(e->exp_pos.p + pos_lo, e->h_exp_pos.data() + pos_lo, sizeof(int64_t) * (e->P + m - pos_lo),
+                                 hipMemcpyHostToDevice, st));
+        e->exp_pos.n = e->P + m;
+        HIPCHK(e, hipStreamSynchronize(st));  // host staging vectors die here
     }
-    HIPCHK(e, e->exp_off.append(eoff.data(), m, st));
-    HIPCHK(e, e->exp_pod.append(epod.data(), (int64_t)epod.size(), st));
-    HIPCHK(e, e->exp_pos.reserve(e->P + m, st));
-    HIPCHK(e, hipMemcpyAsync(e->exp_pos.p + pos_lo, e->h_exp_pos.data() + pos_lo, sizeof(int64_t) * (e->P + m - pos_lo),
-                             hipMemcpyHostToDevice, st));
-    e->exp_pos.n = e->P + m;
-    HIPCHK(e, hipStreamSynchronize(st));  // host staging vectors die here
+    e->h_pods.insert(e->h_pods.end(), recs.begin(), recs.end());
+    e->h_exp_pod.insert(e->h_exp_pod.end(), epod.begin(), epod.end());
+    e->h_expired.resize(e->P + m, 0);
     e->h_bind_tick.insert(e->h_bind_tick.end(), t0.begin(), t0.end());
     e->h_fin.insert(e->h_fin.end(), fin.begin(), fin.end());
     e->h_dur.insert(e->h_dur.end(), dur.begin(), dur.end());
@@ -850,6 +958,74 @@ ks_status ks_step(ks_engine* e, int64_t ticks, ks_bind* out, int64_t cap, int64_
     return device_stop(e, step_body(e, ticks, out, cap, n_out));
 }
 
+// Expiries attached to pods [lo, hi) have been applied on the device (the batch path applies
+// every expiry attached to a processed pod whose pod was bound Ok): mirror them.
+static void mirror_expired(ks_engine* e, int64_t lo, int64_t hi) {
+    for (int64_t j = lo; j < hi; j++)
+        for (int64_t u = e->h_exp_off[j]; u < e->h_exp_off[j + 1]; u++) {
+            const int32_t q = e->h_exp_pod[u];
+            if (e->h_status[q] == KS_POD_OK) e->h_expired[q] = 1;
+        }
+}
+
+// The per-tick path (ks_tick.hip): exactly one pod binds in this step — one launch does the
+// staged submits, the pod's expiries, the full-cluster evaluation, the argmax and the bind.
+// Returns false (nothing done) when the pod's expiries do not fit the launch's by-value list.
+static bool tick_step(ks_engine* e, int64_t t_end, ks_bind* out, int64_t cap, int64_t* n_out, ks_status* rc) {
+    const int64_t j = e->done;
+    ks::TickArgs a{};
+    for (int64_t u = e->h_exp_off[j]; u < e->h_exp_off[j + 1]; u++) {
+        const int32_t q = e->h_exp_pod[u];
+        if (e->h_status[q] != KS_POD_OK || e->h_expired[q]) continue;
+        if (a.n_exp == ks::kTickMaxExp) return false;
+        ks::TickExp& x = a.exp[a.n_exp++];
+        x.node = e->h_node[q];
+        x.q = q;
+        for (int k = 0; k < 3; k++) x.req[k] = e->h_pods[q].req[k];
+    }
+    *rc = KS_OK;
+    if (!e->d_tick) {
+        hipError_t r = hipMalloc(&e->d_tick, sizeof(ks::TickScratch));
+        if (r == hipSuccess) r = hipMemsetAsync(e->d_tick, 0, sizeof(ks::TickScratch), e->st);
+        if (r == hipSuccess) r = hipHostMalloc(&e->h_tick, sizeof(ks::TickOut), hipHostMallocMapped);
+        if (r == hipSuccess) r = hipHostGetDevicePointer((void**)&e->h_tick_dev, e->h_tick, 0);
+        if (r == hipSuccess && !e->stage_ev) r = hipEventCreateWithFlags(&e->stage_ev, hipEventDisableTiming);
+        if (r != hipSuccess) { *rc = fail(e, KS_EDEVICE, "per-tick path setup: %s", hipGetErrorString(r)); return true; }
+    }
+    a.c = e->dc;
+    a.s = e->s;
+    a.pod = e->h_pods[j];
+    a.j = j;
+    a.run = e->h_dur[j] > 0;
+    a.b_node = e->b_node.p;
+    a.b_status = e->b_status.p;
+    a.expired = e->expired.p;
+    a.scr = e->d_tick;
+    a.out = e->h_tick_dev;
+    a.segs = e->segs_dev + e->seg_done;
+    a.n_seg = e->nseg - e->seg_done;
+    e->seg_done = e->nseg;
+    e->h_tick->code = -1;
+    hipError_t r = ks::launch_tick(a, e->mode, e->st);
+    if (r == hipSuccess) r = hipEventRecord(e->stage_ev, e->st);
+    if (r == hipSuccess) r = hipStreamSynchronize(e->st);
+    if (r != hipSuccess) { *rc = fail(e, KS_EDEVICE, "per-tick launch: %s", hipGetErrorString(r)); return true; }
+    ks::TickOut o;
+    o.node = ((volatile ks::TickOut*)e->h_tick)->node;
+    o.status = ((volatile ks::TickOut*)e->h_tick)->status;
+    o.code = ((volatile ks::TickOut*)e->h_tick)->code;
+    for (int k = 0; k < a.n_exp; k++) e->h_expired[a.exp[k].q] = 1;
+    e->stats = ks_step_stats{};
+    e->stats.launches = 1;
+    e->h_ctr[2] = o.code;
+    e->h_ctr[3] = j;
+    if (o.code < 0) { *rc = fail(e, KS_EDEVICE, "per-tick kernel wrote no result"); return true; }
+    const int32_t node = o.node, status = o.status;
+    *rc = step_finish(e, t_end, o.code ? j : j + 1, &node, &status, out, cap, n_out);
+    e->stats.pods = *n_out;
+    return true;
+}
+
 static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t cap, int64_t* n_out) {
     HIPCHK(e, hipSetDevice(e->device));
     const int64_t t_end = e->tick + ticks;
@@ -858,6 +1034,12 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
         e->tick = t_end;
         return KS_OK;
     }
+    if (p_hi == e->done + 1 && !e->group && e->world * e->vsh == 1 && e->n > 0 && !e->profiling) {
+        ks_status rc = KS_OK;
+        if (tick_step(e, t_end, out, cap, n_out, &rc)) return rc;
+    }
+    const int64_t done0 = e->done;
+    HIPCHK(e, stage_flush(e));
     hipStream_t st = e->st;
     HIPCHK(e, hipMemcpyAsync(e->d_ctr, e->h_ctr, 5 * sizeof(int64_t), hipMemcpyHostToDevice, st));
     HIPCHK(e, hipMemcpyAsync(e->d_args, e->h_args, sizeof(ks::EngineArgs), hipMemcpyHostToDevice, st));
@@ -904,7 +1086,7 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
                 HIPCHK(e, ks::launch_merge(d, 1, e->B, e->cand_all, L, G, BL, e->cand, G, st));
             }
             if (ev[3]) HIPCHK(e, hipEventRecord(ev[3], st));
-            HIPCHK(e, launch_resolver(d, 1, e->mode, resolver_of(e), st, e->sweeps));
+            HIPCHK(e, launch_resolver(d, 1, e->mode, resolver_of(e), st));
             if (ev[4]) HIPCHK(e, hipEventRecord(ev[4], st));
             launches++;
         }
@@ -944,7 +1126,9 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
     e->stats.other_ms = other_ms;
     e->stats.launches = launches;
     e->stats.pods = nb;
-    return step_finish(e, t_end, new_done, node.data(), status.data(), out, cap, n_out);
+    const ks_status rc = step_finish(e, t_end, new_done, node.data(), status.data(), out, cap, n_out);
+    if (rc == KS_OK) mirror_expired(e, done0, e->done);
+    return rc;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1064,14 +1248,14 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
     std::vector<int64_t> p_hi(S, 0), t_end(S, 0);
     std::vector<char> live(S, 0), part(S, 0);  // part: takes part in this step
     int mode = ks::kEvalMicro, blk_n = 0, B = 0;  // B: the largest member batch (grid size)
-    bool k16 = true, small = true, pair = true;
+    bool k16 = true, small = true;
     for (ks_engine* e : g->engs) {
         B = std::max(B, e->B);
         k16 = k16 && key16(e);
         small = small && small_resolver(e);
-        pair = pair && pair_resolver(e);  // (no sweep resolver in groups: it takes one engine)
     }
-    const int which = small ? kResolveSmall : pair ? kResolvePair : kResolveRole;
+    // (the chunk and sequential resolvers take one engine per launch: not in groups)
+    const int which = small ? kResolveSmall : kResolveRole;
     int64_t blocks = 0;
     for (int i = 0; i < S; i++) {
         ks_engine* e = g->engs[i];
@@ -1235,7 +1419,45 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
     return KS_OK;
 }
 
+// Apply every not-yet-applied expiry with finish tick <= the current tick (ks_filter / ks_score
+// see the state Run's next scheduleOne would).  While the run is live the host knows them
+// exactly: every expiry attached to a pod < done has been applied (mirror_expired), an expiry
+// attached to a later pod j > done finishes after bind_tick[j - 1] >= bind_tick[done] > tick, so
+// only the next pod's attached expiries and the unattached ones (pending, when every submitted pod
+// is bound) can be due — usually none, and no launch is made.
 static ks_status flush_expiries(ks_engine* e) {
+    if (e->err == KS_OK) {
+        std::vector<int32_t> qs;
+        auto add = [&](int64_t q) {
+            if (e->h_status[q] == KS_POD_OK && !e->h_expired[q] && e->h_fin[q] <= e->tick) qs.push_back((int32_t)q);
+        };
+        if (e->done < e->P)
+            for (int64_t u = e->h_exp_off[e->done]; u < e->h_exp_off[e->done + 1]; u++) add(e->h_exp_pod[u]);
+        if (!e->pending.empty() && e->pending.top().first <= e->tick) {
+            auto pq = e->pending;
+            while (!pq.empty() && pq.top().first <= e->tick) {
+                add(pq.top().second);
+                pq.pop();
+            }
+        }
+        if ((int)qs.size() <= ks::kTickMaxExp) {
+            if (!qs.empty()) {
+                ks::ExpList L{};
+                for (int32_t q : qs) {
+                    ks::TickExp& x = L.x[L.n++];
+                    x.node = e->h_node[q];
+                    x.q = q;
+                    for (int k = 0; k < 3; k++) x.req[k] = e->h_pods[q].req[k];
+                }
+                HIPCHK(e, ks::launch_apply_exp(e->s, e->expired.p, L, e->st));
+            }
+        } else {
+            HIPCHK(e, ks::launch_flush(e->s, e->pods.p, e->fin.p, e->tick, e->done, e->b_node.p, e->b_status.p,
+                                       e->expired.p, e->st));
+        }
+        for (int32_t q : qs) e->h_expired[q] = 1;
+        return KS_OK;
+    }
     HIPCHK(e, ks::launch_flush(e->s, e->pods.p, e->fin.p, e->tick, e->done, e->b_node.p, e->b_status.p,
                                e->expired.p, e->st));
     return KS_OK;
@@ -1245,6 +1467,7 @@ static ks_status eval_pod(ks_engine* e, int64_t pod) {
     if (!e->nodes_loaded) return fail(e, KS_EINVAL, "no nodes loaded");
     if (pod < 0 || pod >= e->P) return fail(e, KS_EINVAL, "pod %lld out of range", (long long)pod);
     HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, stage_flush(e));
     ks_status r = flush_expiries(e);
     if (r != KS_OK) return r;
     if (e->n == 0) return KS_OK;
@@ -1299,6 +1522,7 @@ ks_status ks_usage_at(ks_engine* e, int64_t t, int64_t* usage_out) {
     if (t < 0 || t > e->tick) return fail(e, KS_EINVAL, "usage tick %lld outside [0, %lld]", (long long)t, (long long)e->tick);
     if (e->n == 0) return KS_OK;
     HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, stage_flush(e));
     const int64_t q_hi = bound_by(e, t);
     const int64_t nb = usage_blocks(e, t, q_hi);
     HIPCHK(e, hipMemsetAsync(e->d_usage, 0, sizeof(unsigned long long) * 3 * e->n, e->st));
@@ -1325,6 +1549,7 @@ ks_status ks_usage_digest(ks_engine* e, int64_t t_lo, int64_t t_hi, uint64_t* ou
         return fail(e, KS_EINVAL, "digest window [%lld, %lld) outside [0, %lld] or longer than %lld ticks",
                     (long long)t_lo, (long long)t_hi, (long long)e->tick + 1, (long long)kMaxDigestTicks);
     HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, stage_flush(e));
     const int64_t T = t_hi - t_lo;
     const int64_t q_hi = bound_by(e, t_hi - 1);
     const int64_t nb = usage_blocks(e, t_lo, q_hi);
@@ -1406,6 +1631,7 @@ ks_status ks_pod_status(ks_engine* e, int64_t pod_lo, int64_t n, ks_pod_info* ou
     std::vector<int32_t> node(nb), status(nb);
     if (nb) {
         HIPCHK(e, hipSetDevice(e->device));
+        HIPCHK(e, stage_flush(e));
         HIPCHK(e, hipMemcpyAsync(node.data(), e->b_node.p + pod_lo, sizeof(int32_t) * nb, hipMemcpyDeviceToHost, e->st));
         HIPCHK(e, hipMemcpyAsync(status.data(), e->b_status.p + pod_lo, sizeof(int32_t) * nb, hipMemcpyDeviceToHost, e->st));
         HIPCHK(e, hipStreamSynchronize(e->st));

@@ -1,0 +1,75 @@
+// ks_kubesim.cpp — KubeSim.Run (kubesim/kubesim.go:90-123) as a C++ host of the engine's C-ABI
+// (include/ks_kubesim.h): the loop the Go shim runs (go/kubesim/engine/kubesim.go), native.
+#include <chrono>
+#include <vector>
+
+#include "../../include/ks_kubesim.h"
+
+extern "C" {
+
+ks_status ks_trace_submit(void* user, int64_t tick, int64_t /*clock_seconds*/, ks_pods* out) {
+    ks_trace_submitter* s = static_cast<ks_trace_submitter*>(user);
+    const ks_pods& t = s->trace;
+    int64_t lo = s->next, hi = lo;
+    while (hi < t.m && t.arrival[hi] <= tick) hi++;
+    s->next = hi;
+    *out = ks_pods{};
+    if (hi == lo) return KS_OK;
+    const int64_t f0 = t.phase_off[lo];
+    out->m = hi - lo;
+    out->arrival = t.arrival + lo;
+    out->req = t.req + 3 * lo;
+    out->keymask = t.keymask + lo;
+    out->tol = t.tol + lo;
+    out->sel = t.sel + lo;
+    out->phase_off = t.phase_off + lo;  // rebased by ks_run (the engine wants phase_off[0] == 0)
+    out->phase_sec = t.phase_sec + f0;
+    out->phase_use = t.phase_use + 3 * f0;
+    out->flags = t.flags ? t.flags + lo : nullptr;
+    out->key_id = t.key_id ? t.key_id + lo : nullptr;
+    return KS_OK;
+}
+
+ks_status ks_run(ks_engine* eng, int64_t ticks, int64_t window, int32_t n_submitters, const ks_submit_fn* fns,
+                 void* const* users, ks_bind* out, int64_t cap, int64_t* n_out, double* seconds_out) {
+    if (!eng || ticks < 0 || window < 1 || n_submitters < 0 || (n_submitters && (!fns || !users)) || !n_out ||
+        cap < 0 || (cap && !out))
+        return KS_EINVAL;
+    *n_out = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<int64_t> arr;
+    std::vector<int32_t> off;
+    const int64_t start = ks_current_tick(eng);
+    int64_t tick = start, stepped = start;
+    ks_status rc = KS_OK;
+    auto step = [&](int64_t k) -> ks_status {
+        if (k <= 0) return KS_OK;
+        int64_t nb = 0;
+        const ks_status r = ks_step(eng, k, out ? out + *n_out : nullptr, cap - *n_out, &nb);
+        *n_out += nb < cap - *n_out ? nb : cap - *n_out;
+        stepped += k;
+        return r;
+    };
+    while (tick < start + ticks && rc == KS_OK) {
+        tick++;
+        for (int32_t s = 0; s < n_submitters && rc == KS_OK; s++) {  // kubesim.go:126-139, registration order
+            ks_pods p{};
+            rc = fns[s](users[s], tick, 0, &p);
+            if (rc != KS_OK || p.m == 0) continue;
+            // the pods arrive at this tick; phase CSR rebased to 0
+            arr.assign(p.m, tick);
+            off.resize(p.m + 1);
+            for (int64_t i = 0; i <= p.m; i++) off[i] = p.phase_off[i] - p.phase_off[0];
+            rc = ks_submit_pods(eng, p.m, arr.data(), p.req, p.keymask, p.tol, p.sel, off.data(), p.phase_sec,
+                                p.phase_use, p.flags, p.key_id);
+        }
+        if (rc != KS_OK) break;
+        if (tick - stepped >= window) rc = step(tick - stepped);  // window 1: scheduleOne every tick
+    }
+    if (rc == KS_OK) rc = step(tick - stepped);
+    if (seconds_out)
+        *seconds_out = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+}
+
+}  // extern "C"

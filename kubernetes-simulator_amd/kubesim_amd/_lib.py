@@ -10,6 +10,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libks_engine.so")
+RUN_LIB_PATH = os.path.join(HERE, "libks_kubesim.so")
 
 KS_OK, KS_EINVAL, KS_ENOTFOUND, KS_EDEVICE, KS_ENOMEM, KS_ERANGE = 0, 1, 2, 3, 4, 5
 KS_FILTER_REFERENCE_LITERAL, KS_FILTER_FEEDS_SCORE = 0, 1
@@ -22,9 +23,8 @@ KS_ENGINE_FORCE_WIDE = 1
 KS_ENGINE_NO_TINY = 2
 KS_ENGINE_NO_MICRO = 4
 KS_ENGINE_ONE_POD_RESOLVER = 8
-KS_ENGINE_PAIR_RESOLVER = 16
-KS_ENGINE_SWEEP_RESOLVER = 32
 KS_ENGINE_CHUNK_RESOLVER = 64
+KS_ENGINE_SEQ_RESOLVER = 128
 KS_SELFTEST_LR_MICRO = 0
 
 STATUS_NAMES = {KS_OK: "OK", KS_EINVAL: "InvalidArgument", KS_ENOTFOUND: "NotFound",
@@ -43,6 +43,8 @@ EXPORTED_SYMBOLS = ("ks_create", "ks_destroy", "ks_load_nodes", "ks_submit_pods"
                     "ks_cluster_nodes", "ks_cluster_tick", "ks_cluster_start_clock", "ks_cluster_arrays",
                     "ks_cluster_node_name", "ks_cluster_tolerations", "ks_cluster_selector")
 KS_COMM_ID_BYTES = 128
+# include/ks_kubesim.h (libks_kubesim.so)
+RUN_SYMBOLS = ("ks_run", "ks_trace_submit")
 
 
 class KsScorer(C.Structure):
@@ -73,7 +75,37 @@ class KsStepStats(C.Structure):
                 ("launches", C.c_int64), ("pods", C.c_int64), ("other_ms", C.c_double)]
 
 
+class KsPods(C.Structure):
+    _fields_ = [("m", C.c_int64), ("arrival", C.c_void_p), ("req", C.c_void_p), ("keymask", C.c_void_p),
+                ("tol", C.c_void_p), ("sel", C.c_void_p), ("phase_off", C.c_void_p), ("phase_sec", C.c_void_p),
+                ("phase_use", C.c_void_p), ("flags", C.c_void_p), ("key_id", C.c_void_p)]
+
+
+class KsTraceSubmitter(C.Structure):
+    _fields_ = [("trace", KsPods), ("next", C.c_int64), ("tick_seconds", C.c_int64)]
+
+
 _lib = None
+_run_lib = None
+
+
+def load_run():
+    """Load libks_kubesim.so (KubeSim.Run in C++ over the C-ABI, include/ks_kubesim.h)."""
+    global _run_lib
+    if _run_lib is not None:
+        return _run_lib
+    load()
+    if not os.path.exists(RUN_LIB_PATH):
+        raise ImportError(f"{RUN_LIB_PATH} is missing: run __graft_entry__.build()")
+    L = C.CDLL(RUN_LIB_PATH)
+    p = C.c_void_p
+    L.ks_run.argtypes = [p, C.c_int64, C.c_int64, C.c_int32, p, p, p, C.c_int64, C.POINTER(C.c_int64),
+                         C.POINTER(C.c_double)]
+    L.ks_run.restype = C.c_int
+    L.ks_trace_submit.argtypes = [p, C.c_int64, C.c_int64, p]
+    L.ks_trace_submit.restype = C.c_int
+    _run_lib = L
+    return L
 
 
 def load():

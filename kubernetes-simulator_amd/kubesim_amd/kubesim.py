@@ -22,11 +22,13 @@ A submitter is a callable ``submit(tick, clock_seconds) -> encoded pods | None``
 """
 from __future__ import annotations
 
+import ctypes as C
 import time
 
 import numpy as np
 
-from .engine import Engine, KsError
+from . import _lib
+from .engine import Engine, KsError, _c, _p
 
 
 def slice_encoded(pods: dict, lo: int, hi: int) -> dict:
@@ -127,6 +129,42 @@ class KubeSim:
         if not self.binds:
             return np.zeros(0, dtype=[("pod", "<i8"), ("node", "<i4"), ("status", "<i4"), ("tick", "<i8")])
         return np.concatenate(self.binds)
+
+
+class NativeRun:
+    """``KubeSim.Run`` as the C++ host runs it (include/ks_kubesim.h, libks_kubesim.so): a trace
+    submitter replayed natively, per tick ``ks_submit_pods`` + ``ks_step(1)`` (``window`` = 1) or
+    ``RunWindowed`` (one ``ks_step(window)`` after ``window`` ticks of submits) — the call sequence
+    of the cgo shim without any Python between the calls."""
+
+    def __init__(self, engine: Engine, enc_pods: dict, tick_seconds: int):
+        self.eng = engine
+        self.L = _lib.load_run()
+        self._keep = [_c(enc_pods["arrival"], np.int64), _c(enc_pods["req"], np.int64).reshape(-1, 3),
+                      _c(enc_pods["keymask"], np.uint8), _c(enc_pods["tol"], np.uint64),
+                      _c(enc_pods["sel"], np.uint64), _c(enc_pods["phase_off"], np.int32),
+                      _c(enc_pods["phase_sec"], np.int32), _c(enc_pods["phase_use"], np.int64).reshape(-1, 3),
+                      _c(enc_pods["flags"], np.uint8)]
+        keys = enc_pods.get("key_id")
+        self._keys = _c(keys, np.int64) if keys is not None else None
+        t = _lib.KsPods(int(enc_pods["m"]), *[_p(a) for a in self._keep],
+                        _p(self._keys) if self._keys is not None else None)
+        self.sub = _lib.KsTraceSubmitter(t, 0, tick_seconds)
+        self._fn = (C.c_void_p * 1)(C.cast(self.L.ks_trace_submit, C.c_void_p))
+        self._user = (C.c_void_p * 1)(C.cast(C.pointer(self.sub), C.c_void_p))
+
+    def run(self, ticks: int, window: int = 1):
+        """Returns (binds, seconds); raises KsError (with the binds before it) as Run would."""
+        out = (_lib.KsBind * max(ticks, 1))()
+        n = C.c_int64(0)
+        sec = C.c_double(0)
+        rc = self.L.ks_run(self.eng.h, ticks, window, 1, self._fn, self._user, out, ticks, C.byref(n), C.byref(sec))
+        arr = np.frombuffer(out, dtype=np.dtype([("pod", "<i8"), ("node", "<i4"), ("status", "<i4"),
+                                                 ("tick", "<i8")]), count=min(n.value, ticks)).copy()
+        self.eng._submitted = int(self.sub.next)
+        if rc != _lib.KS_OK:
+            raise KsError(rc, self.eng._L.ks_last_error(self.eng.h).decode(), arr)
+        return arr, sec.value
 
 
 def head_probe(eng: Engine, tick: int):

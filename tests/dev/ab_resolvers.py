@@ -1,6 +1,6 @@
 """A/B of the resolvers on the C3 bench workload (and C5 with --c5): per-launch resolve / scan /
 other device time (HIP events), pods per launch, wall pods/s and a CRC of the binds (must agree).
-    python tests/dev/ab_resolvers.py [--c5] [one_pod pair sweep sweep:8 chunk@224 ...]   (sweep:N = KS_SWEEPS=N, @B = batch)"""
+    python tests/dev/ab_resolvers.py [--c5] [one_pod chunk seq seq@192 ...]   (@B = batch)"""
 import os, sys, time, zlib
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -12,18 +12,14 @@ from kubesim_amd import tracegen, encode
 from kubesim_amd.engine import Engine
 args = [x for x in sys.argv[1:] if not x.startswith("--")]
 c5 = "--c5" in sys.argv
-names = args or ["one_pod", "pair", "sweep"]
-FLAGS = {"one_pod": 8, "pair": 16, "sweep": 32, "chunk": 64}
+names = args or ["chunk", "seq"]
+FLAGS = {"one_pod": 8, "chunk": 64, "seq": 128}
 tr = tracegen.c5_trace(n_pods=120_000) if c5 else tracegen.c3_trace(n_pods=200_000)
 enc = encode.encode_trace(tr)
 for rep in range(2):
     for nm in names:
         nm0, _, bp = nm.partition("@")  # name@B: batch of B pods
-        base, _, sw = nm0.partition(":")
-        if sw:
-            os.environ["KS_SWEEPS"] = sw
-        else:
-            os.environ.pop("KS_SWEEPS", None)
+        base = nm0
         eng = Engine(tick_seconds=10, filter_mode=1, filters=7, scorers=((1, 1, 0), (2, 1, 0)), engine_flags=FLAGS[base],
                      batch_pods=int(bp) if bp else 0)
         eng.load_nodes(enc["alloc"], enc["taint"], enc["label"])
@@ -34,7 +30,11 @@ for rep in range(2):
         st = eng.last_step_stats()
         nl = max(st["launches"], 1)
         crc = zlib.crc32(np.ascontiguousarray(b["node"]).tobytes() + np.ascontiguousarray(b["status"]).tobytes())
+        extra = ""
+        if os.environ.get("KS_DIAG_LIB"):
+            d = eng.debug_counters()
+            extra = " diag " + " ".join(str(int(x)) for x in d[5:16])
         print(f"{nm:10s}: resolve {st['resolve_ms'] / nl * 1e3:6.1f} us/launch ({st['resolve_ms'] * 1e6 / max(st['pods'], 1):5.0f} ns/pod), "
               f"scan {st['scan_ms'] / nl * 1e3:5.1f}, other {st['other_ms'] / nl * 1e3:5.1f}; {st['pods'] / nl:6.1f} pods/launch; "
-              f"{65536 / dt:8.0f} pods/s; crc {crc:08x}", flush=True)
+              f"{65536 / dt:8.0f} pods/s; crc {crc:08x}{extra}", flush=True)
         eng.close()

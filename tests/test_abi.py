@@ -15,17 +15,33 @@ def _declared():
         if h.endswith(".h"):
             src += open(os.path.join(ROOT, "include", h)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"typedef[^;]*;", "", src)  # callback types are not entry points
     return sorted(set(re.findall(r"\b(ks_[a-z_]+)\s*\(", src)))
 
 
 def test_header_and_binding_agree():
-    assert _declared() == sorted(_lib.EXPORTED_SYMBOLS)
+    assert _declared() == sorted(_lib.EXPORTED_SYMBOLS + _lib.RUN_SYMBOLS)
 
 
 def test_library_exports_every_declared_symbol():
     L = _lib.load()
-    for sym in _declared():
+    R = _lib.load_run()  # include/ks_kubesim.h: the C++ Run loop over the C-ABI
+    for sym in _lib.EXPORTED_SYMBOLS:
         assert hasattr(L, sym), sym
+    for sym in _lib.RUN_SYMBOLS:
+        assert hasattr(R, sym), sym
+
+
+def test_retired_resolver_flags_rejected_without_device():
+    """Bits 16 and 32 were the pair and sweep resolvers (removed in round 4): refused."""
+    L = _lib.load()
+    for bit in (16, 32, 256):
+        cfg = _lib.KsConfig()
+        cfg.abi_version = _lib.KS_ABI_VERSION
+        cfg.tick_seconds = 10
+        cfg.engine_flags = bit
+        h = C.c_void_p()
+        assert L.ks_create(C.byref(cfg), C.byref(h)) == _lib.KS_EINVAL
 
 
 def test_bad_configs_rejected_without_device():

@@ -93,3 +93,101 @@ def test_windowed_refuses_placement_aware_submitters():
     ks.register_submitter(lambda t, c: None)   # no placement_blind declaration
     with pytest.raises(ValueError):
         ks.run_windowed(10, 4)
+
+
+# ---- the C++ Run loop (include/ks_kubesim.h) and the per-tick path (ks_tick.hip) --------------
+def _native(tr, enc, mode, **kw):
+    from kubesim_amd.kubesim import NativeRun
+    eng = make_engine(tr, enc, mode, **kw)
+    return NativeRun(eng, enc["pods"], tr["tick_seconds"])
+
+
+@pytest.mark.parametrize("window", [1, 16])
+def test_c1_kat_through_the_native_run_loop(window):
+    with open(os.path.join(GOLDEN, "c1_kat.json")) as f:
+        kat = json.load(f)
+    T = kat["ticks"]
+    tr = tracegen.c1_trace(T)
+    nr = _native(tr, encoded(tr), "literal_const")
+    b, _ = nr.run(T, window)
+    got = [[int(x["pod"]), int(x["node"]), int(x["tick"]), int(x["status"])] for x in b]
+    assert got == kat["binds"]
+    np.testing.assert_array_equal(nr.eng.usage(), np.array(kat["usage"][T - 1]))
+
+
+@pytest.mark.parametrize("window", [1, 64])
+def test_c2_prefix_native_run_equals_oracle(window):
+    P, T = 2000, 2100
+    tr = tracegen.c2_trace(n_pods=P, arrival="stream")
+    enc = encoded(tr)
+    mode = "feeds_all_lrba"
+    ora = make_oracle(tr, mode)
+    ora.submit(tr)
+    ob, rc = ora.step(T, cap=T)
+    assert rc == 0
+    nr = _native(tr, enc, mode)
+    b, sec = nr.run(T, window)
+    assert_same_binds(b, ob)
+    np.testing.assert_array_equal(nr.eng.usage(), ora.usage())
+    print(f"\nnative Run window {window}: {len(b) / sec:.0f} pods/s ({sec / T * 1e6:.1f} us/tick)")
+
+
+def test_tick_path_dense_expiries_mixed_steps_and_probes():
+    """Short phases (many expiries due per tick), one pod per tick: ks_step(1) takes the one-launch
+    path, its by-value expiry list and the host-staged submits; interleaved with batched steps
+    (the batch path must see the same device state) and filter/score probes (the exact host flush
+    list) — every bind, the usage and the probes against the oracle."""
+    tr = small_trace(11, n_nodes=600, n_pods=3000, taints=False, selectors=False, tolerations=False)
+    p = tr["pods"]
+    p["phase_sec"][:] = 1 + (np.arange(len(p["phase_sec"])) % 40)
+    p["arrival"][:] = np.arange(1, p["m"] + 1)
+    enc = encoded(tr)
+    mode = "feeds_all_lrba"
+    eng = make_engine(tr, enc, mode)
+    ora = make_oracle(tr, mode)
+    ora.submit(tr)
+    ks = KubeSim(eng, tr["tick_seconds"])
+    ks.register_submitter(TraceSubmitter(enc["pods"]))
+    t = 0
+    for phase, (k, per_tick) in enumerate([(400, True), (700, False), (300, True), (900, False), (200, True)]):
+        if per_tick:
+            ks.run(k)
+        else:
+            ks.run_windowed(k, k)
+        ob, rc = ora.step(k, cap=k)
+        assert rc == 0
+        got = ks.all_binds()[-len(ob["pod"]):] if len(ob["pod"]) else ks.all_binds()[:0]
+        assert_same_binds(got, ob)
+        np.testing.assert_array_equal(eng.usage(), ora.usage(), err_msg=f"phase {phase}")
+        t += k
+        q = eng._submitted - eng.queued
+        if q < p["m"]:
+            feas, score = ora.eval(q)
+            np.testing.assert_array_equal(eng.filter(q), feas)
+            np.testing.assert_array_equal(eng.score(q), score)
+
+
+@pytest.mark.parametrize("mode,code", [("no_scorers", 2), ("bad_spec", 1)])
+def test_tick_path_stops_as_run(mode, code):
+    """NotFound (no candidate) and a bad simSpec stop Run at that pod's tick (kubesim.go:217-220,
+    pod.go:31-39): the per-tick path returns the same error, binds and tick as the oracle."""
+    from kubesim_amd.engine import KsError
+    tr = small_trace(5, n_nodes=64, n_pods=40)
+    tr["pods"]["arrival"][:] = np.arange(1, 41)
+    m = "feeds_all_lrba"
+    if mode == "bad_spec":
+        tr["pods"]["flags"][17] = 2
+    else:
+        m = "no_scorers"
+    enc = encoded(tr)
+    ora = make_oracle(tr, m)
+    ora.submit(tr)
+    ob, orc = ora.step(60, cap=60)
+    eng = make_engine(tr, enc, m)
+    ks = KubeSim(eng, tr["tick_seconds"])
+    ks.register_submitter(TraceSubmitter(enc["pods"]))
+    with pytest.raises(KsError) as ex:
+        ks.run(60)
+    assert ex.value.code == orc == code
+    assert_same_binds(ks.all_binds(), ob)
+    assert eng.tick == ora.tick

@@ -105,12 +105,12 @@ def test_c3_40k_pods_bit_exact_with_usage_samples(c3):
     assert_same_binds(eb, ob)
 
 
-@pytest.mark.parametrize("flags", [0, 16, 32, 64], ids=["default", "pair", "sweep", "chunk"])
+@pytest.mark.parametrize("flags", [0, 128], ids=["default", "seq"])
 def test_c3_whole_trace_matches_oracle_golden(c3, flags):
     """Every pod of the 1M-pod trace — the whole range bench.py times — bind-for-bind against the
     oracle's committed digests (tests/golden/full_run.json, tests/golden/make_full_run.py), at
     the bench's batch (the engine default), with usage at every other window end; the engine's
-    default resolver and the forced pair / sweep / chunk resolvers."""
+    default resolver and the forced sequential resolver."""
     tr, enc = c3
     g = full_run_digest.load("c3")
     assert g is not None and g["pods"] == tr["pods"]["m"] and g["nodes"] == tr["nodes"]["n"]
@@ -141,7 +141,7 @@ def test_c3_reference_literal_prefix(c3):
 def test_c3_full_trace_batch_independent_and_invariants(c3):
     tr, enc = c3
     m, n = tr["pods"]["m"], tr["nodes"]["n"]
-    a = make_engine(tr, enc, MODE)             # default batch (256)
+    a = make_engine(tr, enc, MODE)             # default batch
     a.submit(enc["pods"])
     b = make_engine(tr, enc, MODE, batch_pods=97)
     b.submit(enc["pods"])
