@@ -17,6 +17,7 @@ package engine
 import "C"
 
 import (
+	"runtime"
 	"unsafe"
 
 	"github.com/cpuguy83/strongerrors"
@@ -117,6 +118,9 @@ func New(c Config) (*Engine, error) {
 	if rc := C.ks_create(&cfg, &e.h); rc != C.KS_OK {
 		return nil, errors.Errorf("ks_create rejected the configuration (%d)", int(rc))
 	}
+	// A caller written against the reference API never calls Close (kubesim.KubeSim has none):
+	// the device state is released when the Engine becomes unreachable.
+	runtime.SetFinalizer(e, (*Engine).Close)
 	return e, nil
 }
 
@@ -126,6 +130,7 @@ func (e *Engine) Close() {
 		C.ks_destroy(e.h)
 		e.h = nil
 	}
+	runtime.SetFinalizer(e, nil)
 }
 
 // LoadNodes loads the cluster once: alloc = n*4 {milli cpu, milli memory, milli gpu, pods}

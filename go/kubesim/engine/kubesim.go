@@ -139,7 +139,8 @@ func (k *KubeSim) start() error {
 // in registration order, their pods are appended FIFO, and one queued pod is scheduled on the
 // device; any plugin or CreatePod error ends the run with that error.
 // The engine stays alive after Run returns (queries through Engine(), a later Run continues
-// the same simulation); Close releases it.
+// the same simulation); Close releases it, and so does the Engine's finalizer once the KubeSim is
+// unreachable (a caller of the reference API, which has no Close, does not leak device memory).
 func (k *KubeSim) Run(ctx context.Context) error {
 	if err := k.start(); err != nil {
 		return err
@@ -176,6 +177,10 @@ type PlacementBlind interface {
 // and errors are identical to Run's — a pod's placement depends only on the pods submitted
 // before it, and every submit happens before the step that binds it; a submitter error at tick t
 // is returned after ticks < t are scheduled, as Run returns it.  ctx is checked once per window.
+// One difference remains after an error: when the STEP fails at tick t (NotFound or
+// InvalidArgument), the pods the submitters returned for ticks t+1 .. of the same window are
+// already queued (Queued(), PodStatus report them Pending), whereas Run would never have called
+// the submitters for those ticks.  Binds, ticks and the error itself are Run's.
 // Every registered submitter must implement PlacementBlind (else an error, nothing run).
 func (k *KubeSim) RunWindowed(ctx context.Context, window int64) error {
 	if window <= 1 {

@@ -154,6 +154,15 @@ ks_status ks_merge_candidates(const uint64_t* cand_all, int32_t parts, int32_t B
 #define KS_COMM_ID_BYTES 128
 ks_status ks_comm_unique_id(uint8_t* id_out /* [KS_COMM_ID_BYTES] */);
 ks_status ks_shard(ks_engine* eng, int32_t world, int32_t rank, const uint8_t* id, int32_t vshards);
+/* The same sharding with a host exchange instead of RCCL (no communicator): at every batch the
+ * engine copies this rank's parts of cand_all[G][B][L] to host memory and calls fn with a buffer of
+ * world x bytes_per_rank bytes (rank-major, this rank's slice filled); fn must fill the other
+ * ranks' slices (an all-gather) and return KS_OK, after which the whole array goes back to the
+ * device.  For ranks that share no RCCL communicator: threads of one process on one or several
+ * GPUs (ks_local_allgather, ks_kubesim.h), or any host transport.  Before ks_load_nodes. */
+typedef ks_status (*ks_allgather_fn)(void* user, int32_t rank, int32_t world, void* buf, int64_t bytes_per_rank);
+ks_status ks_shard_host(ks_engine* eng, int32_t world, int32_t rank, int32_t vshards, ks_allgather_fn fn,
+                        void* user);
 
 /* Load the cluster (once).  alloc[n][4] = {cpu, memory, nvidia.com/gpu, pods};
  * taint[n] = OR of dictionary bits of the node's NoSchedule/NoExecute taints;

@@ -62,6 +62,15 @@ typedef struct {
 } ks_trace_submitter;
 ks_status ks_trace_submit(void* user /* ks_trace_submitter* */, int64_t tick, int64_t clock_seconds, ks_pods* out);
 
+/* In-process all-gather for ks_shard_host: `world` engines driven by threads of one process
+ * (one per rank, on one GPU or several) exchange their candidate parts through host memory.
+ * Pass ks_local_allgather as the fn and the exchange as the user pointer of every rank. */
+typedef struct ks_local_exchange ks_local_exchange;
+ks_local_exchange* ks_local_exchange_create(int32_t world);
+void ks_local_exchange_destroy(ks_local_exchange* x);
+ks_status ks_local_allgather(void* user /* ks_local_exchange* */, int32_t rank, int32_t world, void* buf,
+                             int64_t bytes_per_rank);
+
 #ifdef __cplusplus
 }
 #endif

@@ -180,6 +180,9 @@ struct ks_engine {
     // node sharding
     int world = 1, rank = 0, vsh = 1;
     ncclComm_t comm = nullptr;
+    ks_allgather_fn xfn = nullptr;  // host exchange (ks_shard_host) instead of RCCL
+    void* xuser = nullptr;
+    uint64_t* h_xbuf = nullptr;     // pinned [world][vsh][B][L]
     std::vector<int> part_lo;  // [world * vsh + 1] block boundaries of the parts
     int blk_lo = 0, blk_n = 0;  // this rank's scan range
     uint64_t* cand_all = nullptr;  // [world * vsh][B][L]
@@ -477,6 +480,7 @@ void engine_free(ks_engine* e) {
     if (e->cand) (void)hipFree(e->cand);
     if (e->cand_all) (void)hipFree(e->cand_all);
     if (e->comm) (void)ncclCommDestroy(e->comm);
+    if (e->h_xbuf) (void)hipHostFree(e->h_xbuf);
     if (!e->group) {
         if (e->d_ctr) (void)hipFree(e->d_ctr);
         if (e->h_ctr) (void)hipHostFree(e->h_ctr);
@@ -537,6 +541,20 @@ ks_status ks_shard(ks_engine* e, int32_t world, int32_t rank, const uint8_t* id,
     e->world = world;
     e->rank = rank;
     e->vsh = vshards;
+    return KS_OK;
+}
+
+ks_status ks_shard_host(ks_engine* e, int32_t world, int32_t rank, int32_t vshards, ks_allgather_fn fn, void* user) {
+    if (!e) return KS_EINVAL;
+    if (e->nodes_loaded) return fail(e, KS_EINVAL, "ks_shard_host must precede ks_load_nodes");
+    if (e->comm || e->xfn) return fail(e, KS_EINVAL, "already sharded");
+    if (!fn || world < 1 || rank < 0 || rank >= world || vshards < 1 || (int64_t)world * vshards > 4096)
+        return fail(e, KS_EINVAL, "bad host-exchange shard geometry world=%d rank=%d vshards=%d", world, rank, vshards);
+    e->world = world;
+    e->rank = rank;
+    e->vsh = vshards;
+    e->xfn = fn;
+    e->xuser = user;
     return KS_OK;
 }
 
@@ -628,7 +646,7 @@ ks_status ks_load_nodes(ks_engine* e, int64_t n, const int64_t* alloc, const uin
     // binds grows with the chunk's position, and 256-pod batches hit the candidate-id table
     // (~215 pods committed): 192 pods binds more per second on C3 (9.96e5 vs 9.12e5 pods/s,
     // 224: 9.53e5, 176: 9.64e5, 128: 9.49e5) and C5 (3.67e5 vs 3.19e5; tests/dev/ab_resolvers.py)
-    if (!e->cfg.batch_pods && !small_resolver(e) && chunk_eligible(e) &&
+    if (!e->cfg.batch_pods && !e->group && !small_resolver(e) && chunk_eligible(e) &&
         !(e->flags & (KS_ENGINE_ONE_POD_RESOLVER | KS_ENGINE_SEQ_RESOLVER)))
         e->B = kChunkBatch;
     // pods per scan workgroup: the most pod reuse per node load that still leaves >= ~2048
@@ -641,11 +659,9 @@ ks_status ks_load_nodes(ks_engine* e, int64_t n, const int64_t* alloc, const uin
     HIPCHK(e, hipMalloc(&e->lists, sizeof(uint64_t) * (size_t)e->B * e->nblk * ks::kTopL));
     HIPCHK(e, hipMalloc(&e->cand, sizeof(uint64_t) * (size_t)e->B * ks::kTopL));
     if (G > 1) HIPCHK(e, hipMalloc(&e->cand_all, sizeof(uint64_t) * (size_t)G * e->B * ks::kTopL));
+    if (G > 1 && e->xfn) HIPCHK(e, hipHostMalloc(&e->h_xbuf, sizeof(uint64_t) * (size_t)G * e->B * ks::kTopL, hipHostMallocDefault));
     HIPCHK(e, hipMalloc(&e->d_mask, std::max<int64_t>(n, 1)));
     HIPCHK(e, hipMalloc(&e->d_score, sizeof(int64_t) * std::max<int64_t>(n, 1)));
-    HIPCHK(e, hipMalloc(&e->d_sweep, sizeof(ks::WinWS)));
-    HIPCHK(e, hipMalloc(&e->d_eidx, sizeof(int32_t) * e->n_pad));
-    HIPCHK(e, hipMemsetAsync(e->d_eidx, 0xFF, sizeof(int32_t) * e->n_pad, e->st));
     HIPCHK(e, hipMalloc(&e->d_usage, sizeof(unsigned long long) * 3 * std::max<int64_t>(n, 1)));
     HIPCHK(e, hipStreamSynchronize(e->st));
     e->nodes_loaded = true;
@@ -1026,8 +1042,20 @@ static bool tick_step(ks_engine* e, int64_t t_end, ks_bind* out, int64_t cap, in
     return true;
 }
 
+// The batch window workspace (~0.8 MB) and the node -> E index, allocated on the first step that
+// runs a resolver using them (what-if group members never do).
+static ks_status ensure_window_ws(ks_engine* e) {
+    const int r = resolver_of(e);
+    if (e->d_sweep || (r != kResolveChunk && r != kResolveSeq)) return KS_OK;
+    HIPCHK(e, hipMalloc(&e->d_sweep, sizeof(ks::WinWS)));
+    HIPCHK(e, hipMalloc(&e->d_eidx, sizeof(int32_t) * e->n_pad));
+    HIPCHK(e, hipMemsetAsync(e->d_eidx, 0xFF, sizeof(int32_t) * e->n_pad, e->st));
+    return KS_OK;
+}
+
 static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t cap, int64_t* n_out) {
     HIPCHK(e, hipSetDevice(e->device));
+    if (ks_status r = ensure_window_ws(e); r != KS_OK) return r;
     const int64_t t_end = e->tick + ticks;
     int64_t p_hi = 0;
     if (!step_prepare(e, ticks, &p_hi)) {
@@ -1082,6 +1110,15 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
                     const ncclResult_t nr = ncclAllGather(e->cand_all + (int64_t)e->rank * e->vsh * BL, e->cand_all,
                                                           (size_t)e->vsh * BL, ncclUint64, e->comm, st);
                     if (nr != ncclSuccess) return fail(e, KS_EDEVICE, "ncclAllGather: %s", ncclGetErrorString(nr));
+                } else if (e->xfn) {  // host exchange: this rank's parts out, every rank's parts back
+                    const int64_t slice = (int64_t)e->vsh * BL, off = (int64_t)e->rank * slice;
+                    HIPCHK(e, hipMemcpyAsync(e->h_xbuf + off, e->cand_all + off, sizeof(uint64_t) * slice,
+                                             hipMemcpyDeviceToHost, st));
+                    HIPCHK(e, hipStreamSynchronize(st));
+                    const ks_status xr = e->xfn(e->xuser, e->rank, e->world, e->h_xbuf, (int64_t)sizeof(uint64_t) * slice);
+                    if (xr != KS_OK) return fail(e, KS_EDEVICE, "host exchange failed (%d)", (int)xr);
+                    HIPCHK(e, hipMemcpyAsync(e->cand_all, e->h_xbuf, sizeof(uint64_t) * slice * e->world,
+                                             hipMemcpyHostToDevice, st));
                 }
                 HIPCHK(e, ks::launch_merge(d, 1, e->B, e->cand_all, L, G, BL, e->cand, G, st));
             }

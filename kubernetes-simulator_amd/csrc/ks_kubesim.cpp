@@ -1,6 +1,9 @@
 // ks_kubesim.cpp — KubeSim.Run (kubesim/kubesim.go:90-123) as a C++ host of the engine's C-ABI
 // (include/ks_kubesim.h): the loop the Go shim runs (go/kubesim/engine/kubesim.go), native.
 #include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "../../include/ks_kubesim.h"
@@ -70,6 +73,53 @@ ks_status ks_run(ks_engine* eng, int64_t ticks, int64_t window, int32_t n_submit
     if (seconds_out)
         *seconds_out = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return rc;
+}
+
+}  // extern "C"
+
+// ---- in-process all-gather (ks_shard_host between threads) ----------------------------------
+struct ks_local_exchange {
+    int32_t world = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<uint8_t> buf;
+    int32_t arrived = 0, left = 0;
+    uint64_t gen = 0;
+};
+
+extern "C" {
+
+ks_local_exchange* ks_local_exchange_create(int32_t world) {
+    if (world < 1) return nullptr;
+    ks_local_exchange* x = new ks_local_exchange();
+    x->world = world;
+    return x;
+}
+
+void ks_local_exchange_destroy(ks_local_exchange* x) { delete x; }
+
+// Two phases per exchange: every rank deposits its slice, the last depositor releases them all;
+// every rank copies the whole array out, the last to leave opens the next exchange.
+ks_status ks_local_allgather(void* user, int32_t rank, int32_t world, void* buf, int64_t bytes_per_rank) {
+    ks_local_exchange* x = static_cast<ks_local_exchange*>(user);
+    if (!x || world != x->world || rank < 0 || rank >= world || bytes_per_rank < 0) return KS_EINVAL;
+    uint8_t* b = static_cast<uint8_t*>(buf);
+    std::unique_lock<std::mutex> lk(x->mu);
+    x->cv.wait(lk, [&] { return x->left == 0; });  // the previous exchange has been read by everyone
+    const uint64_t g = x->gen;
+    if ((int64_t)x->buf.size() < bytes_per_rank * world) x->buf.resize(bytes_per_rank * world);
+    std::memcpy(x->buf.data() + rank * bytes_per_rank, b + rank * bytes_per_rank, bytes_per_rank);
+    if (++x->arrived == world) {
+        x->arrived = 0;
+        x->left = world;
+        x->gen++;
+        x->cv.notify_all();
+    } else {
+        x->cv.wait(lk, [&] { return x->gen != g; });
+    }
+    std::memcpy(b, x->buf.data(), bytes_per_rank * world);
+    if (--x->left == 0) x->cv.notify_all();
+    return KS_OK;
 }
 
 }  // extern "C"

@@ -34,7 +34,7 @@ STATUS_NAMES = {KS_OK: "OK", KS_EINVAL: "InvalidArgument", KS_ENOTFOUND: "NotFou
 EXPORTED_SYMBOLS = ("ks_create", "ks_destroy", "ks_load_nodes", "ks_submit_pods", "ks_step",
                     "ks_filter", "ks_score", "ks_usage", "ks_current_tick", "ks_queued_pods",
                     "ks_last_error", "ks_last_step_stats", "ks_set_profiling", "ks_debug_counters", "ks_selftest",
-                    "ks_comm_unique_id", "ks_shard", "ks_group_create", "ks_group_destroy",
+                    "ks_comm_unique_id", "ks_shard", "ks_shard_host", "ks_group_create", "ks_group_destroy",
                     "ks_group_add", "ks_group_size", "ks_group_step", "ks_pod_status",
                     "ks_usage_at", "ks_usage_digest", "ks_node_mix", "ks_pod_lookup", "ks_node_pods",
                     "ks_shard_layout", "ks_merge_candidates",
@@ -44,7 +44,8 @@ EXPORTED_SYMBOLS = ("ks_create", "ks_destroy", "ks_load_nodes", "ks_submit_pods"
                     "ks_cluster_node_name", "ks_cluster_tolerations", "ks_cluster_selector")
 KS_COMM_ID_BYTES = 128
 # include/ks_kubesim.h (libks_kubesim.so)
-RUN_SYMBOLS = ("ks_run", "ks_trace_submit")
+RUN_SYMBOLS = ("ks_run", "ks_trace_submit", "ks_local_exchange_create", "ks_local_exchange_destroy",
+               "ks_local_allgather")
 
 
 class KsScorer(C.Structure):
@@ -104,6 +105,12 @@ def load_run():
     L.ks_run.restype = C.c_int
     L.ks_trace_submit.argtypes = [p, C.c_int64, C.c_int64, p]
     L.ks_trace_submit.restype = C.c_int
+    L.ks_local_exchange_create.argtypes = [C.c_int32]
+    L.ks_local_exchange_create.restype = p
+    L.ks_local_exchange_destroy.argtypes = [p]
+    L.ks_local_exchange_destroy.restype = None
+    L.ks_local_allgather.argtypes = [p, C.c_int32, C.c_int32, p, C.c_int64]
+    L.ks_local_allgather.restype = C.c_int
     _run_lib = L
     return L
 
@@ -158,6 +165,8 @@ def load():
     L.ks_comm_unique_id.restype = C.c_int
     L.ks_shard.argtypes = [p, C.c_int32, C.c_int32, p, C.c_int32]
     L.ks_shard.restype = C.c_int
+    L.ks_shard_host.argtypes = [p, C.c_int32, C.c_int32, C.c_int32, p, p]
+    L.ks_shard_host.restype = C.c_int
     L.ks_group_create.argtypes = [C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]
     L.ks_group_create.restype = C.c_int
     L.ks_group_destroy.argtypes = [p]

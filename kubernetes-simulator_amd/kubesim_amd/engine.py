@@ -108,6 +108,12 @@ class Engine:
             buf = (C.c_uint8 * _lib.KS_COMM_ID_BYTES).from_buffer_copy(comm_id)
         self._check(self._L.ks_shard(self.h, world, rank, buf, vshards))
 
+    def shard_host(self, world: int, rank: int, exchange: "LocalExchange", vshards: int = 1):
+        """Node sharding with a host exchange instead of RCCL (ks_shard_host): ranks are engines
+        driven by threads of this process, exchanging candidates through ``exchange``."""
+        self._xchg = exchange  # keep alive
+        self._check(self._L.ks_shard_host(self.h, world, rank, vshards, exchange.fn, exchange.h))
+
     # -- cluster / queue ---------------------------------------------------------------------
     def load_nodes(self, alloc, taint, label):
         alloc = _c(alloc, np.int64).reshape(-1, 4)
@@ -251,6 +257,26 @@ def selftest(test: int = _lib.KS_SELFTEST_LR_MICRO, device: int = 0) -> int:
     if rc != 0:
         raise KsError(rc, "ks_selftest failed")
     return n.value
+
+
+class LocalExchange:
+    """An in-process all-gather for ``world`` engines sharded with :meth:`Engine.shard_host`
+    (ks_local_allgather, include/ks_kubesim.h)."""
+
+    def __init__(self, world: int):
+        self._R = _lib.load_run()
+        self.h = self._R.ks_local_exchange_create(world)
+        if not self.h:
+            raise ValueError("bad world size")
+        self.fn = C.cast(self._R.ks_local_allgather, C.c_void_p)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._R.ks_local_exchange_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
 
 
 def comm_unique_id() -> bytes:

@@ -122,7 +122,13 @@ class KubeSim:
             k = min(window, end - self.tick)
             for _ in range(k):
                 self.tick += 1
-                self._submit(self.tick)
+                try:
+                    self._submit(self.tick)
+                except Exception:
+                    # Run would have scheduled ticks < t before calling the submitters at t (the
+                    # Go shim's RunWindowed does the same)
+                    self._step(self.tick - 1 - self.eng.tick)
+                    raise
             self._step(self.tick - self.eng.tick)
 
     def all_binds(self):

@@ -99,6 +99,7 @@ static void* dupmem(const void* p, size_t bytes) {
 ko_sim* ko_create(const ko_config* cfg, int64_t n, const int64_t* alloc, const uint8_t* alloc_has,
                   const int32_t* taint_off, const int32_t* taint, const int32_t* label_off,
                   const int32_t* label) {
+    if (!cfg || cfg->tick_seconds < 1) return NULL;  /* the engine's ks_create refuses the same */
     ko_sim* s = (ko_sim*)calloc(1, sizeof(ko_sim));
     s->cfg = *cfg;
     s->n = n;
@@ -452,12 +453,23 @@ int ko_step(ko_sim* s, int64_t ticks, int64_t* out_pod, int32_t* out_node, int64
             int32_t* out_status, int64_t cap, int64_t* n_out) {
     *n_out = 0;
     if (s->err) return s->err;
-    for (int64_t i = 0; i < ticks; i++) {
-        int64_t t = s->tick + 1;
-        if (s->first_bind >= 0 && t - s->first_bind > (int64_t)INT32_MAX / s->cfg.tick_seconds) {
-            snprintf(s->errmsg, sizeof s->errmsg, "tick %lld: 2^31 s after the first bind", (long long)t);
+    /* The int32 passed-seconds domain, checked for the whole step before any tick runs (as the
+     * engine's ks_step does): the run's first bind is first_bind, or — none yet — the next queued
+     * pod's bind tick (it binds at the first tick >= its arrival) when that falls in this step. */
+    {
+        int64_t fb = s->first_bind;
+        if (fb < 0 && s->qhead < s->m) {
+            fb = s->arrival[s->qhead] > s->tick + 1 ? s->arrival[s->qhead] : s->tick + 1;
+            if (fb > s->tick + ticks) fb = -1;
+        }
+        if (fb >= 0 && s->tick + ticks - fb > (int64_t)INT32_MAX / s->cfg.tick_seconds) {
+            snprintf(s->errmsg, sizeof s->errmsg, "step to tick %lld: 2^31 s after the first bind (tick %lld)",
+                     (long long)(s->tick + ticks), (long long)fb);
             return KO_ERANGE;
         }
+    }
+    for (int64_t i = 0; i < ticks; i++) {
+        int64_t t = s->tick + 1;
         while (s->arrived < s->m && s->arrival[s->arrived] <= t) s->arrived++;
         if (s->qhead < s->arrived) {
             int64_t p = s->qhead;

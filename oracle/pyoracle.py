@@ -75,6 +75,8 @@ class COracle:
                       _c(nd["taint_off"], np.int32), _c(nd["taint"], np.int32),
                       _c(nd["label_off"], np.int32), _c(nd["label"], np.int32)]
         self.h = lib().ko_create(C.byref(cfg), self.n, *[_ptr(a) for a in self._keep])
+        if not self.h:
+            raise ValueError("ko_create refused the configuration (tick_seconds must be >= 1)")
         self.m = 0
 
     def set_threads(self, n: int):
@@ -82,7 +84,7 @@ class COracle:
         lib().ko_set_threads(self.h, int(n))
 
     def close(self):
-        if self.h:
+        if getattr(self, "h", None):
             lib().ko_destroy(self.h)
             self.h = None
 

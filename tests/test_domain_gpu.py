@@ -74,3 +74,32 @@ def test_submit_past_domain_refused_atomically():
     late["arrival"] = np.array([first + SPAN - 2, first + SPAN - 1, first + SPAN], np.int64)
     eng.submit(late)                           # the last bind tick is exactly the domain's end
     assert eng.queued == m0 + 3
+
+
+def test_multi_tick_step_crossing_the_domain_refused_whole_on_both():
+    """one ks_step(N) / ko_step(N) whose end leaves the domain — both refuse it before
+    any tick runs (same binds, same tick, same usage after)."""
+    from kubesim_amd import _lib
+    from kubesim_amd.engine import KsError
+    tr = _trace()
+    enc = encoded(tr)
+    eng = make_engine(tr, enc, MODE)
+    eng.submit(enc["pods"])
+    ora = make_oracle(tr, MODE)
+    ora.submit(tr)
+    eb = eng.step(30)
+    ob, rc = ora.step(30)
+    assert rc == 0
+    assert_same_binds(eb, ob)
+    last = int(eb["tick"][0]) + SPAN
+    with pytest.raises(KsError) as ex:
+        eng.step(last - eng.tick + 3)
+    assert ex.value.code == _lib.KS_ERANGE
+    b, rc = ora.step(last - ora.tick + 3)
+    assert rc == _lib.KS_ERANGE and len(b["pod"]) == 0
+    assert eng.tick == ora.tick
+    np.testing.assert_array_equal(eng.usage(), ora.usage())
+    eb = eng.step(last - eng.tick)
+    ob, rc = ora.step(last - ora.tick)
+    assert rc == 0
+    assert_same_binds(eb, ob)

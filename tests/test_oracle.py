@@ -117,3 +117,29 @@ def test_oracle_refuses_ticks_past_int32_passed_seconds():
     assert rc == 5 and co.tick == last and len(b["pod"]) == 0
     b, rc = co.step(1)                    # refused again, nothing changes
     assert rc == 5 and co.tick == last
+
+
+def test_oracle_refuses_a_multi_tick_step_crossing_the_domain_whole():
+    """A step whose last tick leaves the int32 passed-seconds domain is refused before any of its
+    ticks runs, exactly as the engine's ks_step (tests/test_domain_gpu.py): no binds, no tick."""
+    tr = small_trace(5, n_nodes=32, n_pods=40, arrival="stream", selectors=False)
+    tr["tick_seconds"] = 1 << 20
+    co = make_oracle(tr, "feeds_all_lrba")
+    co.submit(tr)
+    b, rc = co.step(3)
+    assert rc == 0
+    t0 = int(b["tick"][0])
+    last = t0 + (2**31 - 1) // (1 << 20)
+    tick0, u0 = co.tick, co.usage()
+    b, rc = co.step(last - co.tick + 5)
+    assert rc == 5 and len(b["pod"]) == 0 and co.tick == tick0
+    np.testing.assert_array_equal(co.usage(), u0)
+    b, rc = co.step(last - co.tick)       # up to the domain's end: runs
+    assert rc == 0 and co.tick == last
+
+
+def test_oracle_refuses_tick_seconds_below_one():
+    tr = small_trace(5, n_nodes=8, n_pods=4)
+    tr["tick_seconds"] = 0
+    with pytest.raises(ValueError):
+        make_oracle(tr, "feeds_all_lrba")
