@@ -88,9 +88,12 @@ def cpu_baseline(trace, scorers, sample_pods, budget_s):
     threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or min(os.cpu_count() or 1, 16)
     d_mt, t_mt = _oracle_rate(trace, scorers, sample_pods, budget_s, threads)
     d_st, t_st = _oracle_rate(trace, scorers, sample_pods, budget_s, 1)
+    host = os.cpu_count() or 0
     return dict(value=d_mt * n / t_mt, unit="evals/s", cores=threads, kind="port",
                 sample=f"C3 nodes ({n}), first {d_mt} pods of the trace, oracle/ks_oracle.c with OpenMP "
                        f"over nodes on {threads} threads ({t_mt:.1f} s)",
+                cores_note=f"{threads} of the host's {host} hardware threads: the job's CPU share "
+                           f"(OMP_NUM_THREADS on the GPU box; gpurun caps a job at 16), not the machine",
                 pods_per_s=d_mt / t_mt,
                 single_thread={"value": d_st * n / t_st, "pods_per_s": d_st / t_st, "cores": 1,
                                "sample": f"first {d_st} pods, one thread ({t_st:.1f} s)"})
@@ -368,47 +371,58 @@ def main():
         dist.destroy_process_group()
 
 
-def dropin_leg(trace, enc, scorers, device, per_tick=1000, probe_ticks=200, windowed=8192, window=1024):
-    """The drop-in's own call sequence (go/kubesim/engine/kubesim.go Run / RunWindowed, replayed
-    call for call by kubesim_amd.kubesim.KubeSim) on the C3 cluster with one pod arriving per
-    tick: per-tick Run (ks_submit_pods + ks_step(1) every tick), the same with the api.Filter /
-    api.Scorer adapters probing the queue head (ks_filter + ks_score), and RunWindowed.  Rates in
-    pods/s (one pod binds per tick); wall time incl. every host call."""
+def dropin_leg(trace, enc, scorers, device, per_tick=4000, probe_ticks=400, windowed=65536, window=1024):
+    """The drop-in's own call sequence on the C3 cluster with one pod arriving per tick.
+    * native: KubeSim.Run / RunWindowed as a C++ host of the C-ABI (include/ks_kubesim.h,
+      libks_kubesim.so) — per tick ks_submit_pods + ks_step(1) (the per-tick path: one launch), or
+      `window` ticks of submits then one ks_step — the calls the Go shim makes through cgo
+      (go/kubesim/engine/kubesim.go), with no interpreter between them;
+    * python: the same loop through the Python twin (kubesim_amd.kubesim.KubeSim), plus the
+      api.Filter / api.Scorer probe of the queue head (ks_filter + ks_score) every tick.
+    Rates in pods/s (one pod binds per tick), wall time including every host call."""
     import numpy as np
     from kubesim_amd.engine import Engine
-    from kubesim_amd.kubesim import KubeSim, TraceSubmitter, head_probe, slice_encoded
+    from kubesim_amd.kubesim import KubeSim, NativeRun, TraceSubmitter, head_probe, slice_encoded
 
-    def sim(n_pods):
+    def pods_of(n_pods):
         pods = dict(slice_encoded(enc["pods"], 0, n_pods))
         pods["arrival"] = np.arange(1, n_pods + 1, dtype=np.int64)
+        return pods
+
+    def engine():
         eng = Engine(tick_seconds=trace["tick_seconds"], filter_mode=1, filters=7, scorers=scorers, device=device)
         eng.load_nodes(enc["alloc"], enc["taint"], enc["label"])
-        ks = KubeSim(eng, trace["tick_seconds"])
-        ks.register_submitter(TraceSubmitter(pods))
-        return ks
+        return eng
 
     out = {"workload": f"C3 cluster ({trace['nodes']['n']} nodes), trace pods 0.., one arrival per tick"}
-    ks = sim(per_tick + 16)
-    ks.run(16)   # warm-up
+    nr = NativeRun(engine(), pods_of(per_tick + 64), trace["tick_seconds"])
+    nr.run(64)  # warm-up
+    b, dt = nr.run(per_tick)
+    out["per_tick"] = {"pods_per_s": len(b) / dt, "us_per_tick": dt / per_tick * 1e6, "ticks": per_tick,
+                       "host": "C++ Run loop over the C-ABI (libks_kubesim.so)"}
+    nr.eng.close()
+    nr = NativeRun(engine(), pods_of(windowed + window), trace["tick_seconds"])
+    nr.run(window, window)
+    b, dt = nr.run(windowed, window)
+    out["windowed"] = {"pods_per_s": len(b) / dt, "window": window, "ticks": windowed,
+                       "host": "C++ RunWindowed over the C-ABI"}
+    nr.eng.close()
+    ks = KubeSim(engine(), trace["tick_seconds"])
+    ks.register_submitter(TraceSubmitter(pods_of(per_tick + 64)))
+    ks.run(64)
     t0 = time.perf_counter()
     ks.run(per_tick)
     dt = time.perf_counter() - t0
-    out["per_tick"] = {"pods_per_s": per_tick / dt, "us_per_tick": dt / per_tick * 1e6, "ticks": per_tick}
+    out["python_per_tick"] = {"pods_per_s": per_tick / dt, "us_per_tick": dt / per_tick * 1e6, "ticks": per_tick}
     ks.eng.close()
-    ks = sim(probe_ticks + 16)
+    ks = KubeSim(engine(), trace["tick_seconds"])
+    ks.register_submitter(TraceSubmitter(pods_of(probe_ticks + 16)))
     ks.run(16)
     t0 = time.perf_counter()
     ks.run(probe_ticks, probe=head_probe)
     dt = time.perf_counter() - t0
-    out["per_tick_with_filter_score_probe"] = {"pods_per_s": probe_ticks / dt, "us_per_tick": dt / probe_ticks * 1e6,
-                                               "ticks": probe_ticks}
-    ks.eng.close()
-    ks = sim(windowed + window)
-    ks.run_windowed(window, window)
-    t0 = time.perf_counter()
-    ks.run_windowed(windowed, window)
-    dt = time.perf_counter() - t0
-    out["windowed"] = {"pods_per_s": windowed / dt, "window": window, "ticks": windowed}
+    out["python_per_tick_with_filter_score_probe"] = {"pods_per_s": probe_ticks / dt,
+                                                      "us_per_tick": dt / probe_ticks * 1e6, "ticks": probe_ticks}
     ks.eng.close()
     return out
 

@@ -164,7 +164,8 @@ def _label_value(st, fam, v):
 def synth_trace(n_nodes: int, n_pods: int, seed: int, *, taints: bool, labels: bool,
                 tolerations: bool, selectors: bool, arrival: str = "bulk",
                 bad_selector_p: float = 0.0, gpu_absent_p: float = 0.05,
-                node_offset: int = 0, config: str = "synthetic", max_sel_pairs: int = 2):
+                node_offset: int = 0, config: str = "synthetic", max_sel_pairs: int = 2,
+                mem_decimal: bool = False):
     """Generate a synthetic trace with the §8(d) distributions.
 
     ``arrival="bulk"`` makes every pod arrive at tick 1 (a Submitter returning the whole
@@ -172,6 +173,10 @@ def synth_trace(n_nodes: int, n_pods: int, seed: int, *, taints: bool, labels: b
     sometimes runs empty (``kubesim/kubesim.go:144-147``).
     ``node_offset`` shifts node-indexed draws so a shard of a bigger cluster can be
     generated without materialising the whole cluster.
+    ``mem_decimal``: memory requests in decimal SI (``500M`` .. ``32G`` in 500M steps) on the
+    binary-SI capacities (``32Gi`` .. ``512Gi``) — the common real-world mix: the gcd of the
+    memory quantities drops to 2^8 bytes and the capacities scale to 2^31, outside the engine's
+    32-bit evaluators (the wide class).
     """
     st = StringTable()
     N, P = int(n_nodes), int(n_pods)
@@ -230,7 +235,10 @@ def synth_trace(n_nodes: int, n_pods: int, seed: int, *, taints: bool, labels: b
         raise ValueError(arrival)
     req = np.zeros((P, 3), dtype=np.int64)
     req[:, CPU] = (1 + uniform_int(seed, 21, pid, 80)) * 100
-    req[:, MEM] = (1 + uniform_int(seed, 22, pid, 128)) * 256 * MI * MILLI
+    if mem_decimal:
+        req[:, MEM] = (1 + uniform_int(seed, 22, pid, 64)) * 500_000_000 * MILLI
+    else:
+        req[:, MEM] = (1 + uniform_int(seed, 22, pid, 128)) * 256 * MI * MILLI
     gsel = uniform_int(seed, 23, pid, 10)
     req[:, GPU] = np.where(gsel < 7, 0, np.array([1, 2, 4], dtype=np.int64)[uniform_int(seed, 24, pid, 3)] * MILLI)
     req_has = np.full(P, 7, dtype=np.uint8)
@@ -325,6 +333,15 @@ def c3_trace(n_nodes=50_000, n_pods=1_000_000, seed=0x5EED0003, **kw):
     """BASELINE.json configs[2]: 50k nodes with taints/labels, tolerations, 1M pods."""
     return synth_trace(n_nodes, n_pods, seed, taints=True, labels=True, tolerations=True,
                        selectors=True, config="C3", **kw)
+
+
+def c3q_trace(n_nodes=50_000, n_pods=1_000_000, seed=0x5EED0003, **kw):
+    """C3 with realistic quantities: decimal-SI memory requests (500M, 1G,
+    3G, ...) on binary-SI capacities (64Gi .. 512Gi), as resource.Quantity accepts any mix
+    (vendor/k8s.io/apimachinery/pkg/api/resource/quantity.go:531-566)."""
+    kw.setdefault("mem_decimal", True)
+    return synth_trace(n_nodes, n_pods, seed, taints=True, labels=True, tolerations=True,
+                       selectors=True, config="C3q", **kw)
 
 
 def c4_scenario(s: int, n_nodes=2000, n_pods=10_000, **kw):

@@ -9,7 +9,7 @@ Per window: blake2b-128 of the binds' (node int32, status int32, tick int64) arr
 order; at sampled window ends: blake2b-128 of usage[n][3] (int64, C order) at that tick.
 The GPU test (tests/test_engine_gpu_full_run.py) recomputes the same digests from the engine.
 
-    python tests/golden/make_full_run.py [--threads 8] [--only c3|c5]
+    python tests/golden/make_full_run.py [--threads 8] [--only c3|c5|c3q]
 """
 import argparse
 import hashlib
@@ -38,6 +38,10 @@ RUNS = {
     "c3": (lambda: tracegen.c3_trace(n_nodes=50_000, n_pods=1_000_000), 1_000_000, 32_768, 2),
     # bench.py's C5 leg: warm-up + 4 timed + 1 profiled steps of 32,768 pods = 196,608 pods
     "c5": (lambda: tracegen.c5_trace(n_pods=196_608), 196_608, 16_384, 2),
+    # C3 with decimal-SI memory requests on binary-SI capacities (the wide evaluator class):
+    # the first 131,072 pods of the 1M-pod trace bench.py's c3q leg uses
+    "c3q": (lambda: tracegen.slice_pods(tracegen.c3q_trace(n_nodes=50_000, n_pods=1_000_000), 0, 131_072),
+            131_072, 16_384, 2),
 }
 
 

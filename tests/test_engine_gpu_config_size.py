@@ -119,6 +119,25 @@ def test_c3_whole_trace_matches_oracle_golden(c3, flags):
     full_run_digest.check_engine_run(eng, g, "c3")
 
 
+@pytest.fixture(scope="module")
+def c3q():
+    tr = tracegen.slice_pods(tracegen.c3q_trace(n_nodes=50_000, n_pods=1_000_000), 0, 131_072)
+    return tr, encoded(tr)
+
+
+@pytest.mark.parametrize("flags", [0, 128], ids=["default", "seq"])
+def test_c3q_decimal_memory_prefix_matches_oracle_golden(c3q, flags):
+    """Realistic quantities: decimal-SI memory requests on binary-SI
+    capacities — memory scales to 2^31 units, the wide evaluator class.  The first 131,072 pods
+    bind-for-bind against the oracle's committed digests (tests/golden/full_run.json "c3q")."""
+    tr, enc = c3q
+    g = full_run_digest.load("c3q")
+    assert g is not None and g["pods"] == tr["pods"]["m"] and g["nodes"] == tr["nodes"]["n"]
+    eng = make_engine(tr, enc, MODE, engine_flags=flags)
+    eng.submit(enc["pods"])
+    full_run_digest.check_engine_run(eng, g, "c3q")
+
+
 def test_c3_reference_literal_prefix(c3):
     """The reference's own filter behaviour at C3 size: scheduleOneFilter's result is discarded
     (kubesim/kubesim.go:182), so the filters constrain nothing and only admission decides Ok vs
