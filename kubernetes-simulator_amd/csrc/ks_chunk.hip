@@ -5,7 +5,7 @@
 // per kubesim/node/node.go:36-60) and the expiries due by its tick leave.  Write f_i(w_{<i}) for
 // that argmax given the earlier winners.  This resolver splits f_i into
 //   S_i(W) = the first entry of pod i's static candidate list cl_i whose node no earlier pod bound
-//            (cl_i, built by chunk_cl_kernel: pod i's snapshot top-L list entries that no pre-batch
+//            (cl_i, built by cand_list, ks_seq.hip: pod i's snapshot top-L list entries that no pre-batch
 //            expiry of the window touches — their snapshot key is exact while unbound — and every
 //            expiry node E whose exact key at pod i's tick reaches thr_i, the list's last key; any
 //            other node scores below thr_i), and
@@ -31,13 +31,11 @@ constexpr int kLanesPerPod = kThreads / 64;  // sweep phases: 64 chunk pods x 8 
 constexpr int kB = kWinMaxB;  // pods per batch
 constexpr int kC = 64;          // pods per chunk: one lane each
 constexpr int kR = kChR;        // static candidates kept per pod
-constexpr int kCid = 1024;      // distinct candidate nodes per batch (E nodes first)
+constexpr int kCid = 1024;      // candidate ids per batch (the batch's candidate slots)
+constexpr int kCidSlots = kCid - kR;  // slots that are cids; the rest: pod 0's private cids
 constexpr int kSlots = kWinSlots;
 constexpr int kSeg = 5;         // stored state segments per replayed node within a chunk
 constexpr int kPend = 4;        // pending own expiries per replayed node
-constexpr int kHashLog2 = 11, kHash = 1 << kHashLog2;
-constexpr int kL = kTopL;
-constexpr int kClBuf = 256;
 constexpr int kWaves = kThreads / kWave;
 constexpr int16_t kNoSeg = INT16_MAX;
 constexpr int kMOvf = kSeg, kMCid = kSeg + 1;
@@ -72,7 +70,6 @@ struct NS32 {
 };
 
 __device__ __forceinline__ int32_t key_node(uint64_t key) { return (int32_t)(0xFFFFFFFFu - (uint32_t)key); }
-__device__ __forceinline__ uint32_t hslot(int32_t n) { return ((uint32_t)n * 2654435761u) >> (32 - kHashLog2); }
 __device__ __forceinline__ int32_t clamp32(int64_t v) { return (int32_t)(v > INT_MAX ? INT_MAX : v); }
 
 // CreatePod admission (kubesim/node/node.go:44-47), requests in int64
@@ -88,69 +85,6 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
     const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
     const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
     return ((uint64_t)hi << 32) | lo;
-}
-
-// ---------------------------------------------------------------------------------------------
-// Static candidates of pod i (one workgroup per pod): its top-L entries outside E and the E nodes
-// whose key at pod i's tick (the pre-batch expiries of slots < win_hi[i] applied) reaches thr.
-template <int kMode>
-__global__ __launch_bounds__(256) void chunk_cl_kernel(const EngineArgs* __restrict__ A) {
-    const EngineArgs& a = A[0];
-    WinWS& ws = *a.sw;
-    const int i = blockIdx.x, tid = threadIdx.x;
-    if (i >= ws.nb) return;
-    const int64_t start = a.ctr[kCtrStart];
-    __shared__ uint64_t buf[kClBuf];
-    __shared__ int cnt;
-    if (tid == 0) cnt = 0;
-    __syncthreads();
-    const PodRec p = a.pods[start + i];
-    const uint64_t last = a.cand[(int64_t)i * kL + kL - 1];
-    const bool full = last != 0;
-    const uint64_t thr = full ? last : 1ull;
-    const int hi = ws.win_hi[i], n_e = ws.n_e;
-    for (int k = tid; k < n_e; k += 256) {
-        const int32_t n = ws.e_node[k];
-        NodeV v = load_node(a.s, n);
-        for (int u = ws.e_off[k], ue = ws.e_off[k + 1]; u < ue; ++u) {
-            const int x = ws.e_slot[u];
-            if (x >= hi) break;  // ascending
-            v.rc -= ws.ex_req[x][0]; v.rm -= ws.ex_req[x][1]; v.rg -= ws.ex_req[x][2]; v.nr -= 1;
-        }
-        const uint64_t key = make_key(eval_t<kMode>(a.c, p, v), (uint32_t)n);
-        if (key >= thr) {
-            const int pos = atomicAdd(&cnt, 1);
-            if (pos < kClBuf) buf[pos] = key;
-        }
-    }
-    if (tid < kL) {
-        const uint64_t x = a.cand[(int64_t)i * kL + tid];
-        if (x != 0 && a.e_idx[key_node(x)] < 0) {
-            const int pos = atomicAdd(&cnt, 1);
-            if (pos < kClBuf) buf[pos] = x;
-        }
-    }
-    __syncthreads();
-    const int c = cnt, n = c < kClBuf ? c : kClBuf;
-    if (tid < n) {  // rank by counting (keys are distinct: the node is in the low bits)
-        const uint64_t me = buf[tid];
-        int r = 0;
-        for (int u = 0; u < n; ++u) r += buf[u] > me;
-        if (r < kR) {
-            // the chunk kernel reads its candidate records from here: one coalesced row per id
-            // instead of ten scattered gathers on one CU
-            ws.cl_key[i][r] = me;
-            const NodeV v = load_node(a.s, key_node(me));
-            uint4* o = ws.cl_rec[i][r];
-            o[0] = make_uint4((uint32_t)(int32_t)v.ac, (uint32_t)(int32_t)v.am, (uint32_t)(int32_t)v.ag, (uint32_t)clamp32(v.ap));
-            o[1] = make_uint4((uint32_t)(int32_t)v.rc, (uint32_t)(int32_t)v.rm, (uint32_t)(int32_t)v.rg, (uint32_t)(int32_t)v.nr);
-            o[2] = make_uint4((uint32_t)v.taint, (uint32_t)(v.taint >> 32), (uint32_t)v.label, (uint32_t)(v.label >> 32));
-        }
-    }
-    if (tid == 0) {
-        ws.cl_info[i] = (c < kR ? c : kR) | (c > kR ? kClTrunc : 0) | (full ? kClFull : 0) | (c > kClBuf ? kClOvf : 0);
-        ws.cl_thr[i] = thr;
-    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -186,16 +120,13 @@ struct ChShared {
     uint64_t cd1[kC], cd2[kC];    // top two keys of pre-chunk nodes per chunk pod
     int16_t cd1c[kC], cd2c[kC];
     uint8_t cdbad[kC];
-    union {
-        struct {
-            int32_t hk[kHash], hv[kHash];
-        } h;
-        struct {
-            uint64_t k[kWaves][kC][2];
-            int16_t c[kWaves][kC][2];  // k[.][.][1] == ~0: the lane met an unknown state
-        } x;
-    } u;
-    int32_t ncid, nbc, cut, fc[2], fs[2];
+    struct {
+        uint64_t k[kWaves][kC][2];
+        int16_t c[kWaves][kC][2];  // k[.][.][1] == ~0: the lane met an unknown state
+    } x;
+    int16_t ceix[kCid];           // cid -> the node's index in E, -1 if not an E node
+    int16_t e2c[kSlots];          // E index -> cid, -1: the E node is no candidate of this batch
+    int32_t nbc, cut, fc[2], fs[2];
 #ifdef KS_CHUNK_DIAG
     int8_t why[kB];  // stop reason of a code-1 decision
 #endif
@@ -216,12 +147,13 @@ struct Replayed {
     bool hp;      // own expiries still pending
     int lost_at;  // INT_MAX, or the first pod whose state is unknown
 };
-__device__ __forceinline__ Replayed replay(ChShared& sh, int k, int n_e, int tb, bool chunk, int c0, int from, int sl, int i_end) {
+__device__ __forceinline__ Replayed replay(ChShared& sh, int k, int tb, bool chunk, int c0, int from, int sl, int i_end) {
     // (no lambdas: their by-reference closures kept the state in scratch memory)
     int32_t vrc = sh.rd[0][k], vrm = sh.rd[1][k], vrg = sh.rd[2][k], vnr = sh.rd[3][k];
     const uint16_t ec = sh.ecur[k];
     int e_u = ec & 0x7FFF;
-    const int e_end = k < n_e ? sh.eoff[k + 1] : 0;
+    const int ex = sh.ceix[k];
+    const int e_end = ex >= 0 ? sh.eoff[ex + 1] : 0;
     // pending own expiries: four named slots (eff INT_MAX = empty), updated by value selects only
     static_assert(kPend == 4, "four pending slots");
     int pe0 = INT_MAX, pe1 = INT_MAX, pe2 = INT_MAX, pe3 = INT_MAX, pj0 = 0, pj1 = 0, pj2 = 0, pj3 = 0;
@@ -384,28 +316,21 @@ __device__ __forceinline__ uint64_t cl_key(const ChShared& sh, uint32_t e) {
     return ((uint64_t)(e & 0xFFFFu) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)sh.cnode[e >> 16]);
 }
 
-// candidate id k's per-batch bookkeeping
-__device__ __forceinline__ void store_book(ChShared& sh, int k, int n_e) {
+// candidate id k's per-batch bookkeeping (its E index set first)
+__device__ __forceinline__ void store_book(ChShared& sh, int k) {
     sh.cmask[k] = 0;
     sh.fhead[k] = -1; sh.ftail[k] = -1; sh.fcur[k] = -1;
-    sh.ecur[k] = k < n_e ? (uint16_t)sh.eoff[k] : 0;
+    sh.ecur[k] = sh.ceix[k] >= 0 ? (uint16_t)sh.eoff[sh.ceix[k]] : 0;
     sh.dirty[k] = 0;
 }
 
-// candidate id k's record (int32 state, taint, label) and its bookkeeping
-__device__ __forceinline__ void store_rec(ChShared& sh, int k, int n_e, const NodeV& v) {
-    sh.rs[0][k] = (int32_t)v.ac; sh.rs[1][k] = (int32_t)v.am; sh.rs[2][k] = (int32_t)v.ag; sh.rs[3][k] = clamp32(v.ap);
-    sh.rd[0][k] = (int32_t)v.rc; sh.rd[1][k] = (int32_t)v.rm; sh.rd[2][k] = (int32_t)v.rg; sh.rd[3][k] = (int32_t)v.nr;
-    sh.rt[k] = v.taint; sh.rl[k] = v.label;
-    store_book(sh, k, n_e);
-}
-
-// the same from a packed candidate-list record (chunk_cl_kernel)
-__device__ __forceinline__ void store_prec(ChShared& sh, int k, int n_e, const uint4* r) {
+// candidate id k's record: int32 state {ac am ag ap} {rc rm rg nr}, {taint label} as u64 pairs —
+// the candidate slot's record (ks_seq.hip cand_list, the narrow format)
+__device__ __forceinline__ void store_prec(ChShared& sh, int k, const uint4* r) {
     sh.rs[0][k] = (int32_t)r[0].x; sh.rs[1][k] = (int32_t)r[0].y; sh.rs[2][k] = (int32_t)r[0].z; sh.rs[3][k] = (int32_t)r[0].w;
     sh.rd[0][k] = (int32_t)r[1].x; sh.rd[1][k] = (int32_t)r[1].y; sh.rd[2][k] = (int32_t)r[1].z; sh.rd[3][k] = (int32_t)r[1].w;
     sh.rt[k] = r[2].x | ((uint64_t)r[2].y << 32); sh.rl[k] = r[2].z | ((uint64_t)r[2].w << 32);
-    store_book(sh, k, n_e);
+    store_book(sh, k);
 }
 
 template <int kMode>
@@ -419,12 +344,14 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
     if (a.ctr[kCtrErr] != 0 || nb <= 0) return;
     const int n_e = ws.n_e, e_cnt = ws.e_cnt;
 
-    // ---- setup: pods, window, candidate ids, records
+    // ---- setup: pods, window, candidate ids, records.  The candidate ids are the batch's
+    // candidate slots (ks_seq.hip cand_list: one per distinct node of the lists, claimed through
+    // node_slot, its record staged): slots < kCidSlots are cids; a pod with an entry on a later slot
+    // cuts the batch before it — except pod 0, whose entries there take the private cids
+    // kCidSlots + r (its record read here), so every launch binds at least one pod.
     DG(uint64_t t_setup = dstamp(); uint64_t acc_cd = 0, acc_sw = 0, acc_fin = 0, acc_ph[4] = {0, 0, 0, 0}, acc_cs = 0, acc_rb = 0, acc_cdp = 0; int n_sweeps = 0, n_sonly = 0, n_chunks = 0;)
-    __shared__ int32_t fcnt[4];  // list entries per 64-pod id phase
-    if (tid == 0) { sh.ncid = n_e; sh.nbc = nb; sh.cut = INT_MAX; sh.fc[0] = sh.fc[1] = INT_MAX; sh.fs[0] = sh.fs[1] = INT_MAX; }
-    if (tid < 4) fcnt[tid] = 0;
-    for (int h = tid; h < kHash; h += kThreads) sh.u.h.hk[h] = -1;
+    const int nslot = ws.nslot < kWinMaxB * kR ? ws.nslot : kWinMaxB * kR;
+    if (tid == 0) { sh.nbc = nb; sh.cut = INT_MAX; sh.fc[0] = sh.fc[1] = INT_MAX; sh.fs[0] = sh.fs[1] = INT_MAX; }
     if (tid < nb) {
         sh.pod[tid] = a.pods[start + tid];
         sh.win_hi[tid] = (int16_t)ws.win_hi[tid];
@@ -445,140 +372,55 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
         sh.xreq[2][x] = clamp32(ws.ex_req[x][2]);
         sh.eslot[x] = (int16_t)ws.e_slot[x];
     }
-    for (int k = tid; k <= n_e; k += kThreads) sh.eoff[k] = (int16_t)ws.e_off[k];
+    for (int k = tid; k <= n_e; k += kThreads) {
+        sh.eoff[k] = (int16_t)ws.e_off[k];
+        if (k < n_e) sh.e2c[k] = -1;
+    }
+    // slot records (16 bytes per thread and step); the other cids inert
+    for (int k = tid; k < kCid; k += kThreads) { sh.ceix[k] = -1; sh.cnode[k] = -1; }
     __syncthreads();
     DG(uint64_t ts1 = dstamp();)
-    // slot x is applied from the first pod i >= 1 with win_hi[i] > x
+    // slot i is applied from the first pod i >= 1 with win_hi[i] > x
     for (int i = tid + 1; i < nb; i += kThreads)
         for (int x = sh.win_hi[i - 1]; x < sh.win_hi[i]; ++x) sh.xeff[x] = (int16_t)i;
-    // Candidate ids: E nodes are cids 0 .. n_e - 1; list nodes are numbered in (pod, entry) order,
-    // 64 pods per phase (claim by CAS, exclusive prefix of the claims over the threads, which run
-    // in pod order), so the batch is cut exactly before the first pod whose nodes do not fit
-    // kCid — pod 0 always fits (its <= L entries beside <= kSlots E nodes).  A phase starts only
-    // when the hash has room for all its entries.
-    // records are loaded after the phases (E: one per thread, issued before them)
-    static_assert(kSlots <= kThreads, "one E node per thread");
-    NodeV erec{};
-    if (tid < n_e) erec = load_node(a.s, ws.e_node[tid]);
-    if (tid < n_e) {  // distinct (the prep kernel's E)
-        const int32_t node = ws.e_node[tid];
-        uint32_t h = hslot(node);
-        while (atomicCAS(&sh.u.h.hk[h], -1, node) != -1) h = (h + 1) & (kHash - 1);  // < kHash keys
-        sh.u.h.hv[h] = tid;
-        sh.cnode[tid] = node;
+    const int nlo = nslot < kCidSlots ? nslot : kCidSlots;
+    for (int k = tid; k < nlo; k += kThreads) {
+        const int32_t nd = ws.slot_node[k];
+        const int ex = ws.slot_eix[k];
+        sh.cnode[k] = nd;
+        sh.ceix[k] = (int16_t)ex;
+        if (ex >= 0) sh.e2c[ex] = (int16_t)k;
+        store_prec(sh, k, reinterpret_cast<const uint4*>(ws.slot_rec[k]));
     }
-    __shared__ int32_t wsum[kWaves];
-    DG(uint64_t sub_k = 0;)
-    {
-        constexpr int kPP = 64, kTPP = kThreads / kPP, kEPT = (kR + kTPP - 1) / kTPP;  // 8 threads, 3 entries
-        static_assert(kTPP * kPP == kThreads, "threads per phase pod");
-        const int pl = tid / kTPP, sub = tid % kTPP;
-        // every phase's keys loaded up front (one global round instead of one per phase); phase
-        // f covers pods [64 f, 64 f + 64)
-        constexpr int kPh = (kB + kPP - 1) / kPP;
-        static_assert(kPh <= 4, "fcnt");
-        uint64_t keys[kPh][kEPT];
-#pragma unroll
-        for (int f = 0; f < kPh; ++f) {
-            const int i = kPP * f + pl;
-            const int nc = i < nb ? sh.clcnt[i] : 0;
-            if (sub == 0 && nc) atomicAdd(&fcnt[f], nc);
-#pragma unroll
-            for (int q = 0; q < kEPT; ++q) {
-                const int r = sub + kTPP * q;
-                keys[f][q] = r < nc ? ws.cl_key[i][r] : 0ull;
-            }
+    for (int k = tid; k < kCid; k += kThreads)
+        if (k >= nlo) store_book(sh, k);
+    for (int idx = tid; idx < nb * kR; idx += kThreads) {
+        const int i = idx / kR, r = idx % kR;
+        if (r >= sh.clcnt[i]) continue;
+        const uint64_t key = ws.cl_key[i][r];
+        int sl = ws.cl_slot[i][r];
+        if (sl < 0) sl = a.n_slot[key_node(key)];  // claimed by another workgroup: published by now
+        int cid = sl;
+        if (sl >= kCidSlots) {
+            if (i > 0) { atomicMin(&sh.nbc, i); continue; }
+            cid = kCidSlots + r;  // pod 0's private cid
+            const int32_t nd = key_node(key);
+            const int ex = a.e_idx[nd];
+            sh.cnode[cid] = nd;
+            sh.ceix[cid] = (int16_t)ex;
+            if (ex >= 0) sh.e2c[ex] = (int16_t)cid;
+            const NodeV v = load_node(a.s, nd);
+            const uint4 rr[3] = {make_uint4((uint32_t)(int32_t)v.ac, (uint32_t)(int32_t)v.am, (uint32_t)(int32_t)v.ag, (uint32_t)clamp32(v.ap)),
+                                 make_uint4((uint32_t)(int32_t)v.rc, (uint32_t)(int32_t)v.rm, (uint32_t)(int32_t)v.rg, (uint32_t)(int32_t)v.nr),
+                                 make_uint4((uint32_t)v.taint, (uint32_t)(v.taint >> 32), (uint32_t)v.label, (uint32_t)(v.label >> 32))};
+            store_prec(sh, cid, rr);
         }
-        __syncthreads();  // fcnt complete; the E inserts precede every list insert
-        DG(sub_k = dstamp() - ts1;)
-        // phases of 64 pods; when the first lacks hash room, pod 0 alone (always fits:
-        // n_e <= kSlots plus <= kR entries) and the batch is cut after it
-        static_assert(kSlots + kR <= kHash - kWave, "pod 0 alone always fits the hash");
-#pragma unroll
-        for (int f = 0; f < kPh; ++f) {
-            const int p0 = kPP * f, pn0 = p0 + kPP;
-            if (p0 >= nb) break;
-            const int i = p0 + pl;
-            // room check (uniform): the keys so far + every entry of this phase (ncid is rewritten
-            // only after this phase's first barrier)
-            const bool room = sh.ncid + fcnt[f] <= kHash - kWave;
-            if (!room && f > 0) { if (tid == 0) atomicMin(&sh.nbc, p0); break; }
-            const int pn = room ? pn0 : 1;
-            if (!room && tid == 0) atomicMin(&sh.nbc, 1);
-            const bool mine = i < pn && i < nb;
-            uint64_t key[kEPT];
-#pragma unroll
-            for (int q = 0; q < kEPT; ++q) key[q] = mine ? keys[f][q] : 0ull;
-            int slot[kEPT];
-            int claims = 0;
-#pragma unroll
-            for (int q = 0; q < kEPT; ++q) {
-                slot[q] = -1;
-                if (key[q] == 0) continue;
-                const int32_t node = key_node(key[q]);
-                uint32_t h = hslot(node);
-                for (;;) {  // the room check keeps the table below kHash keys: terminates
-                    const int32_t prev = atomicCAS(&sh.u.h.hk[h], -1, node);
-                    if (prev == -1) { slot[q] = (int)h | (1 << 30); ++claims; break; }
-                    if (prev == node) { slot[q] = (int)h; break; }
-                    h = (h + 1) & (kHash - 1);
-                }
-            }
-            // exclusive prefix of the claims in thread (= pod, entry) order
-            int incl = claims;
-#pragma unroll
-            for (int o = 1; o < kWave; o <<= 1) {
-                const int v = __shfl_up(incl, o);
-                if (lane >= o) incl += v;
-            }
-            if (lane == kWave - 1) wsum[wave] = incl;
-            __syncthreads();
-            int base = sh.ncid;
-            for (int g = 0; g < wave; ++g) base += wsum[g];
-            int c = base + incl - claims;
-#pragma unroll
-            for (int q = 0; q < kEPT; ++q)
-                if (slot[q] >= 0 && (slot[q] & (1 << 30))) {
-                    const int h = slot[q] & ~(1 << 30);
-                    sh.u.h.hv[h] = c;
-                    if (c < kCid) {  // fhead holds the (pod, entry) of the id's record until store_prec
-                        sh.cnode[c] = key_node(key[q]);
-                        sh.fhead[c] = (int16_t)(i * kR + sub + kTPP * q);
-                    }
-                    ++c;
-                }
-            __syncthreads();
-            if (tid == kThreads - 1) sh.ncid = c;  // the last thread's next id is the phase total
-#pragma unroll
-            for (int q = 0; q < kEPT; ++q) {
-                if (slot[q] < 0) continue;
-                const int cid = sh.u.h.hv[slot[q] & ~(1 << 30)];
-                if (cid >= kCid) atomicMin(&sh.nbc, i);
-                else sh.cl[i][sub + kTPP * q] = ((uint32_t)cid << 16) | (uint32_t)(key[q] >> 32);
-            }
-            __syncthreads();
-            if (sh.nbc < pn0) break;
-        }
-        if (tid == 0) sh.cut = INT_MAX;
+        sh.cl[i][r] = ((uint32_t)cid << 16) | (uint32_t)(key >> 32);
     }
     __syncthreads();
     nb = sh.nbc < nb ? sh.nbc : nb;
-    const int ncid = sh.ncid < kCid ? sh.ncid : kCid;
-    DG(uint64_t ts2 = dstamp();)
-    if (tid < n_e) store_rec(sh, tid, n_e, erec);
-    // list-node records: one pass after the id phases over the packed rows chunk_cl_kernel wrote
-    // (two ids per thread, 48 contiguous bytes each), so the phases carry no HBM round trip
-    static_assert(kCid <= 2 * kThreads, "two list records per thread");
-    static_assert(kB * kR <= 32767, "(pod, entry) index in int16");
-    {
-        const int k1 = n_e + tid, k2 = k1 + kThreads;
-        const uint4* rows = &ws.cl_rec[0][0][0];
-        uint4 r1[3], r2[3];
-        if (k1 < ncid) { const uint4* q = rows + 3 * sh.fhead[k1]; r1[0] = q[0]; r1[1] = q[1]; r1[2] = q[2]; }
-        if (k2 < ncid) { const uint4* q = rows + 3 * sh.fhead[k2]; r2[0] = q[0]; r2[1] = q[1]; r2[2] = q[2]; }
-        if (k1 < ncid) store_prec(sh, k1, n_e, r1);
-        if (k2 < ncid) store_prec(sh, k2, n_e, r2);
-    }
+    const int ncid = kCid;  // (inert cids have no events: skipped by every loop)
+    DG(uint64_t ts2 = dstamp(); uint64_t sub_k = 0;)
     __syncthreads();
 
     // ---- chunks
@@ -592,8 +434,8 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
         if (c0 > 0) {
             // rebase every node with events to c0 (binds < c0, events effective < c0)
             for (int k = tid; k < ncid; k += kThreads) {
-                if (k < n_e || sh.fhead[k] >= 0) {
-                    const Replayed r = replay(sh, k, n_e, tb, false, c0, c0, -1, c0);
+                if (sh.ceix[k] >= 0 || sh.fhead[k] >= 0) {
+                    const Replayed r = replay(sh, k, tb, false, c0, c0, -1, c0);
                     if (r.lost_at != INT_MAX) atomicMin(&sh.cut, c0);
                     sh.rd[0][k] = r.v.rc; sh.rd[1][k] = r.v.rm; sh.rd[2][k] = r.v.rg; sh.rd[3][k] = r.v.nr;
                     sh.ecur[k] = (uint16_t)(r.ecur | (r.hp ? 0x8000 : 0));
@@ -611,7 +453,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
             if ((tid & 1) == 0 && (tid >> 1) < c0) {
                 const int j = tid >> 1;
                 const int k = sh.wf[j];
-                if (k >= 0 && sh.fhead[k] == j) (void)replay(sh, k, n_e, tb, false, c0, c0, j, c1);
+                if (k >= 0 && sh.fhead[k] == j) (void)replay(sh, k, tb, false, c0, c0, j, c1);
                 else sh.smeta[j][kMCid] = -1;
             }
             __syncthreads();
@@ -646,8 +488,8 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                         else if (key > k2) { k2 = key; q2 = (int16_t)k; }
                     }
                 }
-                sh.u.x.k[wave][lane][0] = k1; sh.u.x.k[wave][lane][1] = bad ? ~0ull : k2;
-                sh.u.x.c[wave][lane][0] = q1; sh.u.x.c[wave][lane][1] = q2;
+                sh.x.k[wave][lane][0] = k1; sh.x.k[wave][lane][1] = bad ? ~0ull : k2;
+                sh.x.c[wave][lane][0] = q1; sh.x.c[wave][lane][1] = q2;
             }
             __syncthreads();
             DG(acc_cdp += dstamp() - tr1;)
@@ -657,11 +499,11 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                 bool bad = false;
 #pragma unroll 4
                 for (int g = 0; g < kWaves; ++g) {
-                    if (sh.u.x.k[g][lane][1] == ~0ull) { bad = true; continue; }
+                    if (sh.x.k[g][lane][1] == ~0ull) { bad = true; continue; }
 #pragma unroll
                     for (int z = 0; z < 2; ++z) {
-                        const uint64_t key = sh.u.x.k[g][lane][z];
-                        const int16_t q = sh.u.x.c[g][lane][z];
+                        const uint64_t key = sh.x.k[g][lane][z];
+                        const int16_t q = sh.x.c[g][lane][z];
                         if (key > k1) { k2 = k1; q2 = q1; k1 = key; q1 = q; }
                         else if (key > k2) { k2 = key; q2 = q; }
                     }
@@ -705,7 +547,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                 if (wcur >= 0 && __builtin_ctzll(sh.cmask[wcur]) == jr) {
                     if (!(KS_CHUNK_ABL & 2) && (sh.dirty[wcur] || sh.smeta[j][kMCid] != wcur)) {
                         sh.dirty[wcur] = 0;
-                        (void)replay(sh, wcur, n_e, tb, true, c0, c0, j, c1);
+                        (void)replay(sh, wcur, tb, true, c0, c0, j, c1);
                     }
                 } else {
                     sh.smeta[j][kMCid] = -1;
@@ -925,13 +767,27 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
     for (int x = tid; x < h_end; x += kThreads)
         if (ws.ex_ok[x]) gptr(a.expired)[ws.ex_q[x]] = 1;
     for (int k = tid; k < ncid; k += kThreads) {
-        if (k < n_e || sh.fhead[k] >= 0) {
-            const NS32 v = replay(sh, k, n_e, tb, false, 0, 0, -1, c).v;
+        if (sh.ceix[k] >= 0 || sh.fhead[k] >= 0) {
+            const NS32 v = replay(sh, k, tb, false, 0, 0, -1, c).v;
             const int32_t n = sh.cnode[k];
             a.s.rc[n] = v.rc; a.s.rm[n] = v.rm; a.s.rg[n] = v.rg; a.s.nr[n] = v.nr;
         }
-        if (k < n_e) a.e_idx[sh.cnode[k]] = -1;
     }
+    // E nodes that are no candidate of this batch: their expiries before pod c - 1's bind here
+    for (int k = tid; k < n_e; k += kThreads) {
+        const int32_t n = ws.e_node[k];
+        if (sh.e2c[k] < 0) {
+            int64_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+            for (int u = sh.eoff[k]; u < sh.eoff[k + 1]; ++u) {
+                const int x = sh.eslot[u];
+                if (x >= h_end) break;  // ascending
+                d0 += ws.ex_req[x][0]; d1 += ws.ex_req[x][1]; d2 += ws.ex_req[x][2]; d3 += 1;
+            }
+            if (d3) { a.s.rc[n] -= d0; a.s.rm[n] -= d1; a.s.rg[n] -= d2; a.s.nr[n] -= d3; }
+        }
+        a.e_idx[n] = -1;
+    }
+    for (int k = tid; k < nslot; k += kThreads) a.n_slot[ws.slot_node[k]] = -1;
     if (tid == 0) {
         a.ctr[kCtrStart] = start + c;
         const bool err = stop_code == 2 || stop_code == 3;
@@ -969,22 +825,13 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
 
 }  // namespace chk
 
-hipError_t launch_resolve_chunk(const EngineArgs* d, int mode, hipStream_t st) {
-    hipError_t r = launch_window_prep(d, st);
-    if (r != hipSuccess) return r;
+// the chunk resolver proper (its window and candidate lists: launch_window_prep(head) and
+// launch_merge_cl, ks_seq.hip)
+hipError_t launch_chunk_only(const EngineArgs* d, int mode, hipStream_t st) {
     switch (mode) {
-        case kEvalMicro:
-            hipLaunchKernelGGL(chk::chunk_cl_kernel<kEvalMicro>, dim3(kWinMaxB), dim3(256), 0, st, d);
-            hipLaunchKernelGGL(chk::resolve_chunk_kernel<kEvalMicro>, dim3(1), dim3(chk::kThreads), 0, st, d);
-            break;
-        case kEvalTiny:
-            hipLaunchKernelGGL(chk::chunk_cl_kernel<kEvalTiny>, dim3(kWinMaxB), dim3(256), 0, st, d);
-            hipLaunchKernelGGL(chk::resolve_chunk_kernel<kEvalTiny>, dim3(1), dim3(chk::kThreads), 0, st, d);
-            break;
-        default:
-            hipLaunchKernelGGL(chk::chunk_cl_kernel<kEvalNarrow>, dim3(kWinMaxB), dim3(256), 0, st, d);
-            hipLaunchKernelGGL(chk::resolve_chunk_kernel<kEvalNarrow>, dim3(1), dim3(chk::kThreads), 0, st, d);
-            break;
+        case kEvalMicro: hipLaunchKernelGGL(chk::resolve_chunk_kernel<kEvalMicro>, dim3(1), dim3(chk::kThreads), 0, st, d); break;
+        case kEvalTiny: hipLaunchKernelGGL(chk::resolve_chunk_kernel<kEvalTiny>, dim3(1), dim3(chk::kThreads), 0, st, d); break;
+        default: hipLaunchKernelGGL(chk::resolve_chunk_kernel<kEvalNarrow>, dim3(1), dim3(chk::kThreads), 0, st, d); break;
     }
     return hipGetLastError();
 }

@@ -551,7 +551,8 @@ enum : int64_t { kErrEinval = 1, kErrNotFound = 2 };
 constexpr int kWinMaxB = 256;
 constexpr int kWinSlots = 512;
 constexpr int kChR = 24;    // static candidates kept per pod
-constexpr int kRecDw = 24;  // a static candidate's staged record, dwords (the widest format, ks_seq.hip)
+constexpr int kRecDw = 20;  // a candidate node's record, dwords (the widest format: ten int64, ks_seq.hip)
+constexpr int kSlotMax = 1536;  // distinct candidate nodes per batch (the sequential resolver's slots)
 enum : int32_t { kClTrunc = 1 << 8, kClFull = 1 << 9, kClOvf = 1 << 10 };
 struct WinWS {
     int32_t nb, e_cnt, n_e, pad_;
@@ -567,9 +568,14 @@ struct WinWS {
     uint64_t cl_key[kWinMaxB][kChR];
     int32_t cl_info[kWinMaxB];            // kept count | kClTrunc | kClFull | kClOvf
     uint64_t cl_thr[kWinMaxB];            // the list's last key when full, else 1
-    // entry r's node record, packed: {ac am ag ap} {rc rm rg nr} as int32, {taint label} as u64 pairs
-    uint4 cl_rec[kWinMaxB][kChR][3];      // (chunk resolver)
-    uint32_t sq_rec[kWinMaxB][kChR][kRecDw];  // (sequential resolver, ks_seq.hip)
+    // (sequential resolver, ks_seq.hip) each distinct candidate node of the batch has one slot:
+    // entry r of pod i is slot cl_slot[i][r] (-2: claimed by another workgroup of the same launch,
+    // read node_slot; -3: no slot left)
+    int32_t cl_slot[kWinMaxB][kChR];
+    int32_t nslot;                        // slots handed out (may exceed kSlotMax: overflow)
+    int32_t slot_node[kSlotMax];
+    int32_t slot_eix[kSlotMax];           // the node's index in E, -1 if not an E node
+    uint32_t slot_rec[kSlotMax][kRecDw];  // the node's record at the batch start (narrow: 12 dwords)
 };
 
 // Arguments of the batch kernels (expire_head / scan / resolve).
@@ -594,6 +600,7 @@ struct EngineArgs {
     int32_t blk_n;
     WinWS* sw;               // batch window workspace (nullptr unless allocated)
     int32_t* e_idx;          // [n_pad] node -> index in the window's E, -1 otherwise
+    int32_t* n_slot;         // [n_pad] node -> its candidate slot in this batch, -1 otherwise
 };
 
 // Launchers and limits (defined in ks_kernels.hip).  The batch launchers take a device array of
@@ -620,13 +627,20 @@ hipError_t launch_resolve_small(const EngineArgs* d, int S, int mode, hipStream_
 int small_resolver_max_batch();
 int small_resolver_max_nodes();
 // the chunk resolver (ks_chunk.hip): one engine (S = 1), batches of <= kWinMaxB pods, evaluator
-// modes >= kEvalNarrow (node state in int32) and every total + 1 < 2^16
-hipError_t launch_resolve_chunk(const EngineArgs* d, int mode, hipStream_t st);
+// modes >= kEvalNarrow (node state in int32) and every total + 1 < 2^16; its batch is
+// launch_window_prep(head) -> scan -> launch_merge_cl -> launch_chunk_only
+hipError_t launch_chunk_only(const EngineArgs* d, int mode, hipStream_t st);
 // the sequential resolver (ks_seq.hip): one engine (S = 1), batches of <= kWinMaxB pods, any
 // evaluator mode
 hipError_t launch_resolve_seq(const EngineArgs* d, int mode, hipStream_t st);
-// the batch window (expiries of the batch's pods, the node set E): the resolvers' first kernel
-hipError_t launch_window_prep(const EngineArgs* d, hipStream_t st);
+// the batch window (expiries of the batch's pods, the node set E): the resolvers' first kernel;
+// head: also apply the expiries due before the batch's first pod (expire_head's work)
+hipError_t launch_window_prep(const EngineArgs* d, bool head, hipStream_t st);
+// the sequential resolver's batch in four launches: window_prep(head) -> scan -> merge_cl (the
+// merge kernel's exact top-L of each pod, then its candidate list) -> seq_only
+hipError_t launch_merge_cl(const EngineArgs* d, int mode, int B, const uint64_t* lists, int64_t pod_stride,
+                           int32_t nl, int64_t list_stride, int nl_max, hipStream_t st);
+hipError_t launch_seq_only(const EngineArgs* d, int mode, hipStream_t st);
 struct BindSeg {
     const int32_t* node;
     const int32_t* status;

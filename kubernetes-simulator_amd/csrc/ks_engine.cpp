@@ -154,6 +154,7 @@ struct ks_engine {
     ks::CopySeg* segs = nullptr;        // pinned segment table
     ks::CopySeg* segs_dev = nullptr;
     int seg_cap = 0, nseg = 0, seg_done = 0;
+    int64_t xpos_lo = INT64_MAX;        // exp_pos rows [xpos_lo, P) changed since the last flush
     hipEvent_t stage_ev = nullptr;      // recorded after the launch that consumed the last segments
     // per-tick path (ks_tick.hip)
     ks::TickScratch* d_tick = nullptr;
@@ -201,6 +202,7 @@ struct ks_engine {
     int64_t* d_score = nullptr;
     ks::WinWS* d_sweep = nullptr;    // batch window workspace and node -> E index (n_pad, -1)
     int32_t* d_eidx = nullptr;
+    int32_t* d_nslot = nullptr;      // node -> candidate slot (sequential resolver), -1
     unsigned long long* d_usage = nullptr;
     DVec<int32_t> d_blk;                  // usage query: candidate pod blocks
     std::vector<int32_t> h_blk;
@@ -258,6 +260,7 @@ ks::EngineArgs make_args(ks_engine* e) {
     a.PG = e->PG;
     a.sw = e->d_sweep;
     a.e_idx = e->d_eidx;
+    a.n_slot = e->d_nslot;
     return a;
 }
 
@@ -265,7 +268,18 @@ ks::EngineArgs make_args(ks_engine* e) {
 // Staged rows are applied in submission order by one scatter launch (stage_flush) or by the
 // per-tick kernel, always before the device work that reads them (stream order).  The arena is
 // reused once the launch that consumed its last segment has completed.
+hipError_t stage_copy(ks_engine* e, void* dst, const void* src, int64_t bytes);
+// The rows of exp_pos that submits rewrote since the last flush, as one segment from the host
+// mirror: per-submit rewrites overlap, and the scatter applies segments in parallel.
+hipError_t stage_xpos(ks_engine* e) {
+    const int64_t lo = e->xpos_lo;
+    if (lo >= e->P) return hipSuccess;
+    e->xpos_lo = INT64_MAX;
+    return stage_copy(e, e->exp_pos.p + lo, e->h_exp_pos.data() + lo, sizeof(int64_t) * (e->P - lo));
+}
+
 hipError_t stage_flush(ks_engine* e) {
+    if (hipError_t r = stage_xpos(e); r != hipSuccess) return r;
     if (e->seg_done >= e->nseg) return hipSuccess;
     hipError_t r = ks::launch_scatter(e->segs_dev + e->seg_done, e->nseg - e->seg_done, e->st);
     if (r == hipSuccess) r = hipEventRecord(e->stage_ev, e->st);
@@ -348,7 +362,8 @@ bool small_resolver(const ks_engine* e) {
 bool chunk_eligible(const ks_engine* e) {
     return e->B <= ks::kWinMaxB && e->mode >= ks::kEvalNarrow && key16(e);
 }
-bool seq_eligible(const ks_engine* e) { return e->B <= ks::kWinMaxB; }
+// the sequential resolver: totals in 16 bits (its candidate entries are slot << 16 | total + 1)
+bool seq_eligible(const ks_engine* e) { return e->B <= ks::kWinMaxB && key16(e); }
 enum Resolver { kResolveRole = 0, kResolveSmall = 1, kResolveChunk = 4, kResolveSeq = 5 };
 // an explicit resolver flag wins over the size class (every resolver is exact on every engine
 // its limits admit; the flags exist to test them against each other)
@@ -362,11 +377,9 @@ int resolver_of(const ks_engine* e) {
     if (small_resolver(e)) return kResolveSmall;
     return chunk_eligible(e) ? kResolveChunk : kResolveRole;
 }
+// (the chunk and sequential resolvers run fused into the batch chain, step_body)
 hipError_t launch_resolver(const ks::EngineArgs* d, int S, int mode, int which, hipStream_t st) {
-    return which == kResolveSmall ? ks::launch_resolve_small(d, S, mode, st)
-         : which == kResolveChunk ? ks::launch_resolve_chunk(d, mode, st)
-         : which == kResolveSeq ? ks::launch_resolve_seq(d, mode, st)
-                                : ks::launch_resolve(d, S, mode, st);
+    return which == kResolveSmall ? ks::launch_resolve_small(d, S, mode, st) : ks::launch_resolve(d, S, mode, st);
 }
 void update_mode(ks_engine* e) {
     int64_t m[3];
@@ -491,6 +504,7 @@ void engine_free(ks_engine* e) {
     if (e->d_score) (void)hipFree(e->d_score);
     if (e->d_sweep) (void)hipFree(e->d_sweep);
     if (e->d_eidx) (void)hipFree(e->d_eidx);
+    if (e->d_nslot) (void)hipFree(e->d_nslot);
     if (e->d_usage) (void)hipFree(e->d_usage);
     if (e->stage) (void)hipHostFree(e->stage);
     if (e->segs) (void)hipHostFree(e->segs);
@@ -838,7 +852,7 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
             HIPCHK(e, stage_flush(e));
             HIPCHK(e, e->exp_pos.reserve(e->P + m, st));
         }
-        HIPCHK(e, stage_copy(e, e->exp_pos.p + pos_lo, e->h_exp_pos.data() + pos_lo, sizeof(int64_t) * (e->P + m - pos_lo)));
+        e->xpos_lo = std::min(e->xpos_lo, pos_lo);  // staged at the next flush (stage_xpos)
         e->exp_pos.n = e->P + m;
     } else {
         HIPCHK(e, stage_flush(e));
@@ -1018,6 +1032,7 @@ static bool tick_step(ks_engine* e, int64_t t_end, ks_bind* out, int64_t cap, in
     a.expired = e->expired.p;
     a.scr = e->d_tick;
     a.out = e->h_tick_dev;
+    if (stage_xpos(e) != hipSuccess) { *rc = fail(e, KS_EDEVICE, "per-tick path: staging failed"); return true; }
     a.segs = e->segs_dev + e->seg_done;
     a.n_seg = e->nseg - e->seg_done;
     e->seg_done = e->nseg;
@@ -1050,6 +1065,8 @@ static ks_status ensure_window_ws(ks_engine* e) {
     HIPCHK(e, hipMalloc(&e->d_sweep, sizeof(ks::WinWS)));
     HIPCHK(e, hipMalloc(&e->d_eidx, sizeof(int32_t) * e->n_pad));
     HIPCHK(e, hipMemsetAsync(e->d_eidx, 0xFF, sizeof(int32_t) * e->n_pad, e->st));
+    HIPCHK(e, hipMalloc(&e->d_nslot, sizeof(int32_t) * e->n_pad));
+    HIPCHK(e, hipMemsetAsync(e->d_nslot, 0xFF, sizeof(int32_t) * e->n_pad, e->st));
     return KS_OK;
 }
 
@@ -1069,6 +1086,8 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
     const int64_t done0 = e->done;
     HIPCHK(e, stage_flush(e));
     hipStream_t st = e->st;
+    const int which = resolver_of(e);
+    const bool fused = which == kResolveSeq || which == kResolveChunk;
     HIPCHK(e, hipMemcpyAsync(e->d_ctr, e->h_ctr, 5 * sizeof(int64_t), hipMemcpyHostToDevice, st));
     HIPCHK(e, hipMemcpyAsync(e->d_args, e->h_args, sizeof(ks::EngineArgs), hipMemcpyHostToDevice, st));
     HIPCHK(e, hipEventRecord(e->ev[0], st));
@@ -1090,15 +1109,18 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
                 }
                 for (int k = 0; k < kProfEv; k++) ev[k] = e->prof_ev[kProfEv * launches + k];
             }
+            // the sequential resolver's chain is fused: window prep with the head's expiries, the
+            // scan, merge with the candidate lists, the resolver (four launches per batch)
             if (ev[0]) HIPCHK(e, hipEventRecord(ev[0], st));
-            HIPCHK(e, ks::launch_expire_head(d, 1, st));
+            HIPCHK(e, fused ? ks::launch_window_prep(d, true, st) : ks::launch_expire_head(d, 1, st));
             if (ev[1]) HIPCHK(e, hipEventRecord(ev[1], st));
             HIPCHK(e, ks::launch_scan(d, 1, e->blk_n, e->B, e->PG, e->mode, key16(e), st));
             if (ev[2]) HIPCHK(e, hipEventRecord(ev[2], st));
             const int G = e->world * e->vsh;
             const int64_t L = ks::kTopL, BL = (int64_t)e->B * L;
             if (G == 1) {
-                HIPCHK(e, ks::launch_merge(d, 1, e->B, nullptr, 0, 0, 0, nullptr, e->nblk, st));
+                HIPCHK(e, fused ? ks::launch_merge_cl(d, e->mode, e->B, nullptr, 0, 0, 0, e->nblk, st)
+                                : ks::launch_merge(d, 1, e->B, nullptr, 0, 0, 0, nullptr, e->nblk, st));
             } else {
                 for (int v = 0; v < e->vsh; v++) {
                     const int p = e->rank * e->vsh + v;
@@ -1120,10 +1142,13 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
                     HIPCHK(e, hipMemcpyAsync(e->cand_all, e->h_xbuf, sizeof(uint64_t) * slice * e->world,
                                              hipMemcpyHostToDevice, st));
                 }
-                HIPCHK(e, ks::launch_merge(d, 1, e->B, e->cand_all, L, G, BL, e->cand, G, st));
+                HIPCHK(e, fused ? ks::launch_merge_cl(d, e->mode, e->B, e->cand_all, L, G, BL, G, st)
+                                : ks::launch_merge(d, 1, e->B, e->cand_all, L, G, BL, e->cand, G, st));
             }
             if (ev[3]) HIPCHK(e, hipEventRecord(ev[3], st));
-            HIPCHK(e, launch_resolver(d, 1, e->mode, resolver_of(e), st));
+            HIPCHK(e, which == kResolveChunk ? ks::launch_chunk_only(d, e->mode, st)
+                    : which == kResolveSeq   ? ks::launch_seq_only(d, e->mode, st)
+                                             : launch_resolver(d, 1, e->mode, which, st));
             if (ev[4]) HIPCHK(e, hipEventRecord(ev[4], st));
             launches++;
         }

@@ -25,6 +25,8 @@
 //
 // Packed key: (total + 1) << 32 | (0xFFFFFFFF - node); 0 = no candidate (NotFound).  Max key =
 // highest total, ties to the lowest node index.
+#include <algorithm>
+
 #include "ks_device.h"
 
 namespace ks {
@@ -40,6 +42,10 @@ constexpr int kMaxPG = KS_MAX_PG;        // pods per scan workgroup (LDS key tab
 #define KS_SCAN_UNROLL 4
 #endif
 constexpr int kScanUnroll = KS_SCAN_UNROLL;  // pods evaluated together per scan loop step
+#ifndef KS_SCAN_TARGET_WG
+#define KS_SCAN_TARGET_WG 2048
+#endif
+constexpr int64_t kScanTargetWg = KS_SCAN_TARGET_WG;  // scan workgroups a launch aims for
 constexpr int kResolveThreads = 1024;    // 16 waves
 constexpr int kOwnerWave0 = 3;           // waves 3..15 own the touched entries, except
 #ifndef KS_WRITER_WAVE
@@ -127,8 +133,7 @@ __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict_
     const int64_t start = sload(a.ctr + kCtrStart), end = sload(a.ctr + kCtrEnd);
     if (sload(a.ctr + kCtrErr) != 0) return;
     const int64_t nb = min<int64_t>(a.B, end - start);
-    const int pg0 = blockIdx.y * a.PG;
-    if (pg0 >= nb) return;
+    if ((int64_t)blockIdx.y * a.PG >= nb) return;
     const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
 #ifdef KS_SCAN_STAMPS  // diagnostic: evaluation / extraction cycles of wave 0, ctr[20] / ctr[21]
     uint64_t st0;
@@ -140,6 +145,10 @@ __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict_
     const bool valid = node < a.c.n_nodes;
     NodeV n{};
     if (node < (int64_t)a.c.nwb * kWave) n = load_node(a.s, node);
+    // pod groups blockIdx.y, blockIdx.y + gridDim.y, ...: a large cluster's launch has enough
+    // blocks to fill the chip with gridDim.y = 1, and each node record is then read once per batch
+    for (int pg0 = blockIdx.y * a.PG; pg0 < nb; pg0 += gridDim.y * a.PG) {
+    if (pg0 != (int)blockIdx.y * a.PG) __syncthreads();  // the previous group's extraction has read kv
     const int np = (int)min<int64_t>(a.PG, nb - pg0);
     const PodRec* pp = a.pods + start + pg0;
     int b = 0;
@@ -192,6 +201,7 @@ __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict_
         }
         if (lane >= cnt && lane < kL) out[lane] = 0ull;
     }
+    }  // pod groups
 #ifdef KS_SCAN_STAMPS
     uint64_t st2;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st2)::"memory");
@@ -1170,7 +1180,12 @@ static void launch_scan_t(const EngineArgs* d, const dim3& g, size_t lds, int mo
 
 hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int mode, bool key16, hipStream_t st) {
     if (blk_n > 0 && S > 0) {
-        const dim3 g(blk_n, (B + PG - 1) / PG, S);
+        // pod-group slices per block: enough workgroups to fill the chip (~2048), the rest of the
+        // groups looped inside a workgroup over the node records it holds (C5's 4,096 blocks: one
+        // slice, each node read once per batch instead of once per group)
+        const int groups = (B + PG - 1) / PG;
+        const int64_t want = (kScanTargetWg + (int64_t)blk_n * S - 1) / ((int64_t)blk_n * S);
+        const dim3 g(blk_n, (int)std::min<int64_t>(groups, std::max<int64_t>(want, 1)), S);
         if (key16)
             launch_scan_t<uint16_t>(d, g, sizeof(uint16_t) * kBlockNodes * PG, mode, st);
         else

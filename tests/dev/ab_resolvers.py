@@ -34,6 +34,8 @@ for rep in range(2):
         if os.environ.get("KS_DIAG_LIB"):
             d = eng.debug_counters()
             extra = " diag " + " ".join(str(int(x)) for x in d[5:16])
+            nl_ = max(int(d[5]), 1)
+            extra += " | cycles/launch: " + " ".join(f"{int(x) // nl_}" for x in d[16:24])
         print(f"{nm:10s}: resolve {st['resolve_ms'] / nl * 1e3:6.1f} us/launch ({st['resolve_ms'] * 1e6 / max(st['pods'], 1):5.0f} ns/pod), "
               f"scan {st['scan_ms'] / nl * 1e3:5.1f}, other {st['other_ms'] / nl * 1e3:5.1f}; {st['pods'] / nl:6.1f} pods/launch; "
               f"{65536 / dt:8.0f} pods/s; crc {crc:08x}{extra}", flush=True)

@@ -15,7 +15,7 @@ import time
 import numpy as np
 import pytest
 
-from harness import assert_same_binds, encoded, make_engine, make_oracle
+from harness import assert_same_binds, encoded, make_engine, make_oracle, small_trace
 from kubesim_amd import tracegen
 from kubesim_amd.kubesim import KubeSim, TraceSubmitter, head_probe
 
@@ -160,8 +160,8 @@ def test_tick_path_dense_expiries_mixed_steps_and_probes():
         assert_same_binds(got, ob)
         np.testing.assert_array_equal(eng.usage(), ora.usage(), err_msg=f"phase {phase}")
         t += k
-        q = eng._submitted - eng.queued
-        if q < p["m"]:
+        q = min(eng._submitted - eng.queued, eng._submitted - 1)  # the queue head, else the last pod
+        if q >= 0:
             feas, score = ora.eval(q)
             np.testing.assert_array_equal(eng.filter(q), feas)
             np.testing.assert_array_equal(eng.score(q), score)
@@ -172,7 +172,7 @@ def test_tick_path_stops_as_run(mode, code):
     """NotFound (no candidate) and a bad simSpec stop Run at that pod's tick (kubesim.go:217-220,
     pod.go:31-39): the per-tick path returns the same error, binds and tick as the oracle."""
     from kubesim_amd.engine import KsError
-    tr = small_trace(5, n_nodes=64, n_pods=40)
+    tr = small_trace(5, n_nodes=64, n_pods=40, selectors=False)  # (a selector no node carries: NotFound)
     tr["pods"]["arrival"][:] = np.arange(1, 41)
     m = "feeds_all_lrba"
     if mode == "bad_spec":
