@@ -98,12 +98,12 @@ typedef struct {
  * one, NO_TINY skips tiny and micro, NO_MICRO skips micro; all are exact, the flags exist to test
  * them against each other. */
 enum { KS_ENGINE_FORCE_WIDE = 1, KS_ENGINE_NO_TINY = 2, KS_ENGINE_NO_MICRO = 4,
-       /* resolvers for batches of clusters above the small class (all give the same binds; the
+       /* resolvers for batches of clusters above the small class (both give the same binds; the
         * flags exist to test them against each other): ONE_POD = the role-split one-pod-per-
         * barrier resolver; CHUNK = chunked Jacobi sweeps in one workgroup's LDS (ks_step only,
-        * evaluator modes >= narrow); SEQ = the one-wave FIFO loop over static candidate lists
-        * (ks_step only).  Bits 16 and 32 (the retired pair and sweep resolvers) are rejected. */
-       KS_ENGINE_ONE_POD_RESOLVER = 8, KS_ENGINE_CHUNK_RESOLVER = 64, KS_ENGINE_SEQ_RESOLVER = 128 };
+        * evaluator modes >= narrow, totals < 2^16).  Bits 16, 32 and 128 (the retired pair, sweep
+        * and sequential resolvers) are rejected. */
+       KS_ENGINE_ONE_POD_RESOLVER = 8, KS_ENGINE_CHUNK_RESOLVER = 64 };
 
 typedef struct {
     int64_t pod;    /* FIFO index (submission order) */

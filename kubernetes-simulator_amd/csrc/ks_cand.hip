@@ -1,0 +1,357 @@
+// ks_cand.hip — a batch's expiry window and static candidate lists (gfx950), the chunk resolver's
+// inputs (ks_chunk.hip).
+//
+// The reference binds one pod per tick in FIFO order (kubesim/kubesim.go:105-121, 143-166): pod i
+// takes the argmax of its key over every node, on the state that the binds of the pods before it
+// (admitted per kubesim/node/node.go:36-60) and the expiries due by its tick leave.  After the scan
+// (ks_kernels.hip) every pod of the batch has per-block top-L lists; this file turns them into
+// what the resolver needs, in two launches around the scan:
+//
+//   window_prep_kernel   (before the scan) the expiries due before the batch's first pod, applied to
+//                        the node state (expire_head's work); the batch's expiry window: the
+//                        expiries due before pods 1 .. nb-1 (slots), the distinct nodes E of the
+//                        pre-batch pods among them, each pod's own slot.
+//   merge_cl_kernel      (after the scan, one workgroup per pod) the exact top-L of the pod's block
+//                        lists (the merge kernel's algorithm), then its static candidates cl_i: the
+//                        top-L entries outside E (their snapshot key is exact while the node is
+//                        unbound) and every E node whose exact key at pod i's tick (the pre-batch
+//                        expiries due by then applied) reaches thr_i, the list's last key — sorted,
+//                        <= kChR.  Any node outside cl_i that no earlier pod of the batch bound
+//                        scores below thr_i.  Every distinct candidate node of the batch gets one
+//                        slot (claimed through node_slot) with its record at the batch start.
+#include <climits>
+
+#include "ks_device.h"
+
+namespace ks {
+namespace sq {
+
+constexpr int kL = kTopL;
+constexpr int kB = kWinMaxB;
+constexpr int kR = kChR;
+constexpr int kES = kB / kWave;            // entry register slots (one entry per bind at most)
+constexpr int kPrepThreads = 1024;
+constexpr int kEHashLog2 = 11, kEHash = 1 << kEHashLog2;
+constexpr int kClBuf = 256;
+static_assert(kR <= kWave, "one candidate per lane");
+static_assert(kWinSlots <= kPrepThreads, "one window slot per prep thread");
+static_assert(kES * kWave < 1023, "entry index fits the ikey's 10 bits");
+
+__device__ __forceinline__ int32_t key_node(uint64_t key) { return (int32_t)(0xFFFFFFFFu - (uint32_t)key); }
+__device__ __forceinline__ uint32_t ehslot(int32_t n) { return ((uint32_t)n * 2654435761u) >> (32 - kEHashLog2); }
+__device__ __forceinline__ int32_t clamp32(int64_t v) { return (int32_t)(v > INT_MAX ? INT_MAX : v); }
+
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T* cg(const T* p) {
+    return (const __attribute__((address_space(1))) T*)p;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Window: the expiries attached to pods start+1 .. start+nb-1 (exp_off CSR), one slot each; the
+// batch shrinks to the largest prefix whose window fits kWinSlots.  E = the distinct nodes of the
+// slots whose pod was bound Ok before the batch and has not expired; e_idx marks them.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kPrepThreads) void window_prep_kernel(const EngineArgs* __restrict__ A, int head) {
+    const EngineArgs& a = A[0];
+    WinWS& ws = *a.sw;
+    const int tid = threadIdx.x;
+    __shared__ int32_t hk[kEHash], hv[kEHash];
+    __shared__ int32_t cnt[kWinSlots], fill[kWinSlots];
+    __shared__ int32_t s_ne;
+    const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
+    int nb = (int)min<int64_t>(min<int64_t>(a.B, kWinMaxB), end - start);
+    if (a.ctr[kCtrErr] != 0 || nb <= 0) {
+        if (tid == 0) { ws.nb = 0; ws.e_cnt = 0; ws.n_e = 0; }
+        return;
+    }
+    if (head) {  // expire_head's work: the expiries due before the batch's first pod
+        const int64_t e0 = a.exp_off[start], e1 = a.exp_off[start + 1];
+        for (int64_t e = e0 + tid; e < e1; e += kPrepThreads) {
+            const int32_t q = a.exp_pod[e];
+            if (a.b_status[q] != 0 || a.expired[q]) continue;
+            const int32_t nd = a.b_node[q];
+            const PodRec& p = a.pods[q];
+            atomicAdd((unsigned long long*)&a.s.rc[nd], (unsigned long long)(-p.req[0]));
+            atomicAdd((unsigned long long*)&a.s.rm[nd], (unsigned long long)(-p.req[1]));
+            atomicAdd((unsigned long long*)&a.s.rg[nd], (unsigned long long)(-p.req[2]));
+            atomicAdd((unsigned long long*)&a.s.nr[nd], (unsigned long long)(-1ll));
+            a.expired[q] = 1;
+        }
+    }
+    const int64_t e_base = a.exp_off[start + 1];
+    const bool fits_win = tid < nb && a.exp_off[start + tid + 1] - e_base <= kWinSlots;
+    for (int h = tid; h < kEHash; h += kPrepThreads) hk[h] = -1;
+    if (tid == 0) s_ne = 0;
+    nb = __syncthreads_count(fits_win);  // exp_off is non-decreasing: a prefix of the pods
+    const int e_cnt = (int)(a.exp_off[start + nb] - e_base);
+    if (tid < nb) {
+        ws.win_hi[tid] = tid >= 1 ? (int32_t)(a.exp_off[start + tid + 1] - e_base) : 0;
+        const int64_t pos = a.exp_pos[start + tid];
+        ws.own[tid] = (pos >= e_base && pos - e_base < e_cnt) ? (int32_t)(pos - e_base) : -1;
+    }
+    int32_t my_node = -1, my_k = -1;
+    if (tid < e_cnt) {
+        const int32_t q = a.exp_pod[e_base + tid];
+        const PodRec& pq = a.pods[q];
+        ws.ex_q[tid] = q;
+        ws.ex_req[tid][0] = pq.req[0]; ws.ex_req[tid][1] = pq.req[1]; ws.ex_req[tid][2] = pq.req[2];
+        const bool ok = q < start && a.b_status[q] == 0 && !a.expired[q];
+        ws.ex_ok[tid] = ok ? 1 : 0;
+        if (ok) my_node = a.b_node[q];
+    }
+    bool claimed = false;
+    if (my_node >= 0) {
+        uint32_t h = ehslot(my_node);
+        for (;;) {  // <= kWinSlots distinct nodes < kEHash slots: terminates
+            const int32_t prev = atomicCAS(&hk[h], -1, my_node);
+            if (prev == -1) { claimed = true; break; }
+            if (prev == my_node) break;
+            h = (h + 1) & (kEHash - 1);
+        }
+        my_k = (int32_t)h;  // hash slot; the claiming thread numbers the node
+        if (claimed) hv[h] = atomicAdd(&s_ne, 1);
+    }
+    __syncthreads();
+    const int n_e = s_ne;
+    if (tid < n_e) { cnt[tid] = 0; fill[tid] = 0; }
+    __syncthreads();
+    int k_of = -1;
+    if (my_node >= 0) {
+        k_of = hv[my_k];
+        ws.e_node[k_of] = my_node;
+        atomicAdd(&cnt[k_of], 1);
+    }
+    __syncthreads();
+    {  // exclusive prefix of the counts (n_e <= kPrepThreads: one per thread)
+        __shared__ int32_t wsum[kPrepThreads / 64];
+        const int lane = tid & 63, wv = tid >> 6;
+        const int v = tid < n_e ? cnt[tid] : 0;
+        int incl = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int u = __shfl_up(incl, o);
+            if (lane >= o) incl += u;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        int base = 0;
+        for (int g = 0; g < wv; ++g) base += wsum[g];
+        if (tid < n_e) ws.e_off[tid] = base + incl - v;
+        if (tid == n_e - 1) ws.e_off[n_e] = base + incl;
+        if (n_e == 0 && tid == 0) ws.e_off[0] = 0;
+    }
+    __syncthreads();
+    if (my_node >= 0) ws.e_slot[ws.e_off[k_of] + atomicAdd(&fill[k_of], 1)] = tid;  // slot x == tid
+    __syncthreads();
+    if (tid < n_e) {  // each node's few slots ascending
+        const int lo = ws.e_off[tid], hi = ws.e_off[tid + 1];
+        for (int u = lo + 1; u < hi; ++u) {
+            const int32_t x = ws.e_slot[u];
+            int v = u - 1;
+            while (v >= lo && ws.e_slot[v] > x) { ws.e_slot[v + 1] = ws.e_slot[v]; --v; }
+            ws.e_slot[v + 1] = x;
+        }
+        a.e_idx[ws.e_node[tid]] = tid;
+    }
+    if (tid == 0) { ws.nb = nb; ws.e_cnt = e_cnt; ws.n_e = n_e; ws.nslot = 0; }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Candidate slots.  Every distinct node in the batch's candidate lists gets one slot (the first
+// workgroup to meet it claims it through node_slot) and its record at the batch start: ac am ag ap
+// rc rm rg nr as int32 (ap clamped), taint, label — 12 dwords; the wide mode the ten int64 fields
+// (20 dwords).  The resolver stages all slots in LDS, so a pod's winner is one LDS read away.
+// ---------------------------------------------------------------------------------------------
+template <int kMode> struct Fmt {
+    static constexpr int kDw = 12;
+    static constexpr int kCap = kSlotMax;  // slots the resolver stages
+};
+template <> struct Fmt<kEvalWide> {
+    static constexpr int kDw = 20;
+    static constexpr int kCap = 896;
+};
+static_assert(Fmt<kEvalWide>::kDw <= kRecDw && Fmt<kEvalWide>::kCap <= kSlotMax, "record size");
+constexpr int kSlotsAll = kWinMaxB * kChR;  // claims a batch can make (slot_node holds every one)
+constexpr int kSlotPending = -2;
+static_assert(kSlotsAll <= 65535, "slot ids in 16 bits");
+
+template <int kMode>
+__device__ __forceinline__ void put_rec(uint32_t* o, const NodeV& v) {
+    if constexpr (kMode == kEvalWide) {
+        const int64_t f[10] = {v.ac, v.am, v.ag, v.ap, v.rc, v.rm, v.rg, v.nr, (int64_t)v.taint, (int64_t)v.label};
+#pragma unroll
+        for (int k = 0; k < 10; ++k) { o[2 * k] = (uint32_t)f[k]; o[2 * k + 1] = (uint32_t)((uint64_t)f[k] >> 32); }
+    } else {
+        o[0] = (uint32_t)(int32_t)v.ac; o[1] = (uint32_t)(int32_t)v.am; o[2] = (uint32_t)(int32_t)v.ag;
+        o[3] = (uint32_t)clamp32(v.ap);
+        o[4] = (uint32_t)(int32_t)v.rc; o[5] = (uint32_t)(int32_t)v.rm; o[6] = (uint32_t)(int32_t)v.rg;
+        o[7] = (uint32_t)(int32_t)v.nr;
+        o[8] = (uint32_t)v.taint; o[9] = (uint32_t)(v.taint >> 32); o[10] = (uint32_t)v.label; o[11] = (uint32_t)(v.label >> 32);
+    }
+}
+
+// Pod i's static candidates from its merged top-L `cand` (LDS or global), by one workgroup: the
+// kept entries (sorted, <= kR) with their slots
+template <int kMode>
+__device__ __forceinline__ void cand_list(const EngineArgs& a, WinWS& ws, int i, const uint64_t* cand) {
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    const int64_t start = a.ctr[kCtrStart];
+    __shared__ uint64_t buf[kClBuf];
+    __shared__ int cnt;
+    if (tid == 0) cnt = 0;
+    __syncthreads();
+    const PodRec p = a.pods[start + i];
+    const uint64_t last = cand[kL - 1];
+    const bool full = last != 0;
+    const uint64_t thr = full ? last : 1ull;
+    const int hi = ws.win_hi[i], n_e = ws.n_e;
+    for (int k = tid; k < n_e; k += nthr) {
+        const int32_t n = ws.e_node[k];
+        NodeV v = load_node(a.s, n);
+        for (int u = ws.e_off[k], ue = ws.e_off[k + 1]; u < ue; ++u) {
+            const int x = ws.e_slot[u];
+            if (x >= hi) break;  // ascending
+            v.rc -= ws.ex_req[x][0]; v.rm -= ws.ex_req[x][1]; v.rg -= ws.ex_req[x][2]; v.nr -= 1;
+        }
+        const uint64_t key = make_key(eval_t<kMode>(a.c, p, v), (uint32_t)n);
+        if (key >= thr) {
+            const int pos = atomicAdd(&cnt, 1);
+            if (pos < kClBuf) buf[pos] = key;
+        }
+    }
+    if (tid < kL) {
+        const uint64_t x = cand[tid];
+        if (x != 0 && a.e_idx[key_node(x)] < 0) {
+            const int pos = atomicAdd(&cnt, 1);
+            if (pos < kClBuf) buf[pos] = x;
+        }
+    }
+    __syncthreads();
+    const int c = cnt, n = c < kClBuf ? c : kClBuf;
+    __shared__ uint64_t kept[kR];
+    if (tid < n) {  // rank by counting (keys are distinct: the node is in the low bits)
+        const uint64_t me = buf[tid];
+        int r = 0;
+        for (int u = 0; u < n; ++u) r += buf[u] > me;
+        if (r < kR) kept[r] = me;
+    }
+    __syncthreads();
+    if (tid < kWave) {  // the kept entries' slots: one wave, one counter update for its claims
+        const int lane = tid;
+        const bool valid = lane < (n < kR ? n : kR);
+        const uint64_t me = valid ? kept[lane] : 0ull;
+        const int32_t nd = key_node(me);
+        int sl = valid ? atomicCAS(&a.n_slot[nd], -1, kSlotPending) : 0;
+        const bool claim = valid && sl == -1;
+        const uint64_t cm = __ballot(claim);
+        int base = 0;
+        if (cm) {
+            const int first = __ffsll((unsigned long long)cm) - 1;
+            if (lane == first) base = atomicAdd(&ws.nslot, __popcll(cm));
+            base = __shfl(base, first);
+        }
+        if (claim) {  // number it, stage its record, publish
+            sl = base + __popcll(cm & ((1ull << lane) - 1ull));
+            ws.slot_node[sl] = nd;
+            if (sl < Fmt<kMode>::kCap) {
+                put_rec<kMode>(ws.slot_rec[sl], load_node(a.s, nd));
+                ws.slot_eix[sl] = a.e_idx[nd];
+            }
+            atomicExch(&a.n_slot[nd], sl);
+        }
+        if (valid) {
+            ws.cl_key[i][lane] = me;
+            ws.cl_slot[i][lane] = sl;  // kSlotPending: read node_slot in the resolver
+        }
+    }
+    if (tid == 0) {
+        ws.cl_info[i] = (c < kR ? c : kR) | (c > kR ? kClTrunc : 0) | (full ? kClFull : 0) | (c > kClBuf ? kClOvf : 0);
+        ws.cl_thr[i] = thr;
+    }
+}
+
+// merge + candidate list of pod b in one workgroup (the merge kernel's exact top-L over nl sorted
+// lists lists[b * pod_stride + k * list_stride], ks_kernels.hip, then cand_list) — one launch
+// fewer per batch.  src == nullptr: the engine's own block lists.
+constexpr int kMergeMaxWaves = 16;
+template <int kMode>
+__global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs* __restrict__ A, const uint64_t* src,
+                                                         int64_t pod_stride, int32_t nl, int64_t list_stride) {
+    const EngineArgs& a = A[0];
+    WinWS& ws = *a.sw;
+    if (src == nullptr) {
+        src = a.lists;
+        pod_stride = (int64_t)a.nblk * kL;
+        nl = a.nblk;
+        list_stride = kL;
+    }
+    const int b = blockIdx.x;
+    if (b >= ws.nb) return;  // (the window prep cut the batch; errors left nb = 0)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint64_t top[kL];
+#pragma unroll
+    for (int k = 0; k < kL; ++k) top[k] = 0;
+    const uint64_t* lists = src + (int64_t)b * pod_stride;
+    const int nthr = blockDim.x, nwav = nthr / kWave;
+    for (int blk = tid; blk < nl; blk += nthr) {
+        const ulonglong2* lp = reinterpret_cast<const ulonglong2*>(lists + (int64_t)blk * list_stride);
+        uint64_t lv[kL];
+#pragma unroll
+        for (int k = 0; k < kL / 2; ++k) {
+            const ulonglong2 w = lp[k];
+            lv[2 * k] = w.x;
+            lv[2 * k + 1] = w.y;
+        }
+        topl_insert(top, lv);
+    }
+    __shared__ uint64_t wl[kMergeMaxWaves][kL];
+    __shared__ uint64_t pc[kL];
+    int head = 0;
+    for (int r = 0; r < kL; ++r) {
+        uint64_t h = 0;
+#pragma unroll
+        for (int k = 0; k < kL; ++k) h = (k == head) ? top[k] : h;
+        const uint64_t m = wave_max_u64(h);
+        const uint64_t hit = __ballot(h == m && m != 0);
+        if (lane == 0) wl[wave][r] = m;
+        if (hit && lane == __ffsll((unsigned long long)hit) - 1) head++;
+    }
+    __syncthreads();
+    if (wave == 0) {
+        const int nc = nwav * kL;
+        uint64_t v0 = lane < nc ? wl[lane / kL][lane % kL] : 0ull;
+        uint64_t v1 = lane + kWave < nc ? wl[(lane + kWave) / kL][(lane + kWave) % kL] : 0ull;
+#pragma unroll
+        for (int r = 0; r < kL; ++r) {
+            const uint64_t m = wave_max_u64(v0 > v1 ? v0 : v1);
+            if (lane == 0) pc[r] = m;
+            if (m == 0) continue;
+            const uint64_t h0 = __ballot(v0 == m), h1 = __ballot(v1 == m);
+            if (h0 && lane == __ffsll((unsigned long long)h0) - 1) v0 = 0;
+            if (!h0 && h1 && lane == __ffsll((unsigned long long)h1) - 1) v1 = 0;
+        }
+    }
+    __syncthreads();
+    cand_list<kMode>(a, ws, b, pc);
+}
+
+}  // namespace sq
+
+hipError_t launch_window_prep(const EngineArgs* d, bool head, hipStream_t st) {
+    hipLaunchKernelGGL(sq::window_prep_kernel, dim3(1), dim3(sq::kPrepThreads), 0, st, d, head ? 1 : 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge_cl(const EngineArgs* d, int mode, int B, const uint64_t* lists, int64_t pod_stride,
+                           int32_t nl, int64_t list_stride, int nl_max, hipStream_t st) {
+    const dim3 g(B), t(nl_max > 1024 ? 1024 : 256);
+    switch (mode) {
+        case kEvalMicro: hipLaunchKernelGGL(sq::merge_cl_kernel<kEvalMicro>, g, t, 0, st, d, lists, pod_stride, nl, list_stride); break;
+        case kEvalTiny: hipLaunchKernelGGL(sq::merge_cl_kernel<kEvalTiny>, g, t, 0, st, d, lists, pod_stride, nl, list_stride); break;
+        case kEvalNarrow: hipLaunchKernelGGL(sq::merge_cl_kernel<kEvalNarrow>, g, t, 0, st, d, lists, pod_stride, nl, list_stride); break;
+        default: hipLaunchKernelGGL(sq::merge_cl_kernel<kEvalWide>, g, t, 0, st, d, lists, pod_stride, nl, list_stride); break;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace ks

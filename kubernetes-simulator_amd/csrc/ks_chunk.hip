@@ -5,7 +5,7 @@
 // per kubesim/node/node.go:36-60) and the expiries due by its tick leave.  Write f_i(w_{<i}) for
 // that argmax given the earlier winners.  This resolver splits f_i into
 //   S_i(W) = the first entry of pod i's static candidate list cl_i whose node no earlier pod bound
-//            (cl_i, built by cand_list, ks_seq.hip: pod i's snapshot top-L list entries that no pre-batch
+//            (cl_i, built by cand_list, ks_cand.hip: pod i's snapshot top-L list entries that no pre-batch
 //            expiry of the window touches — their snapshot key is exact while unbound — and every
 //            expiry node E whose exact key at pod i's tick reaches thr_i, the list's last key; any
 //            other node scores below thr_i), and
@@ -325,7 +325,7 @@ __device__ __forceinline__ void store_book(ChShared& sh, int k) {
 }
 
 // candidate id k's record: int32 state {ac am ag ap} {rc rm rg nr}, {taint label} as u64 pairs —
-// the candidate slot's record (ks_seq.hip cand_list, the narrow format)
+// the candidate slot's record (ks_cand.hip cand_list, the narrow format)
 __device__ __forceinline__ void store_prec(ChShared& sh, int k, const uint4* r) {
     sh.rs[0][k] = (int32_t)r[0].x; sh.rs[1][k] = (int32_t)r[0].y; sh.rs[2][k] = (int32_t)r[0].z; sh.rs[3][k] = (int32_t)r[0].w;
     sh.rd[0][k] = (int32_t)r[1].x; sh.rd[1][k] = (int32_t)r[1].y; sh.rd[2][k] = (int32_t)r[1].z; sh.rd[3][k] = (int32_t)r[1].w;
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
     const int n_e = ws.n_e, e_cnt = ws.e_cnt;
 
     // ---- setup: pods, window, candidate ids, records.  The candidate ids are the batch's
-    // candidate slots (ks_seq.hip cand_list: one per distinct node of the lists, claimed through
+    // candidate slots (ks_cand.hip cand_list: one per distinct node of the lists, claimed through
     // node_slot, its record staged): slots < kCidSlots are cids; a pod with an entry on a later slot
     // cuts the batch before it — except pod 0, whose entries there take the private cids
     // kCidSlots + r (its record read here), so every launch binds at least one pod.
@@ -826,7 +826,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
 }  // namespace chk
 
 // the chunk resolver proper (its window and candidate lists: launch_window_prep(head) and
-// launch_merge_cl, ks_seq.hip)
+// launch_merge_cl, ks_cand.hip)
 hipError_t launch_chunk_only(const EngineArgs* d, int mode, hipStream_t st) {
     switch (mode) {
         case kEvalMicro: hipLaunchKernelGGL(chk::resolve_chunk_kernel<kEvalMicro>, dim3(1), dim3(chk::kThreads), 0, st, d); break;

@@ -545,13 +545,13 @@ enum : uint32_t { kFlagBadKey = 1, kFlagBadSpec = 2 };
 enum : int64_t { kErrEinval = 1, kErrNotFound = 2 };
 
 // Batch window workspace, one per engine, in HBM: the expiry window and the static candidate lists
-// of a batch (window_prep_kernel and the candidate-list kernels, ks_seq.hip), read by the chunk and
+// of a batch (window_prep_kernel and the candidate-list kernels, ks_cand.hip), read by the chunk and
 // sequential resolvers.  Batches of up to kWinMaxB pods whose expiry window holds up to kWinSlots
 // slots.
 constexpr int kWinMaxB = 256;
 constexpr int kWinSlots = 512;
 constexpr int kChR = 24;    // static candidates kept per pod
-constexpr int kRecDw = 20;  // a candidate node's record, dwords (the widest format: ten int64, ks_seq.hip)
+constexpr int kRecDw = 20;  // a candidate node's record, dwords (the widest format: ten int64, ks_cand.hip)
 constexpr int kSlotMax = 1536;  // distinct candidate nodes per batch (the sequential resolver's slots)
 enum : int32_t { kClTrunc = 1 << 8, kClFull = 1 << 9, kClOvf = 1 << 10 };
 struct WinWS {
@@ -568,7 +568,7 @@ struct WinWS {
     uint64_t cl_key[kWinMaxB][kChR];
     int32_t cl_info[kWinMaxB];            // kept count | kClTrunc | kClFull | kClOvf
     uint64_t cl_thr[kWinMaxB];            // the list's last key when full, else 1
-    // (sequential resolver, ks_seq.hip) each distinct candidate node of the batch has one slot:
+    // each distinct candidate node of the batch has one slot (ks_cand.hip):
     // entry r of pod i is slot cl_slot[i][r] (-2: claimed by another workgroup of the same launch,
     // read node_slot; -3: no slot left)
     int32_t cl_slot[kWinMaxB][kChR];
@@ -630,17 +630,13 @@ int small_resolver_max_nodes();
 // modes >= kEvalNarrow (node state in int32) and every total + 1 < 2^16; its batch is
 // launch_window_prep(head) -> scan -> launch_merge_cl -> launch_chunk_only
 hipError_t launch_chunk_only(const EngineArgs* d, int mode, hipStream_t st);
-// the sequential resolver (ks_seq.hip): one engine (S = 1), batches of <= kWinMaxB pods, any
-// evaluator mode
-hipError_t launch_resolve_seq(const EngineArgs* d, int mode, hipStream_t st);
 // the batch window (expiries of the batch's pods, the node set E): the resolvers' first kernel;
 // head: also apply the expiries due before the batch's first pod (expire_head's work)
 hipError_t launch_window_prep(const EngineArgs* d, bool head, hipStream_t st);
-// the sequential resolver's batch in four launches: window_prep(head) -> scan -> merge_cl (the
-// merge kernel's exact top-L of each pod, then its candidate list) -> seq_only
+// merge + candidate lists (ks_cand.hip): per pod the merge kernel's exact top-L over its lists, then
+// its static candidates and their slots
 hipError_t launch_merge_cl(const EngineArgs* d, int mode, int B, const uint64_t* lists, int64_t pod_stride,
                            int32_t nl, int64_t list_stride, int nl_max, hipStream_t st);
-hipError_t launch_seq_only(const EngineArgs* d, int mode, hipStream_t st);
 struct BindSeg {
     const int32_t* node;
     const int32_t* status;

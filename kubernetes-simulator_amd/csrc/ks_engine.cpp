@@ -202,7 +202,7 @@ struct ks_engine {
     int64_t* d_score = nullptr;
     ks::WinWS* d_sweep = nullptr;    // batch window workspace and node -> E index (n_pad, -1)
     int32_t* d_eidx = nullptr;
-    int32_t* d_nslot = nullptr;      // node -> candidate slot (sequential resolver), -1
+    int32_t* d_nslot = nullptr;      // node -> candidate slot of the batch (ks_cand.hip), -1
     unsigned long long* d_usage = nullptr;
     DVec<int32_t> d_blk;                  // usage query: candidate pod blocks
     std::vector<int32_t> h_blk;
@@ -356,19 +356,16 @@ bool small_resolver(const ks_engine* e) {
 // Resolvers, the same binds: the role-split resolve_kernel (16 waves, ks_kernels.hip) takes any
 // engine; the register-table resolver (4 waves, ks_resolve.hip) is lighter — four per CU, so a
 // what-if group's resolvers run side by side (C4 2.29e11 against 2.16e11 evals/s with the
-// role-split kernel's half-size class); the chunk resolver (ks_chunk.hip) and the
-// sequential resolver (ks_seq.hip) take one engine per launch, batches of <= kWinMaxB pods.
+// role-split kernel's half-size class); the chunk resolver (ks_chunk.hip) takes one
+// engine per launch, batches of <= kWinMaxB pods.
 // the chunk resolver: node state in int32 (evaluator modes >= narrow), totals in 16 bits
 bool chunk_eligible(const ks_engine* e) {
     return e->B <= ks::kWinMaxB && e->mode >= ks::kEvalNarrow && key16(e);
 }
-// the sequential resolver: totals in 16 bits (its candidate entries are slot << 16 | total + 1)
-bool seq_eligible(const ks_engine* e) { return e->B <= ks::kWinMaxB && key16(e); }
-enum Resolver { kResolveRole = 0, kResolveSmall = 1, kResolveChunk = 4, kResolveSeq = 5 };
+enum Resolver { kResolveRole = 0, kResolveSmall = 1, kResolveChunk = 4 };
 // an explicit resolver flag wins over the size class (every resolver is exact on every engine
 // its limits admit; the flags exist to test them against each other)
 int resolver_of(const ks_engine* e) {
-    if ((e->flags & KS_ENGINE_SEQ_RESOLVER) && seq_eligible(e)) return kResolveSeq;
     if ((e->flags & KS_ENGINE_CHUNK_RESOLVER) && chunk_eligible(e)) return kResolveChunk;
     if (e->flags & KS_ENGINE_ONE_POD_RESOLVER) return kResolveRole;
     // default: the register-table resolver for the small class, else the chunk resolver where
@@ -377,7 +374,7 @@ int resolver_of(const ks_engine* e) {
     if (small_resolver(e)) return kResolveSmall;
     return chunk_eligible(e) ? kResolveChunk : kResolveRole;
 }
-// (the chunk and sequential resolvers run fused into the batch chain, step_body)
+// (the chunk resolver runs fused into the batch chain, step_body)
 hipError_t launch_resolver(const ks::EngineArgs* d, int S, int mode, int which, hipStream_t st) {
     return which == kResolveSmall ? ks::launch_resolve_small(d, S, mode, st) : ks::launch_resolve(d, S, mode, st);
 }
@@ -417,7 +414,7 @@ ks_status engine_init(const ks_config* cfg, ks_engine** out) {
     if (cfg->batch_pods < 0 || cfg->batch_pods > kMaxBatch) return KS_EINVAL;
     if (cfg->engine_flags &
         ~(uint32_t)(KS_ENGINE_FORCE_WIDE | KS_ENGINE_NO_TINY | KS_ENGINE_NO_MICRO | KS_ENGINE_ONE_POD_RESOLVER |
-                    KS_ENGINE_CHUNK_RESOLVER | KS_ENGINE_SEQ_RESOLVER))
+                    KS_ENGINE_CHUNK_RESOLVER))
         return KS_EINVAL;
     int64_t const_total = 0, w_lr = 0, w_ba = 0;
     for (int i = 0; i < cfg->n_scorers; i++) {
@@ -661,7 +658,7 @@ ks_status ks_load_nodes(ks_engine* e, int64_t n, const int64_t* alloc, const uin
     // (~215 pods committed): 192 pods binds more per second on C3 (9.96e5 vs 9.12e5 pods/s,
     // 224: 9.53e5, 176: 9.64e5, 128: 9.49e5) and C5 (3.67e5 vs 3.19e5; tests/dev/ab_resolvers.py)
     if (!e->cfg.batch_pods && !e->group && !small_resolver(e) && chunk_eligible(e) &&
-        !(e->flags & (KS_ENGINE_ONE_POD_RESOLVER | KS_ENGINE_SEQ_RESOLVER)))
+        !(e->flags & KS_ENGINE_ONE_POD_RESOLVER))
         e->B = kChunkBatch;
     // pods per scan workgroup: the most pod reuse per node load that still leaves >= ~2048
     // workgroups (8 per CU) per scan
@@ -1061,7 +1058,7 @@ static bool tick_step(ks_engine* e, int64_t t_end, ks_bind* out, int64_t cap, in
 // runs a resolver using them (what-if group members never do).
 static ks_status ensure_window_ws(ks_engine* e) {
     const int r = resolver_of(e);
-    if (e->d_sweep || (r != kResolveChunk && r != kResolveSeq)) return KS_OK;
+    if (e->d_sweep || r != kResolveChunk) return KS_OK;
     HIPCHK(e, hipMalloc(&e->d_sweep, sizeof(ks::WinWS)));
     HIPCHK(e, hipMalloc(&e->d_eidx, sizeof(int32_t) * e->n_pad));
     HIPCHK(e, hipMemsetAsync(e->d_eidx, 0xFF, sizeof(int32_t) * e->n_pad, e->st));
@@ -1087,7 +1084,7 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
     HIPCHK(e, stage_flush(e));
     hipStream_t st = e->st;
     const int which = resolver_of(e);
-    const bool fused = which == kResolveSeq || which == kResolveChunk;
+    const bool fused = which == kResolveChunk;
     HIPCHK(e, hipMemcpyAsync(e->d_ctr, e->h_ctr, 5 * sizeof(int64_t), hipMemcpyHostToDevice, st));
     HIPCHK(e, hipMemcpyAsync(e->d_args, e->h_args, sizeof(ks::EngineArgs), hipMemcpyHostToDevice, st));
     HIPCHK(e, hipEventRecord(e->ev[0], st));
@@ -1109,8 +1106,8 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
                 }
                 for (int k = 0; k < kProfEv; k++) ev[k] = e->prof_ev[kProfEv * launches + k];
             }
-            // the sequential resolver's chain is fused: window prep with the head's expiries, the
-            // scan, merge with the candidate lists, the resolver (four launches per batch)
+            // the chunk resolver's chain is fused: window prep with the head's expiries, the scan,
+            // merge with the candidate lists, the resolver (four launches per batch)
             if (ev[0]) HIPCHK(e, hipEventRecord(ev[0], st));
             HIPCHK(e, fused ? ks::launch_window_prep(d, true, st) : ks::launch_expire_head(d, 1, st));
             if (ev[1]) HIPCHK(e, hipEventRecord(ev[1], st));
@@ -1146,9 +1143,7 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
                                 : ks::launch_merge(d, 1, e->B, e->cand_all, L, G, BL, e->cand, G, st));
             }
             if (ev[3]) HIPCHK(e, hipEventRecord(ev[3], st));
-            HIPCHK(e, which == kResolveChunk ? ks::launch_chunk_only(d, e->mode, st)
-                    : which == kResolveSeq   ? ks::launch_seq_only(d, e->mode, st)
-                                             : launch_resolver(d, 1, e->mode, which, st));
+            HIPCHK(e, fused ? ks::launch_chunk_only(d, e->mode, st) : launch_resolver(d, 1, e->mode, which, st));
             if (ev[4]) HIPCHK(e, hipEventRecord(ev[4], st));
             launches++;
         }
@@ -1316,7 +1311,7 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
         k16 = k16 && key16(e);
         small = small && small_resolver(e);
     }
-    // (the chunk and sequential resolvers take one engine per launch: not in groups)
+    // (the chunk resolver takes one engine per launch: not in groups)
     const int which = small ? kResolveSmall : kResolveRole;
     int64_t blocks = 0;
     for (int i = 0; i < S; i++) {

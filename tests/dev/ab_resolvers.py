@@ -1,6 +1,6 @@
 """A/B of the resolvers on the C3 bench workload (and C5 with --c5): per-launch resolve / scan /
 other device time (HIP events), pods per launch, wall pods/s and a CRC of the binds (must agree).
-    python tests/dev/ab_resolvers.py [--c5] [one_pod chunk seq seq@192 ...]   (@B = batch)"""
+    python tests/dev/ab_resolvers.py [--c5] [one_pod chunk chunk@256 ...]   (@B = batch)"""
 import os, sys, time, zlib
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -12,8 +12,8 @@ from kubesim_amd import tracegen, encode
 from kubesim_amd.engine import Engine
 args = [x for x in sys.argv[1:] if not x.startswith("--")]
 c5 = "--c5" in sys.argv
-names = args or ["chunk", "seq"]
-FLAGS = {"one_pod": 8, "chunk": 64, "seq": 128}
+names = args or ["chunk", "one_pod"]
+FLAGS = {"one_pod": 8, "chunk": 64}
 tr = tracegen.c5_trace(n_pods=120_000) if c5 else tracegen.c3_trace(n_pods=200_000)
 enc = encode.encode_trace(tr)
 for rep in range(2):

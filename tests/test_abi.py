@@ -33,9 +33,9 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_retired_resolver_flags_rejected_without_device():
-    """Bits 16 and 32 were the pair and sweep resolvers (removed in round 4): refused."""
+    """Bits 16, 32 and 128 were the pair, sweep and sequential resolvers (removed in round 4)."""
     L = _lib.load()
-    for bit in (16, 32, 256):
+    for bit in (16, 32, 128, 256):
         cfg = _lib.KsConfig()
         cfg.abi_version = _lib.KS_ABI_VERSION
         cfg.tick_seconds = 10

@@ -105,12 +105,12 @@ def test_c3_40k_pods_bit_exact_with_usage_samples(c3):
     assert_same_binds(eb, ob)
 
 
-@pytest.mark.parametrize("flags", [0, 128], ids=["default", "seq"])
+@pytest.mark.parametrize("flags", [0], ids=["default"])
 def test_c3_whole_trace_matches_oracle_golden(c3, flags):
     """Every pod of the 1M-pod trace — the whole range bench.py times — bind-for-bind against the
     oracle's committed digests (tests/golden/full_run.json, tests/golden/make_full_run.py), at
     the bench's batch (the engine default), with usage at every other window end; the engine's
-    default resolver and the forced sequential resolver."""
+    default resolver (the chunk resolver)."""
     tr, enc = c3
     g = full_run_digest.load("c3")
     assert g is not None and g["pods"] == tr["pods"]["m"] and g["nodes"] == tr["nodes"]["n"]
@@ -125,7 +125,7 @@ def c3q():
     return tr, encoded(tr)
 
 
-@pytest.mark.parametrize("flags", [0, 128], ids=["default", "seq"])
+@pytest.mark.parametrize("flags", [0], ids=["default"])
 def test_c3q_decimal_memory_prefix_matches_oracle_golden(c3q, flags):
     """Realistic quantities: decimal-SI memory requests on binary-SI
     capacities — memory scales to 2^31 units, the wide evaluator class.  The first 131,072 pods

@@ -1,9 +1,8 @@
 """Every resolver against the oracle (kubesim/kubesim.go:90-225 restated in oracle/ks_oracle.c).
 
 The engine has exact resolvers for step 4 of a batch: the role-split one-pod
-kernel, the register-table kernel (small clusters), the chunk kernel (chunked Jacobi sweeps in one
-workgroup's LDS) and the sequential kernel (one wave walks the batch over static candidate
-lists, ks_seq.hip).  The engine picks one
+kernel, the register-table kernel (small clusters) and the chunk kernel (chunked Jacobi sweeps in
+one workgroup's LDS, over the candidate lists of ks_cand.hip).  The engine picks one
 by size class; the KS_ENGINE_*_RESOLVER flags force one, and each forced resolver must give the
 oracle's binds, statuses and usage on every case below — all filter / scorer modes, batch sizes
 from 3 to 256, dense in-batch expiries, forced list exhaustion, and a C2 prefix.
@@ -15,8 +14,7 @@ from harness import MODES, assert_same_binds, encoded, engine_run, make_engine, 
 from kubesim_amd import _lib, tracegen
 
 pytestmark = pytest.mark.gpu
-RESOLVERS = {"one_pod": _lib.KS_ENGINE_ONE_POD_RESOLVER, "chunk": _lib.KS_ENGINE_CHUNK_RESOLVER,
-             "seq": _lib.KS_ENGINE_SEQ_RESOLVER}
+RESOLVERS = {"one_pod": _lib.KS_ENGINE_ONE_POD_RESOLVER, "chunk": _lib.KS_ENGINE_CHUNK_RESOLVER}
 
 
 def _run(tr, mode, ticks, batch, flags, chunks):
