@@ -27,15 +27,12 @@ namespace ks {
 namespace sq {
 
 constexpr int kL = kTopL;
-constexpr int kB = kWinMaxB;
 constexpr int kR = kChR;
-constexpr int kES = kB / kWave;            // entry register slots (one entry per bind at most)
 constexpr int kPrepThreads = 1024;
 constexpr int kEHashLog2 = 11, kEHash = 1 << kEHashLog2;
 constexpr int kClBuf = 256;
 static_assert(kR <= kWave, "one candidate per lane");
 static_assert(kWinSlots <= kPrepThreads, "one window slot per prep thread");
-static_assert(kES * kWave < 1023, "entry index fits the ikey's 10 bits");
 
 __device__ __forceinline__ int32_t key_node(uint64_t key) { return (int32_t)(0xFFFFFFFFu - (uint32_t)key); }
 __device__ __forceinline__ uint32_t ehslot(int32_t n) { return ((uint32_t)n * 2654435761u) >> (32 - kEHashLog2); }
@@ -259,9 +256,19 @@ __device__ __forceinline__ void cand_list(const EngineArgs& a, WinWS& ws, int i,
             }
             atomicExch(&a.n_slot[nd], sl);
         }
+        // a node another workgroup claimed: wait for its number (every workgroup publishes its own
+        // claims before it waits, and the claimer is running: it executed its CAS)
+        bool wait = valid && sl == kSlotPending;
+        while (__ballot(wait)) {
+            if (wait) {
+                sl = __hip_atomic_load(&a.n_slot[nd], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                wait = sl < 0;
+            }
+            if (__ballot(wait)) __builtin_amdgcn_s_sleep(1);
+        }
         if (valid) {
             ws.cl_key[i][lane] = me;
-            ws.cl_slot[i][lane] = sl;  // kSlotPending: read node_slot in the resolver
+            ws.cl_slot[i][lane] = sl;
         }
     }
     if (tid == 0) {

@@ -394,12 +394,23 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
     }
     for (int k = tid; k < kCid; k += kThreads)
         if (k >= nlo) store_book(sh, k);
-    for (int idx = tid; idx < nb * kR; idx += kThreads) {
-        const int i = idx / kR, r = idx % kR;
-        if (r >= sh.clcnt[i]) continue;
-        const uint64_t key = ws.cl_key[i][r];
-        int sl = ws.cl_slot[i][r];
-        if (sl < 0) sl = a.n_slot[key_node(key)];  // claimed by another workgroup: published by now
+    // every entry's key and slot loaded before any is used (one round of loads in flight)
+    constexpr int kEntPer = (kB * kR + kThreads - 1) / kThreads;
+    uint64_t ekey[kEntPer];
+    int32_t eslt[kEntPer];
+#pragma unroll
+    for (int q = 0; q < kEntPer; ++q) {
+        const int idx = tid + q * kThreads, i = idx / kR, r = idx % kR;
+        const bool v = i < nb && r < sh.clcnt[i];
+        ekey[q] = v ? ws.cl_key[i][r] : 0ull;
+        eslt[q] = v ? ws.cl_slot[i][r] : -1;
+    }
+#pragma unroll
+    for (int q = 0; q < kEntPer; ++q) {
+        const int idx = tid + q * kThreads, i = idx / kR, r = idx % kR;
+        if (eslt[q] < 0) continue;
+        const uint64_t key = ekey[q];
+        const int sl = eslt[q];
         int cid = sl;
         if (sl >= kCidSlots) {
             if (i > 0) { atomicMin(&sh.nbc, i); continue; }
