@@ -127,13 +127,12 @@ def stream_copy_gbs(device: int, mib: int = 2048, reps: int = 10):
         return None
 
 
-# the kernels of one batch round (ks_step: expire_head -> scan -> merge -> resolve); every
-# resolver variant counts as "resolve" (the chunk resolver is three kernels: window prep,
-# candidate lists, the resolver proper)
-BATCH_KERNELS = {"ks::expire_head_kernel": "expire_head", "ks::scan_kernel": "scan", "ks::merge_kernel": "merge",
-                 "ks::resolve_kernel": "resolve", "ks::pr::resolve_pair_kernel": "resolve",
-                 "ks::resolve_pair_kernel": "resolve", "ks::sw::sweep_prep_kernel": "resolve",
-                 "ks::chk::chunk_cl_kernel": "resolve", "ks::chk::resolve_chunk_kernel": "resolve"}
+# the kernels of one batch round.  The chunk resolver's chain (ks_step): window prep with the
+# head's expiries -> scan -> merge with the candidate lists -> the chunk kernel; the small-cluster
+# chain: expire_head -> scan -> merge -> resolve_kernel
+BATCH_KERNELS = {"ks::expire_head_kernel": "expire_head", "ks::sq::window_prep_kernel": "expire_head",
+                 "ks::scan_kernel": "scan", "ks::merge_kernel": "merge", "ks::sq::merge_cl_kernel": "merge",
+                 "ks::resolve_kernel": "resolve", "ks::chk::resolve_chunk_kernel": "resolve"}
 
 
 def load_traffic(config: str = "c3"):
@@ -226,6 +225,7 @@ def main():
     ap.add_argument("--vshards", type=int, default=1, help="c5: virtual node shards per rank")
     ap.add_argument("--no-c5", action="store_true", help="c3: skip the C5 node-sharded leg")
     ap.add_argument("--no-dropin", action="store_true", help="c3: skip the drop-in Run-loop leg")
+    ap.add_argument("--no-c3q", action="store_true", help="c3: skip the decimal-SI memory (C3q) leg")
     ap.add_argument("--c5-steps", type=int, default=4, help="c3: timed steps of the C5 leg")
     ap.add_argument("--c5-timeout", type=float, default=240.0,
                     help="c3: seconds the C5 leg may take before it is abandoned (the C3 line still prints)")
@@ -312,6 +312,7 @@ def main():
     digest_ms = (time.perf_counter() - t_u) * 1e3
     eng.close()
     dropin = dropin_leg(trace, enc, scorers, local) if rank == 0 and not args.no_dropin else None
+    c3q = c3q_leg(args, scorers, local) if rank == 0 and not args.no_c3q else None
     line = None
 
     if rank == 0:
@@ -356,6 +357,7 @@ def main():
                             "note": "ks_usage_at wall time at ticks near the end of the run, incl. the "
                                     "24 B/node copy to the host; digest = every tick of the last step's window"},
             "dropin": dropin,
+            "c3q": c3q,
             "c5_sharded": None,
             "cpu_baseline": cpu,
             "host": {"cpu": platform.processor() or platform.machine(), "nproc": os.cpu_count()},
@@ -369,6 +371,38 @@ def main():
         print(json.dumps({k: v for k, v in line.items() if k != "_printed"}), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def c3q_leg(args, scorers, device, steps=3, warmup=1, S=32768):
+    """C3q: the C3 cluster and trace with decimal-SI memory requests on binary-SI
+    capacities (tracegen.c3q_trace; the whole-run prefix is pinned by tests/golden/full_run.json
+    "c3q").  The gcd of the memory quantities drops to 2^9: the node capacities scale past the micro
+    evaluator's range.  Same timing bracket as the headline, fewer steps."""
+    from kubesim_amd import encode, tracegen
+    from kubesim_amd.engine import Engine
+    n_pods = (steps + warmup + 1) * S
+    tr = tracegen.c3q_trace(n_nodes=args.nodes, n_pods=1_000_000)
+    tr = tracegen.slice_pods(tr, 0, n_pods)
+    enc = encode.encode_trace(tr)
+    eng = Engine(tick_seconds=tr["tick_seconds"], filter_mode=1, filters=7, scorers=scorers, device=device)
+    eng.load_nodes(enc["alloc"], enc["taint"], enc["label"])
+    eng.submit(enc["pods"])
+    for _ in range(warmup):
+        eng.step(S)
+    t0 = time.perf_counter()
+    binds = 0
+    for _ in range(steps):
+        binds += len(eng.step(S))
+    dt = time.perf_counter() - t0
+    eng.set_profiling(True)
+    eng.step(S)
+    st = eng.last_step_stats()
+    eng.close()
+    L = max(st["launches"], 1)
+    return {"evals_per_s": binds * args.nodes / dt, "pods_per_s": binds / dt, "steps": steps, "pods_per_step": S,
+            "pods_per_launch": st["pods"] / L, "scan_avg_ms": st["scan_ms"] / L,
+            "resolve_avg_ms": st["resolve_ms"] / L, "other_avg_ms": st["other_ms"] / L,
+            "workload": "C3q: C3 with decimal-SI memory requests on binary-SI capacities"}
 
 
 def dropin_leg(trace, enc, scorers, device, per_tick=4000, probe_ticks=400, windowed=65536, window=1024):
