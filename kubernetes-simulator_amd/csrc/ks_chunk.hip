@@ -528,14 +528,85 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
 
         // (2) sweeps
         DG(uint64_t t1 = dstamp(); acc_cd += t1 - t0;)
-        // Rounds in two modes.  First exclusion-only rounds (w_i = the first static candidate no
-        // earlier pod takes; no evaluation, no replay) to their fixed point — a guess without the
-        // piles a cold start makes (every pod on its own best node) — then full sweeps from it.
+        // (2a) The guess: exclusion-only rounds (w_i = the first static candidate no earlier pod
+        // takes; no evaluation, no replay) to their fixed point — the sequential greedy over the
+        // lists, without the piles a cold start makes (every pod on its own best node).  One wave,
+        // lane = pod, no barrier: a round reads every lane's entries, then moves the changed
+        // lanes' mask bits; the pods before the first change are final.
+        if (wave == 0) {
+            const int i = c0 + lane;
+            const int nc = i < c1 ? sh.clcnt[i] : 0;
+            const uint64_t below = (1ull << lane) - 1ull;
+            // the lane's entries no pre-chunk bind took, in list order (static in the chunk): the
+            // list in the cache phase's (idle) buffer, its first eight in registers
+            int16_t* al = reinterpret_cast<int16_t*>(&sh.x.k[0][0][0]) + lane * kR;
+            static_assert(sizeof(sh.x.k) >= kC * kR * sizeof(int16_t), "avail lists");
+            int na = 0;
+            {
+                uint32_t e[kR];
+#pragma unroll
+                for (int q = 0; q < kR / 4; ++q) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(&sh.cl[i < c1 ? i : c0][4 * q]);
+                    e[4 * q] = v.x; e[4 * q + 1] = v.y; e[4 * q + 2] = v.z; e[4 * q + 3] = v.w;
+                }
+                int16_t fh[kR];
+#pragma unroll
+                for (int r = 0; r < kR; ++r) fh[r] = sh.fhead[r < nc ? (e[r] >> 16) : 0];
+#pragma unroll
+                for (int r = 0; r < kR; ++r) {  // compacted without branches
+                    al[na] = (int16_t)(e[r] >> 16);
+                    na += (r < nc && fh[r] < 0) ? 1 : 0;
+                }
+            }
+            static_assert(kR % 4 == 0 && kR > 8, "entry rows in 16-byte reads; two probe stages");
+            int rg[kR];
+#pragma unroll
+            for (int q = 0; q < kR; ++q) rg[q] = q < na ? al[q] : 0;
+            int cur = -1, lo_l = 0;
+            for (;;) {
+                DG(++n_sonly;)
+                const bool act = lane >= lo_l && nc > 0;
+                int nw = act ? -1 : cur;
+                {  // probe the first eight (every lane, unconditional loads), then the rest if needed
+                    uint64_t cm[8];
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) cm[q] = sh.cmask[rg[q]];
+#pragma unroll
+                    for (int q = 7; q >= 0; --q)  // the lowest free entry wins
+                        if (act && q < na && (cm[q] & below) == 0) nw = rg[q];
+                }
+                if (__ballot(act && nw < 0 && na > 8)) {
+                    uint64_t cm[kR - 8];
+#pragma unroll
+                    for (int q = 8; q < kR; ++q) cm[q - 8] = sh.cmask[rg[q]];
+                    int nw2 = -1;
+#pragma unroll
+                    for (int q = kR - 1; q >= 8; --q)
+                        if (q < na && (cm[q - 8] & below) == 0) nw2 = rg[q];
+                    if (act && nw < 0) nw = nw2;
+                }
+                const bool ch = nw != cur;
+                const uint64_t chm = __ballot(ch);
+                if (chm == 0ull) break;
+                if (ch) {
+                    if (cur >= 0) atomicAnd((unsigned long long*)&sh.cmask[cur], ~(1ull << lane));
+                    if (nw >= 0) atomicOr((unsigned long long*)&sh.cmask[nw], 1ull << lane);
+                    cur = nw;
+                }
+                lo_l = __builtin_ctzll(chm) + 1;
+            }
+            if (i < c1) {
+                sh.w[0][i] = (int16_t)cur; sh.w[1][i] = (int16_t)cur;
+                sh.code[0][i] = 0; sh.code[1][i] = 0;
+            }
+        }
+        __syncthreads();
+        DG(uint64_t tx = dstamp(); acc_cs += tx - t1;)
+        // (2b) full sweeps from the guess
         int par = 0, lo = c0, fsv = INT_MAX;
-        bool sonly = true;
         for (;;) {
-            DG(if (sonly) ++n_sonly; else ++n_sweeps; uint64_t q0 = dstamp();)
-            // A: the guesses' chunk binds (pod c0 + jr on thread 16 jr: spread over the waves)
+            DG(++n_sweeps; uint64_t q0 = dstamp();)
+            // A: the guesses' chunk binds (pod c0 + jr on thread 8 jr: spread over the waves)
             // incrementally: a pod whose guess changed moves its bit and marks both nodes dirty
             int wcur = -1;
             const int jr = tid / kLanesPerPod;
@@ -550,10 +621,9 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
             }
             __syncthreads();
             DG(uint64_t q1 = dstamp(); acc_ph[0] += q1 - q0;)
-            // B: replay each chunk node (its first chunk binder's thread) into that pod's slot
             // B: replay each changed chunk node (or one whose first binder moved) into its first
             // chunk binder's slot
-            if (!sonly && jlead && c0 + jr < c1) {
+            if (jlead && c0 + jr < c1) {
                 const int j = c0 + jr;
                 if (wcur >= 0 && __builtin_ctzll(sh.cmask[wcur]) == jr) {
                     if (!(KS_CHUNK_ABL & 2) && (sh.dirty[wcur] || sh.smeta[j][kMCid] != wcur)) {
@@ -564,96 +634,115 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                     sh.smeta[j][kMCid] = -1;
                 }
             }
-            if (!sonly) __syncthreads();  // (exclusion-only rounds replay nothing)
+            __syncthreads();
             DG(uint64_t q2 = dstamp(); acc_ph[1] += q2 - q1;)
-            // C: pod i = c0 + tid / 8, 8 lanes each
+            // C: the pods c0 + g and c0 + 63 - g on the 16 lanes of group g — together 63 rows
+            // (chunk binders before them), four per lane, so every wave evaluates the same
             {
-                constexpr int G = kLanesPerPod;
-                static_assert(G == 8 && kR <= 3 * G, "three entries per lane of an 8-lane pod group");
-                const int pi = tid / G, sub = tid % G, rowsh = lane & ~(G - 1);
-                const int i = c0 + pi;
-                const bool act = i < c1 && i >= lo;
-                const uint64_t below = (1ull << pi) - 1ull;
+                constexpr int G = 16;
+                static_assert(kThreads / G == kC / 2, "two pods per 16-lane group");
+                static_assert(kR <= 3 * (G / 2), "three entries per lane of a pod's 8-lane half");
+                const int g = tid / G, sub = tid % G, half = sub >> 3, s8 = sub & 7;
+                const int iA = c0 + g, iB = c0 + kC - 1 - g;
+                const bool actA = iA < c1 && iA >= lo, actB = iB < c1 && iB >= lo;
+                const int ih = half ? iB : iA;
+                const bool acth = half ? actB : actA;
+                // the static list of this half's pod: the lowest free entry
                 bool f[3] = {false, false, false};
                 uint32_t e[3] = {0u, 0u, 0u};
-                if (act) {
-                    const int nc = sh.clcnt[i];
+                if (acth) {
+                    const int nc = sh.clcnt[ih];
+                    const uint64_t belowh = (1ull << (ih - c0)) - 1ull;
 #pragma unroll
                     for (int q = 0; q < 3; ++q)
-                        if (sub + G * q < nc) e[q] = sh.cl[i][sub + G * q];
+                        if (s8 + 8 * q < nc) e[q] = sh.cl[ih][s8 + 8 * q];
 #pragma unroll
                     for (int q = 0; q < 3; ++q)
-                        if (sub + G * q < nc) {
+                        if (s8 + 8 * q < nc) {
                             const int c = e[q] >> 16;
-                            f[q] = sh.fhead[c] < 0 && (sh.cmask[c] & below) == 0;
+                            f[q] = sh.fhead[c] < 0 && (sh.cmask[c] & belowh) == 0;
                         }
                 }
+                const int rowsh = lane & ~7;
                 int rfree = kR;
                 uint32_t efree = 0u;
 #pragma unroll
-                for (int q = 2; q >= 0; --q) {  // the lowest free entry wins
+                for (int q = 2; q >= 0; --q) {
                     const uint32_t rq = (uint32_t)(__ballot(f[q]) >> rowsh) & 0xFFu;
                     const uint32_t eq = (uint32_t)__shfl((int)e[q], rowsh + (rq ? __builtin_ctz(rq) : 0));
-                    if (rq) { rfree = G * q + __builtin_ctz(rq); efree = eq; }
+                    if (rq) { rfree = 8 * q + __builtin_ctz(rq); efree = eq; }
                 }
-                uint64_t dk = 0;
-                int dc = -1;
-                bool bad = false;
-                if (act && !sonly) {
-                    // the chunk's first binders j = c0 + sub + 8 q before pod i: rows together
-                    // (no float-bound pruning here: measured slower — in SIMT the exact
-                    // evaluation still runs whenever one lane of the wave passes the bound)
-                    const PodRec p = sh.pod[i];
-                    constexpr int NQ = kC / G;
-                    SRow r[NQ];
+                // D over the chunk's first binders: row index rr < g is pod A's row c0 + rr, the
+                // rest pod B's row c0 + rr - g (no float-bound pruning: in SIMT the exact evaluation
+                // runs whenever one lane of the wave passes the bound)
+                uint64_t dkA = 0, dkB = 0;
+                int dcA = -1, dcB = -1;
+                bool badA = false, badB = false;
+                if (actA || actB) {
+                    const PodRec pA = sh.pod[actA ? iA : iB], pB = sh.pod[actB ? iB : iA];
+                    SRow r[4];
+                    bool isA[4];
 #pragma unroll
-                    for (int q = 0; q < NQ; ++q) {
-                        const int jj = sub + G * q;
-                        r[q] = srow(sh, c0 + (jj < pi ? jj : 0));
-                        if (jj >= pi) r[q].clear_cid();
+                    for (int q = 0; q < 4; ++q) {
+                        const int rr = sub + G * q;
+                        isA[q] = rr < g;
+                        const int j = isA[q] ? rr : rr - g;
+                        const bool v = isA[q] ? actA : (rr < kC - 1 && actB);
+                        r[q] = srow(sh, c0 + (v ? j : 0));
+                        if (!v) r[q].clear_cid();
                     }
 #pragma unroll
-                    for (int q = 0; q < NQ; ++q) {
+                    for (int q = 0; q < 4; ++q) {
                         const int k = r[q].m(kMCid);
                         if (k < 0) continue;
-                        if (r[q].m(kMOvf) <= i) { bad = true; continue; }
-                        if (KS_CHUNK_ABL & 1) continue;
-                        const uint64_t key = key_at<kMode>(a, sh, p, i, k, c0 + sub + G * q, r[q]);
-                        if (key > dk) { dk = key; dc = k; }
-                    }
-                    if (sub == 0) {  // pre-chunk nodes: the best one not rebound before pod i
-                        if (sh.cdbad[pi]) {
-                            bad = true;
-                        } else {
-                            uint64_t ck = sh.cd1[pi];
-                            int cc = sh.cd1c[pi];
-                            if (ck != 0 && (sh.cmask[cc] & below)) {
-                                ck = sh.cd2[pi];
-                                cc = sh.cd2c[pi];
-                                if (ck != 0 && (sh.cmask[cc] & below)) bad = true;
-                            }
-                            if (ck > dk) { dk = ck; dc = cc; }
+                        const int rr = sub + G * q;
+                        const int i = isA[q] ? iA : iB;
+                        if (r[q].m(kMOvf) <= i) {
+                            if (isA[q]) badA = true; else badB = true;
+                            continue;
                         }
+                        if (KS_CHUNK_ABL & 1) continue;
+                        const uint64_t key = key_at<kMode>(a, sh, isA[q] ? pA : pB, i, k,
+                                                           c0 + (isA[q] ? rr : rr - g), r[q]);
+                        if (isA[q]) { if (key > dkA) { dkA = key; dcA = k; } }
+                        else if (key > dkB) { dkB = key; dcB = k; }
+                    }
+                }
+                if ((sub & 7) == 0 && acth) {  // pre-chunk nodes: the best one not rebound before the pod
+                    const int pi = ih - c0;
+                    const uint64_t below = (1ull << pi) - 1ull;
+                    uint64_t& dk = half ? dkB : dkA;
+                    int& dc = half ? dcB : dcA;
+                    bool& bad = half ? badB : badA;
+                    if (sh.cdbad[pi]) {
+                        bad = true;
+                    } else {
+                        uint64_t ck = sh.cd1[pi];
+                        int cc = sh.cd1c[pi];
+                        if (ck != 0 && (sh.cmask[cc] & below)) {
+                            ck = sh.cd2[pi];
+                            cc = sh.cd2c[pi];
+                            if (ck != 0 && (sh.cmask[cc] & below)) bad = true;
+                        }
+                        if (ck > dk) { dk = ck; dc = cc; }
                     }
                 }
 #pragma unroll
                 for (int o = 1; o < G; o <<= 1) {
-                    const uint64_t ok = shfl_xor64(dk, o);
-                    const int oc = __shfl_xor(dc, o);
-                    if (ok > dk) { dk = ok; dc = oc; }
+                    const uint64_t okA = shfl_xor64(dkA, o), okB = shfl_xor64(dkB, o);
+                    const int ocA = __shfl_xor(dcA, o), ocB = __shfl_xor(dcB, o);
+                    if (okA > dkA) { dkA = okA; dcA = ocA; }
+                    if (okB > dkB) { dkB = okB; dcB = ocB; }
                 }
-                bad = ((__ballot(bad) >> rowsh) & 0xFFu) != 0;
-                if (sonly) {
-                    if (sub == 0 && i < c1) {
-                        const int nw = act ? (rfree < kR ? (int)(efree >> 16) : -1) : sh.w[par][i];
-                        if (act && nw != sh.w[par][i]) atomicMin(&sh.fc[par], i);
-                        sh.w[par ^ 1][i] = (int16_t)nw;
-                        sh.code[par ^ 1][i] = 0;
-                    }
-                } else if (sub == 0 && i < c1) {
+                const int gsh = lane & ~(G - 1);
+                const bool bad = half ? ((__ballot(badB) >> gsh) & 0xFFFFu) != 0 : ((__ballot(badA) >> gsh) & 0xFFFFu) != 0;
+                const uint64_t dk = half ? dkB : dkA;
+                const int dc = half ? dcB : dcA;
+                if (s8 == 0 && ih < c1) {
+                    const int i = ih;
                     int code;
                     int nw;
-                    if (act) {
+                    if (acth) {
                         const uint8_t fl = sh.clfl[i];
                         uint64_t win = 0;
                         int wc = -1;
@@ -690,7 +779,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                 }
             }
             __syncthreads();
-            DG(uint64_t q3 = dstamp(); if (sonly) acc_cs += q3 - q2; else acc_ph[2] += q3 - q2;)
+            DG(uint64_t q3 = dstamp(); acc_ph[2] += q3 - q2;)
             // D: convergence; clear this sweep's masks and the next sweep's accumulators
             const int fcv = sh.fc[par];
             fsv = sh.fs[par];
@@ -700,11 +789,6 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
             if (tid == 0) { sh.fc[par ^ 1] = INT_MAX; sh.fs[par ^ 1] = INT_MAX; }
             DG(acc_ph[3] += dstamp() - q3;)
             par ^= 1;
-            if (sonly) {
-                if (fcv == INT_MAX) { sonly = false; lo = c0; }  // full sweeps recompute every pod
-                else lo = fcv + 1;
-                continue;
-            }
             if (fcv == INT_MAX || fcv >= fsv) break;
             lo = fcv + 1;
         }
