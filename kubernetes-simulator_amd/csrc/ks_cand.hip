@@ -156,35 +156,23 @@ __global__ __launch_bounds__(kPrepThreads) void window_prep_kernel(const EngineA
 // ---------------------------------------------------------------------------------------------
 // Candidate slots.  Every distinct node in the batch's candidate lists gets one slot (the first
 // workgroup to meet it claims it through node_slot) and its record at the batch start: ac am ag ap
-// rc rm rg nr as int32 (ap clamped), taint, label — 12 dwords; the wide mode the ten int64 fields
-// (20 dwords).  The resolver stages all slots in LDS, so a pod's winner is one LDS read away.
+// rc rm rg nr in 32-bit words (capacities / usage as uint32, -1 = absent; ap clamped), taint,
+// label — 12 dwords (ks_chunk.hip NS32; the engine routes an engine here only when its scaled
+// capacities are < 2^32 - 1).  The resolver stages all slots in LDS, so a pod's winner is one LDS
+// read away.
 // ---------------------------------------------------------------------------------------------
-template <int kMode> struct Fmt {
-    static constexpr int kDw = 12;
-    static constexpr int kCap = kSlotMax;  // slots the resolver stages
-};
-template <> struct Fmt<kEvalWide> {
-    static constexpr int kDw = 20;
-    static constexpr int kCap = 896;
-};
-static_assert(Fmt<kEvalWide>::kDw <= kRecDw && Fmt<kEvalWide>::kCap <= kSlotMax, "record size");
+constexpr int kRecWords = 12;
+static_assert(kRecWords <= kRecDw, "record size");
 constexpr int kSlotsAll = kWinMaxB * kChR;  // claims a batch can make (slot_node holds every one)
 constexpr int kSlotPending = -2;
 static_assert(kSlotsAll <= 65535, "slot ids in 16 bits");
 
-template <int kMode>
 __device__ __forceinline__ void put_rec(uint32_t* o, const NodeV& v) {
-    if constexpr (kMode == kEvalWide) {
-        const int64_t f[10] = {v.ac, v.am, v.ag, v.ap, v.rc, v.rm, v.rg, v.nr, (int64_t)v.taint, (int64_t)v.label};
-#pragma unroll
-        for (int k = 0; k < 10; ++k) { o[2 * k] = (uint32_t)f[k]; o[2 * k + 1] = (uint32_t)((uint64_t)f[k] >> 32); }
-    } else {
-        o[0] = (uint32_t)(int32_t)v.ac; o[1] = (uint32_t)(int32_t)v.am; o[2] = (uint32_t)(int32_t)v.ag;
-        o[3] = (uint32_t)clamp32(v.ap);
-        o[4] = (uint32_t)(int32_t)v.rc; o[5] = (uint32_t)(int32_t)v.rm; o[6] = (uint32_t)(int32_t)v.rg;
-        o[7] = (uint32_t)(int32_t)v.nr;
-        o[8] = (uint32_t)v.taint; o[9] = (uint32_t)(v.taint >> 32); o[10] = (uint32_t)v.label; o[11] = (uint32_t)(v.label >> 32);
-    }
+    o[0] = (uint32_t)v.ac; o[1] = (uint32_t)v.am; o[2] = (uint32_t)v.ag;
+    o[3] = (uint32_t)clamp32(v.ap);
+    o[4] = (uint32_t)v.rc; o[5] = (uint32_t)v.rm; o[6] = (uint32_t)v.rg;
+    o[7] = (uint32_t)v.nr;
+    o[8] = (uint32_t)v.taint; o[9] = (uint32_t)(v.taint >> 32); o[10] = (uint32_t)v.label; o[11] = (uint32_t)(v.label >> 32);
 }
 
 // Pod i's static candidates from its merged top-L `cand` (LDS or global), by one workgroup: the
@@ -250,8 +238,8 @@ __device__ __forceinline__ void cand_list(const EngineArgs& a, WinWS& ws, int i,
         if (claim) {  // number it, stage its record, publish
             sl = base + __popcll(cm & ((1ull << lane) - 1ull));
             ws.slot_node[sl] = nd;
-            if (sl < Fmt<kMode>::kCap) {
-                put_rec<kMode>(ws.slot_rec[sl], load_node(a.s, nd));
+            if (sl < kSlotMax) {
+                put_rec(ws.slot_rec[sl], load_node(a.s, nd));
                 ws.slot_eix[sl] = a.e_idx[nd];
             }
             atomicExch(&a.n_slot[nd], sl);

@@ -63,7 +63,11 @@ __device__ __forceinline__ uint64_t dstamp() {
 #define KS_CHUNK_ABL 0  // diagnostic ablations (timing only, results invalid): 1 no D pairs, 2 no replays
 #endif
 
-// A node's state in int32 (evaluator modes >= narrow: capacities < 2^29; `ap` clamped)
+// A node's state in 32-bit words: capacities and usage as uint32 (scaled capacities < 2^32 - 1;
+// 0xFFFFFFFF = an absent capacity, -1), `ap` and `nr` as int32 (`ap` clamped).  Evaluator modes
+// >= narrow (capacities < 2^29) read the words as int32 directly; the wide mode (the decimal-SI
+// memory class: capacities up to 2^31 after the gcd scaling) widens them (wide_node) and runs the
+// wide evaluator.  Usage never exceeds its capacity (admission), so uint32 arithmetic is exact.
 struct NS32 {
     int32_t ac, am, ag, ap, rc, rm, rg, nr;
     uint64_t taint, label;
@@ -71,14 +75,27 @@ struct NS32 {
 
 __device__ __forceinline__ int32_t key_node(uint64_t key) { return (int32_t)(0xFFFFFFFFu - (uint32_t)key); }
 __device__ __forceinline__ int32_t clamp32(int64_t v) { return (int32_t)(v > INT_MAX ? INT_MAX : v); }
+__device__ __forceinline__ int64_t cap64(int32_t w) { return w == -1 ? -1 : (int64_t)(uint32_t)w; }
+__device__ __forceinline__ int64_t use64(int32_t w) { return (int64_t)(uint32_t)w; }
+// a capacity or usage in one word (values in [-1, 2^32 - 1))
+__device__ __forceinline__ int32_t word32(int64_t v) { return (int32_t)(uint32_t)v; }
 
-// CreatePod admission (kubesim/node/node.go:44-47), requests in int64
-__device__ __forceinline__ bool fits32(const PodRec& p, const NS32& n) {
-    bool ok = n.nr < n.ap;
-    if (p.keymask & 1) ok &= (int64_t)n.rc + p.req[0] <= n.ac;
-    if (p.keymask & 2) ok &= (int64_t)n.rm + p.req[1] <= n.am;
-    if (p.keymask & 4) ok &= (int64_t)n.rg + p.req[2] <= n.ag;
-    return ok;
+__device__ __forceinline__ NodeV wide_node(const NS32& n) {
+    NodeV v;
+    v.ac = cap64(n.ac); v.am = cap64(n.am); v.ag = cap64(n.ag); v.ap = n.ap;
+    v.rc = use64(n.rc); v.rm = use64(n.rm); v.rg = use64(n.rg); v.nr = n.nr;
+    v.taint = n.taint; v.label = n.label;
+    return v;
+}
+template <int kMode>
+__device__ __forceinline__ uint32_t eval32(const Cfg& c, const PodRec& p, const NS32& n) {
+    if constexpr (kMode == kEvalWide) return eval_t<kEvalWide>(c, p, wide_node(n));
+    else return eval_t<kMode>(c, p, n);
+}
+template <int kMode>
+__device__ __forceinline__ PruneF prune32(const Cfg& c, const NS32& n) {
+    if constexpr (kMode == kEvalWide) return prune_prep(c, wide_node(n));
+    else return prune_prep_t<kMode>(c, n);
 }
 
 __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
@@ -149,7 +166,8 @@ struct Replayed {
 };
 __device__ __forceinline__ Replayed replay(ChShared& sh, int k, int tb, bool chunk, int c0, int from, int sl, int i_end) {
     // (no lambdas: their by-reference closures kept the state in scratch memory)
-    int32_t vrc = sh.rd[0][k], vrm = sh.rd[1][k], vrg = sh.rd[2][k], vnr = sh.rd[3][k];
+    uint32_t vrc = (uint32_t)sh.rd[0][k], vrm = (uint32_t)sh.rd[1][k], vrg = (uint32_t)sh.rd[2][k];
+    int32_t vnr = sh.rd[3][k];
     const uint16_t ec = sh.ecur[k];
     int e_u = ec & 0x7FFF;
     const int ex = sh.ceix[k];
@@ -191,7 +209,7 @@ __device__ __forceinline__ Replayed replay(ChShared& sh, int k, int tb, bool chu
                 if (ns == kSeg) { ovf = t_; ok_ = false; }                                           \
                 else { sh.smeta[sl][ns] = (int16_t)t_; ++ns; last_t = t_; }                          \
             }                                                                                        \
-            if (ok_) *reinterpret_cast<int4*>(&sh.sst[sl][ns - 1][0]) = make_int4(vrc, vrm, vrg, vnr); \
+            if (ok_) *reinterpret_cast<int4*>(&sh.sst[sl][ns - 1][0]) = make_int4((int)vrc, (int)vrm, (int)vrg, vnr); \
         }                                                                                            \
     } while (0)
     if (sl >= 0) {
@@ -200,6 +218,7 @@ __device__ __forceinline__ Replayed replay(ChShared& sh, int k, int tb, bool chu
         KS_STORE(from);
     }
     const int32_t ac = sh.rs[0][k], am = sh.rs[1][k], ag = sh.rs[2][k], ap = sh.rs[3][k];
+    const int64_t ac64 = cap64(ac), am64 = cap64(am), ag64 = cap64(ag);
     int j = sh.fcur[k];
     uint64_t m = chunk ? sh.cmask[k] : 0ull;
     // one event loop: the next bind (final list, then the chunk mask) against the next expiry
@@ -214,7 +233,7 @@ __device__ __forceinline__ Replayed replay(ChShared& sh, int k, int tb, bool chu
         if (nx <= lim) {  // an expiry effective before the next bind (or before i_end)
             if (ne == nx) {
                 const int x = sh.eslot[e_u++];
-                vrc -= sh.xreq[0][x]; vrm -= sh.xreq[1][x]; vrg -= sh.xreq[2][x]; vnr -= 1;
+                vrc -= (uint32_t)sh.xreq[0][x]; vrm -= (uint32_t)sh.xreq[1][x]; vrg -= (uint32_t)sh.xreq[2][x]; vnr -= 1;
             } else {
                 const bool h0 = pe0 == pm, h1 = !h0 && pe1 == pm, h2 = !h0 && !h1 && pe2 == pm,
                            h3 = !h0 && !h1 && !h2;
@@ -222,7 +241,7 @@ __device__ __forceinline__ Replayed replay(ChShared& sh, int k, int tb, bool chu
                 pe0 = h0 ? INT_MAX : pe0; pe1 = h1 ? INT_MAX : pe1;
                 pe2 = h2 ? INT_MAX : pe2; pe3 = h3 ? INT_MAX : pe3;
                 const PodRec& p = sh.pod[jq];
-                vrc -= (int32_t)p.req[0]; vrm -= (int32_t)p.req[1]; vrg -= (int32_t)p.req[2]; vnr -= 1;
+                vrc -= (uint32_t)p.req[0]; vrm -= (uint32_t)p.req[1]; vrg -= (uint32_t)p.req[2]; vnr -= 1;
             }
             KS_STORE(nx);
             continue;
@@ -237,13 +256,13 @@ __device__ __forceinline__ Replayed replay(ChShared& sh, int k, int tb, bool chu
             ok = sh.adm[jb] == 1;
         } else {  // CreatePod admission (kubesim/node/node.go:44-47)
             ok = !lost && vnr < ap;
-            if (p.keymask & 1) ok &= (int64_t)vrc + p.req[0] <= ac;
-            if (p.keymask & 2) ok &= (int64_t)vrm + p.req[1] <= am;
-            if (p.keymask & 4) ok &= (int64_t)vrg + p.req[2] <= ag;
+            if (p.keymask & 1) ok &= (int64_t)vrc + p.req[0] <= ac64;
+            if (p.keymask & 2) ok &= (int64_t)vrm + p.req[1] <= am64;
+            if (p.keymask & 4) ok &= (int64_t)vrg + p.req[2] <= ag64;
             sh.adm[jb] = lost ? 2 : (ok ? 1 : 0);
         }
         if (ok && (sh.clfl[jb] & kFlRun)) {
-            vrc += (int32_t)p.req[0]; vrm += (int32_t)p.req[1]; vrg += (int32_t)p.req[2]; vnr += 1;
+            vrc += (uint32_t)p.req[0]; vrm += (uint32_t)p.req[1]; vrg += (uint32_t)p.req[2]; vnr += 1;
             KS_STORE(jb + 1);
             const int x = sh.own[jb];
             if (x >= 0) KS_PUSH(sh.xeff[x], jb);
@@ -254,7 +273,7 @@ __device__ __forceinline__ Replayed replay(ChShared& sh, int k, int tb, bool chu
     if (sl >= 0) sh.smeta[sl][kMOvf] = (int16_t)ovf;
     Replayed out;
     out.v.ac = ac; out.v.am = am; out.v.ag = ag; out.v.ap = ap;
-    out.v.rc = vrc; out.v.rm = vrm; out.v.rg = vrg; out.v.nr = vnr;
+    out.v.rc = (int32_t)vrc; out.v.rm = (int32_t)vrm; out.v.rg = (int32_t)vrg; out.v.nr = vnr;
     out.v.taint = 0; out.v.label = 0;
     out.ecur = e_u;
     out.hp = (pe0 & pe1 & pe2 & pe3) != INT_MAX;  // any slot holds a (non-negative) pod index
@@ -290,7 +309,7 @@ __device__ __forceinline__ uint64_t key_at(const EngineArgs& a, const ChShared& 
     n.ac = sh.rs[0][k]; n.am = sh.rs[1][k]; n.ag = sh.rs[2][k]; n.ap = sh.rs[3][k];
     n.rc = st.x; n.rm = st.y; n.rg = st.z; n.nr = st.w;
     n.taint = sh.rt[k]; n.label = sh.rl[k];
-    return make_key(eval_t<kMode>(a.c, p, n), (uint32_t)sh.cnode[k]);
+    return make_key(eval32<kMode>(a.c, p, n), (uint32_t)sh.cnode[k]);
 }
 
 // The same, 0 when the float upper bound of the total (prune_tmax: filters ignored, exact slack)
@@ -306,10 +325,11 @@ __device__ __forceinline__ uint64_t key_at_lb(const EngineArgs& a, const ChShare
     n.ac = sh.rs[0][k]; n.am = sh.rs[1][k]; n.ag = sh.rs[2][k]; n.ap = sh.rs[3][k];
     n.rc = st.x; n.rm = st.y; n.rg = st.z; n.nr = st.w;
     const uint32_t node = (uint32_t)sh.cnode[k];
-    const PruneF f = prune_prep_t<kMode>(a.c, n);
+    n.taint = 0; n.label = 0;
+    const PruneF f = prune32<kMode>(a.c, n);
     if (!f.live || make_key(prune_tmax(a.c, f, (float)p.req[0], (float)p.req[1]) + 1u, node) < lb) return 0;
     n.taint = sh.rt[k]; n.label = sh.rl[k];
-    return make_key(eval_t<kMode>(a.c, p, n), node);
+    return make_key(eval32<kMode>(a.c, p, n), node);
 }
 
 __device__ __forceinline__ uint64_t cl_key(const ChShared& sh, uint32_t e) {
@@ -367,9 +387,9 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
         sh.code[0][tid] = 0; sh.code[1][tid] = 0;
     }
     for (int x = tid; x < e_cnt; x += kThreads) {
-        sh.xreq[0][x] = clamp32(ws.ex_req[x][0]);
-        sh.xreq[1][x] = clamp32(ws.ex_req[x][1]);
-        sh.xreq[2][x] = clamp32(ws.ex_req[x][2]);
+        sh.xreq[0][x] = word32(ws.ex_req[x][0]);
+        sh.xreq[1][x] = word32(ws.ex_req[x][1]);
+        sh.xreq[2][x] = word32(ws.ex_req[x][2]);
         sh.eslot[x] = (int16_t)ws.e_slot[x];
     }
     for (int k = tid; k <= n_e; k += kThreads) {
@@ -421,8 +441,8 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
             sh.ceix[cid] = (int16_t)ex;
             if (ex >= 0) sh.e2c[ex] = (int16_t)cid;
             const NodeV v = load_node(a.s, nd);
-            const uint4 rr[3] = {make_uint4((uint32_t)(int32_t)v.ac, (uint32_t)(int32_t)v.am, (uint32_t)(int32_t)v.ag, (uint32_t)clamp32(v.ap)),
-                                 make_uint4((uint32_t)(int32_t)v.rc, (uint32_t)(int32_t)v.rm, (uint32_t)(int32_t)v.rg, (uint32_t)(int32_t)v.nr),
+            const uint4 rr[3] = {make_uint4((uint32_t)v.ac, (uint32_t)v.am, (uint32_t)v.ag, (uint32_t)clamp32(v.ap)),
+                                 make_uint4((uint32_t)v.rc, (uint32_t)v.rm, (uint32_t)v.rg, (uint32_t)v.nr),
                                  make_uint4((uint32_t)v.taint, (uint32_t)(v.taint >> 32), (uint32_t)v.label, (uint32_t)(v.label >> 32))};
             store_prec(sh, cid, rr);
         }
@@ -865,7 +885,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
         if (sh.ceix[k] >= 0 || sh.fhead[k] >= 0) {
             const NS32 v = replay(sh, k, tb, false, 0, 0, -1, c).v;
             const int32_t n = sh.cnode[k];
-            a.s.rc[n] = v.rc; a.s.rm[n] = v.rm; a.s.rg[n] = v.rg; a.s.nr[n] = v.nr;
+            a.s.rc[n] = use64(v.rc); a.s.rm[n] = use64(v.rm); a.s.rg[n] = use64(v.rg); a.s.nr[n] = v.nr;
         }
     }
     // E nodes that are no candidate of this batch: their expiries before pod c - 1's bind here
@@ -926,7 +946,8 @@ hipError_t launch_chunk_only(const EngineArgs* d, int mode, hipStream_t st) {
     switch (mode) {
         case kEvalMicro: hipLaunchKernelGGL(chk::resolve_chunk_kernel<kEvalMicro>, dim3(1), dim3(chk::kThreads), 0, st, d); break;
         case kEvalTiny: hipLaunchKernelGGL(chk::resolve_chunk_kernel<kEvalTiny>, dim3(1), dim3(chk::kThreads), 0, st, d); break;
-        default: hipLaunchKernelGGL(chk::resolve_chunk_kernel<kEvalNarrow>, dim3(1), dim3(chk::kThreads), 0, st, d); break;
+        case kEvalNarrow: hipLaunchKernelGGL(chk::resolve_chunk_kernel<kEvalNarrow>, dim3(1), dim3(chk::kThreads), 0, st, d); break;
+        default: hipLaunchKernelGGL(chk::resolve_chunk_kernel<kEvalWide>, dim3(1), dim3(chk::kThreads), 0, st, d); break;
     }
     return hipGetLastError();
 }

@@ -358,9 +358,16 @@ bool small_resolver(const ks_engine* e) {
 // what-if group's resolvers run side by side (C4 2.29e11 against 2.16e11 evals/s with the
 // role-split kernel's half-size class); the chunk resolver (ks_chunk.hip) takes one
 // engine per launch, batches of <= kWinMaxB pods.
-// the chunk resolver: node state in int32 (evaluator modes >= narrow), totals in 16 bits
+// the chunk resolver: node state in 32-bit words (every scaled capacity < 2^32 - 1: the modes >=
+// narrow, and the wide mode's decimal-SI memory class, whose capacities scale to 2^31), totals in
+// 16 bits
 bool chunk_eligible(const ks_engine* e) {
-    return e->B <= ks::kWinMaxB && e->mode >= ks::kEvalNarrow && key16(e);
+    bool words = e->mode >= ks::kEvalNarrow;
+    if (!words) {
+        words = true;
+        for (int k = 0; k < 3; k++) words &= e->max_alloc[k] / e->scale[k] < (int64_t)0xFFFFFFFF;
+    }
+    return e->B <= ks::kWinMaxB && words && key16(e);
 }
 enum Resolver { kResolveRole = 0, kResolveSmall = 1, kResolveChunk = 4 };
 // an explicit resolver flag wins over the size class (every resolver is exact on every engine

@@ -78,3 +78,22 @@ def test_list_exhaustion(res):
 def test_c2_prefix(res, mode):
     tr = tracegen.c2_trace(n_pods=12_000)
     _run(tr, mode, 12_000, 0, RESOLVERS[res], (4096, 7904))
+
+
+# ---- the chunk resolver on the wide evaluator (32-bit state words, ks_chunk.hip NS32) -----------
+@pytest.mark.parametrize("mode", ["feeds_all_lrba", "literal_lrba_filters_ignored"])
+def test_chunk_wide_evaluator(mode):
+    """FORCE_WIDE on small capacities: the chunk kernel's wide instantiation (widened words, the
+    wide evaluator) on the cases above."""
+    tr = small_trace(1, n_nodes=400, n_pods=600, arrival="stream")
+    _run(tr, mode, 800, 256, RESOLVERS["chunk"] | _lib.KS_ENGINE_FORCE_WIDE, (1, 7, 100, 692))
+
+
+def test_chunk_decimal_memory_class():
+    """Decimal-SI memory requests on binary-SI capacities (C3q's distributions at 2k nodes): the
+    gcd scaling leaves memory capacities up to 2^31, beyond int32 — the engine's default picks the
+    chunk resolver on uint32 words with the wide evaluator; binds, statuses and usage against the
+    oracle, with dense expiries."""
+    tr = tracegen.c3q_trace(n_nodes=2000, n_pods=8000)
+    assert int(np.max(tr["nodes"]["alloc"][:, 1])) == 512 * (1 << 30) * 1000  # 512Gi: 2^31 after the gcd
+    _run(tr, "feeds_all_lrba", 8000, 0, 0, (2500, 5500))
