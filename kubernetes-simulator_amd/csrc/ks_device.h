@@ -667,6 +667,12 @@ struct TickScratch {    // device, zero between launches (the last workgroup res
 struct TickOut {        // host-mapped
     int32_t node, status, code, pad_;
 };
+constexpr int kTickInl = 1024;   // inline staged bytes per per-tick launch
+constexpr int kTickInlSeg = 32;  // inline staged segments per per-tick launch
+struct TickSeg {
+    uint8_t* dst;
+    int32_t off, bytes;
+};
 struct TickArgs {
     Cfg c;
     NodeSoA s;
@@ -680,8 +686,11 @@ struct TickArgs {
     uint8_t* expired;
     TickScratch* scr;
     TickOut* out;
-    const CopySeg* segs;  // host-staged submits applied by the last workgroup first
-    int32_t n_seg, pad_;
+    // this call's host-staged submits, inline in the kernel arguments (no device read of pinned
+    // host memory): segment k copies bytes [off, off + bytes) of inl to dst
+    int32_t n_iseg, pad_;
+    TickSeg iseg[kTickInlSeg];
+    alignas(16) uint8_t inl[kTickInl];
 };
 hipError_t launch_tick(const TickArgs& a, int mode, hipStream_t st);
 struct ExpList {

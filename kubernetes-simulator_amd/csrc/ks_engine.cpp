@@ -1037,18 +1037,49 @@ static bool tick_step(ks_engine* e, int64_t t_end, ks_bind* out, int64_t cap, in
     a.scr = e->d_tick;
     a.out = e->h_tick_dev;
     if (stage_xpos(e) != hipSuccess) { *rc = fail(e, KS_EDEVICE, "per-tick path: staging failed"); return true; }
-    a.segs = e->segs_dev + e->seg_done;
-    a.n_seg = e->nseg - e->seg_done;
-    e->seg_done = e->nseg;
-    e->h_tick->code = -1;
+    // the pending staged rows inline in the arguments when they fit (one pod's submit does), else
+    // one scatter launch ahead of the kernel
+    {
+        int32_t off = 0;
+        bool fits = e->nseg - e->seg_done <= ks::kTickInlSeg;
+        for (int k = e->seg_done; fits && k < e->nseg; k++) {
+            off += (int32_t)((e->segs[k].bytes + 15) / 16 * 16);
+            fits = off <= ks::kTickInl;
+        }
+        if (fits) {
+            off = 0;
+            for (int k = e->seg_done; k < e->nseg; k++) {
+                const ks::CopySeg& sg = e->segs[k];
+                std::memcpy(a.inl + off, e->stage + (sg.src - e->stage_dev), (size_t)sg.bytes);
+                a.iseg[a.n_iseg++] = ks::TickSeg{sg.dst, off, (int32_t)sg.bytes};
+                off += (int32_t)((sg.bytes + 15) / 16 * 16);
+            }
+            e->seg_done = e->nseg;
+        } else if (stage_flush(e) != hipSuccess) {
+            *rc = fail(e, KS_EDEVICE, "per-tick path: staging failed");
+            return true;
+        }
+    }
+    __atomic_store_n(&e->h_tick->code, -1, __ATOMIC_RELAXED);
     hipError_t r = ks::launch_tick(a, e->mode, e->st);
     if (r == hipSuccess) r = hipEventRecord(e->stage_ev, e->st);
-    if (r == hipSuccess) r = hipStreamSynchronize(e->st);
+    // the result: poll the host-mapped code the last workgroup stores (release) after node and
+    // status — microseconds sooner than a stream synchronisation; the stream is queried now and
+    // then so that a failed launch still ends the wait
+    for (uint32_t spin = 1; r == hipSuccess; spin++) {
+        if (__atomic_load_n(&e->h_tick->code, __ATOMIC_ACQUIRE) >= 0) break;
+        if ((spin & 1023) == 0) {
+            const hipError_t q = hipStreamQuery(e->st);
+            if (q == hipSuccess) break;  // done: the code is read below
+            if (q != hipErrorNotReady) r = q;
+        }
+        __builtin_ia32_pause();
+    }
     if (r != hipSuccess) { *rc = fail(e, KS_EDEVICE, "per-tick launch: %s", hipGetErrorString(r)); return true; }
     ks::TickOut o;
+    o.code = __atomic_load_n(&e->h_tick->code, __ATOMIC_ACQUIRE);
     o.node = ((volatile ks::TickOut*)e->h_tick)->node;
     o.status = ((volatile ks::TickOut*)e->h_tick)->status;
-    o.code = ((volatile ks::TickOut*)e->h_tick)->code;
     for (int k = 0; k < a.n_exp; k++) e->h_expired[a.exp[k].q] = 1;
     e->stats = ks_step_stats{};
     e->stats.launches = 1;

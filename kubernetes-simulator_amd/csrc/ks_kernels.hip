@@ -42,10 +42,6 @@ constexpr int kMaxPG = KS_MAX_PG;        // pods per scan workgroup (LDS key tab
 #define KS_SCAN_UNROLL 4
 #endif
 constexpr int kScanUnroll = KS_SCAN_UNROLL;  // pods evaluated together per scan loop step
-#ifndef KS_SCAN_TARGET_WG
-#define KS_SCAN_TARGET_WG 2048
-#endif
-constexpr int64_t kScanTargetWg = KS_SCAN_TARGET_WG;  // scan workgroups a launch aims for
 constexpr int kResolveThreads = 1024;    // 16 waves
 constexpr int kOwnerWave0 = 3;           // waves 3..15 own the touched entries, except
 #ifndef KS_WRITER_WAVE
@@ -125,30 +121,54 @@ __global__ __launch_bounds__(256) void expire_head_kernel(const EngineArgs* __re
 // KT: the key table's word, uint16_t when every total + 1 < 2^16 (the host's check on the scorer
 // weights) — half the LDS per workgroup, so more workgroups fit a CU.
 template <int kMode, typename KT>
-__global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict__ A) {
+__global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict__ A, int xcd) {
     extern __shared__ uint32_t kv_raw[];
     KT* const kv = reinterpret_cast<KT*>(kv_raw);  // [PG][kBlockNodes]: total+1 per (pod, node of the block)
     const EngineArgs a = A[blockIdx.z];
-    if ((int)blockIdx.x >= a.blk_n) return;  // a group's scenarios may differ in size
     const int64_t start = sload(a.ctr + kCtrStart), end = sload(a.ctr + kCtrEnd);
     if (sload(a.ctr + kCtrErr) != 0) return;
     const int64_t nb = min<int64_t>(a.B, end - start);
-    if ((int64_t)blockIdx.y * a.PG >= nb) return;
+    if (nb <= 0) return;
+    const int groups = (int)((nb + a.PG - 1) / a.PG);
+    // work items (block, pod group), item = block * groups + group, one per workgroup: grid
+    // (blk_n, groups, S), or — one engine (xcd) — a 1-D grid dealt XCD-aware: blocks b and b + 8
+    // share an XCD (round-robin dispatch, MI355X_MICROARCH.md), so workgroup w takes item
+    // (w % 8) * per + w / 8 — each XCD a contiguous item range, the groups of a node block on one
+    // XCD back to back: the block's node records come from HBM once and from that XCD's L2 for
+    // the other groups (the placement is for speed only; any placement gives the same lists)
+    int64_t it_lo;
+    if (xcd) {
+        const int64_t tot = (int64_t)a.blk_n * groups, per = (tot + 7) / 8;
+        const int64_t k = blockIdx.x / 8;
+        if (k >= per) return;
+        it_lo = (int64_t)(blockIdx.x % 8) * per + k;
+        if (it_lo >= tot) return;
+    } else {
+        if ((int)blockIdx.x >= a.blk_n || (int)blockIdx.y >= groups) return;  // scenarios may differ in size
+        it_lo = (int64_t)blockIdx.x * groups + blockIdx.y;
+    }
+    const int64_t it_hi = it_lo + 1;
     const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
 #ifdef KS_SCAN_STAMPS  // diagnostic: evaluation / extraction cycles of wave 0, ctr[20] / ctr[21]
     uint64_t st0;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st0)::"memory");
 #endif
-    const int blk = a.blk_lo + blockIdx.x;
-    const uint32_t blk_base = (uint32_t)blk * kBlockNodes;
-    const int64_t node = (int64_t)blk_base + threadIdx.x;
-    const bool valid = node < a.c.n_nodes;
+    int cur = -1, blk = 0;
+    uint32_t blk_base = 0;
+    bool valid = false;
     NodeV n{};
-    if (node < (int64_t)a.c.nwb * kWave) n = load_node(a.s, node);
-    // pod groups blockIdx.y, blockIdx.y + gridDim.y, ...: a large cluster's launch has enough
-    // blocks to fill the chip with gridDim.y = 1, and each node record is then read once per batch
-    for (int pg0 = blockIdx.y * a.PG; pg0 < nb; pg0 += gridDim.y * a.PG) {
-    if (pg0 != (int)blockIdx.y * a.PG) __syncthreads();  // the previous group's extraction has read kv
+    for (int64_t it = it_lo; it < it_hi; ++it) {
+    const int bx = (int)(it / groups), pg0 = (int)(it - (int64_t)bx * groups) * a.PG;
+    if (it != it_lo) __syncthreads();  // the previous item's extraction has read kv
+    if (bx != cur) {
+        cur = bx;
+        blk = a.blk_lo + bx;
+        blk_base = (uint32_t)blk * kBlockNodes;
+        const int64_t node = (int64_t)blk_base + threadIdx.x;
+        valid = node < a.c.n_nodes;
+        n = NodeV{};
+        if (node < (int64_t)a.c.nwb * kWave) n = load_node(a.s, node);
+    }
     const int np = (int)min<int64_t>(a.PG, nb - pg0);
     const PodRec* pp = a.pods + start + pg0;
     int b = 0;
@@ -201,7 +221,7 @@ __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict_
         }
         if (lane >= cnt && lane < kL) out[lane] = 0ull;
     }
-    }  // pod groups
+    }  // work items
 #ifdef KS_SCAN_STAMPS
     uint64_t st2;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st2)::"memory");
@@ -1169,27 +1189,26 @@ hipError_t launch_expire_head(const EngineArgs* d, int S, hipStream_t st) {
 }
 
 template <typename KT>
-static void launch_scan_t(const EngineArgs* d, const dim3& g, size_t lds, int mode, hipStream_t st) {
+static void launch_scan_t(const EngineArgs* d, const dim3& g, size_t lds, int mode, int xcd, hipStream_t st) {
     switch (mode) {
-        case kEvalMicro: hipLaunchKernelGGL((scan_kernel<kEvalMicro, KT>), g, dim3(kBlockNodes), lds, st, d); break;
-        case kEvalTiny: hipLaunchKernelGGL((scan_kernel<kEvalTiny, KT>), g, dim3(kBlockNodes), lds, st, d); break;
-        case kEvalNarrow: hipLaunchKernelGGL((scan_kernel<kEvalNarrow, KT>), g, dim3(kBlockNodes), lds, st, d); break;
-        default: hipLaunchKernelGGL((scan_kernel<kEvalWide, KT>), g, dim3(kBlockNodes), lds, st, d); break;
+        case kEvalMicro: hipLaunchKernelGGL((scan_kernel<kEvalMicro, KT>), g, dim3(kBlockNodes), lds, st, d, xcd); break;
+        case kEvalTiny: hipLaunchKernelGGL((scan_kernel<kEvalTiny, KT>), g, dim3(kBlockNodes), lds, st, d, xcd); break;
+        case kEvalNarrow: hipLaunchKernelGGL((scan_kernel<kEvalNarrow, KT>), g, dim3(kBlockNodes), lds, st, d, xcd); break;
+        default: hipLaunchKernelGGL((scan_kernel<kEvalWide, KT>), g, dim3(kBlockNodes), lds, st, d, xcd); break;
     }
 }
 
 hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int mode, bool key16, hipStream_t st) {
     if (blk_n > 0 && S > 0) {
-        // pod-group slices per block: enough workgroups to fill the chip (~2048), the rest of the
-        // groups looped inside a workgroup over the node records it holds (C5's 4,096 blocks: one
-        // slice, each node read once per batch instead of once per group)
+        // one (block, pod group) item per workgroup; one engine: the XCD-aware 1-D deal
         const int groups = (B + PG - 1) / PG;
-        const int64_t want = (kScanTargetWg + (int64_t)blk_n * S - 1) / ((int64_t)blk_n * S);
-        const dim3 g(blk_n, (int)std::min<int64_t>(groups, std::max<int64_t>(want, 1)), S);
+        const size_t lds = (key16 ? sizeof(uint16_t) : sizeof(uint32_t)) * kBlockNodes * PG;
+        const bool xcd = S == 1;
+        const dim3 g = xcd ? dim3((unsigned)(((int64_t)blk_n * groups + 7) / 8 * 8), 1, 1) : dim3(blk_n, groups, S);
         if (key16)
-            launch_scan_t<uint16_t>(d, g, sizeof(uint16_t) * kBlockNodes * PG, mode, st);
+            launch_scan_t<uint16_t>(d, g, lds, mode, xcd ? 1 : 0, st);
         else
-            launch_scan_t<uint32_t>(d, g, sizeof(uint32_t) * kBlockNodes * PG, mode, st);
+            launch_scan_t<uint32_t>(d, g, lds, mode, xcd ? 1 : 0, st);
     }
     return hipGetLastError();
 }

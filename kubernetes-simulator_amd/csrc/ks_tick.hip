@@ -10,10 +10,11 @@
 //                 pod (fused Filter + Score, the expiries due before the pod applied on the fly from
 //                 a by-value list), reduces its block maximum of the packed key and folds it into one
 //                 u64 with a device-scope atomicMax.  The last workgroup to arrive (atomic counter)
-//                 applies the host-staged submits (copy segments from pinned host memory), applies the
-//                 expiries to the node state, binds the pod on the winner (CreatePod admission,
-//                 kubesim/node/node.go:36-60; NotFound and bad-pod stops as kubesim.go:217-220), and
-//                 writes the result to host-mapped memory.  One launch, one host synchronisation.
+//                 applies the expiries to the node state, binds the pod on the winner (CreatePod
+//                 admission, kubesim/node/node.go:36-60; NotFound and bad-pod stops as
+//                 kubesim.go:217-220), and writes the result to host-mapped memory, which the host
+//                 polls (no stream synchronisation).  One extra workgroup applies the call's staged
+//                 submits, passed inline in the kernel arguments, beside the evaluation.
 //   scatter_kernel  the host-staged submits alone (before any other device work reads them).
 #include "ks_device.h"
 
@@ -41,9 +42,27 @@ __global__ __launch_bounds__(kTickThreads) void scatter_kernel(const CopySeg* se
 template <int kMode>
 __global__ __launch_bounds__(kTickThreads) void tick_kernel(const TickArgs A) {
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid >> 6;
+    // the extra (last) workgroup applies this call's staged submits (inline in the arguments)
+    // beside the evaluation; it arrives like the others, so the bind — which writes the pod's own
+    // submitted rows (b_node, b_status) — follows the copy
+    const bool copier = (int)blockIdx.x == (int)gridDim.x - 1;
     const int64_t i = (int64_t)blockIdx.x * kTickThreads + tid;
     uint64_t key = 0;
-    if (i < A.c.n_nodes) {
+    if (copier) {
+        const uint8_t* base = A.inl;
+        for (int k = 0; k < A.n_iseg; ++k) {
+            const TickSeg sg = A.iseg[k];
+            const uint8_t* src = base + sg.off;
+            if ((((uintptr_t)sg.dst | (uint32_t)sg.bytes) & 3) == 0) {
+                const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
+                uint32_t* d4 = reinterpret_cast<uint32_t*>(sg.dst);
+                for (int w = tid; w < sg.bytes / 4; w += kTickThreads) d4[w] = s4[w];
+            } else {
+                for (int w = tid; w < sg.bytes; w += kTickThreads) sg.dst[w] = src[w];
+            }
+        }
+        __threadfence();
+    } else if (i < A.c.n_nodes) {
         NodeV v = load_node(A.s, i);
         for (int e = 0; e < A.n_exp; ++e)
             if (A.exp[e].node == i) { v.rc -= A.exp[e].req[0]; v.rm -= A.exp[e].req[1]; v.rg -= A.exp[e].req[2]; v.nr -= 1; }
@@ -66,7 +85,6 @@ __global__ __launch_bounds__(kTickThreads) void tick_kernel(const TickArgs A) {
     if (!last) return;
     // ---- the last workgroup: every other one has folded its maximum
     __threadfence();
-    copy_segs(A.segs, A.n_seg, tid, kTickThreads);  // this call's submits (the pod's own rows first)
     if (tid < A.n_exp) {
         const TickExp& x = A.exp[tid];
         atomicAdd((unsigned long long*)&A.s.rc[x.node], (unsigned long long)(-x.req[0]));
@@ -99,10 +117,11 @@ __global__ __launch_bounds__(kTickThreads) void tick_kernel(const TickArgs A) {
         }
         A.scr->best = 0;
         A.scr->count = 0;
+        // the result to host-mapped memory: node and status, then (release, system scope) the code
+        // the host polls on
         A.out->node = node;
         A.out->status = status;
-        A.out->code = code;
-        __threadfence_system();
+        __hip_atomic_store(&A.out->code, code, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -123,7 +142,7 @@ hipError_t launch_apply_exp(const NodeSoA& s, uint8_t* expired, const ExpList& l
 }
 
 hipError_t launch_tick(const TickArgs& a, int mode, hipStream_t st) {
-    const int grid = (int)((a.c.n_nodes + kTickThreads - 1) / kTickThreads);
+    const int grid = (int)((a.c.n_nodes + kTickThreads - 1) / kTickThreads) + 1;  // + the copy workgroup
     switch (mode) {
         case kEvalMicro: hipLaunchKernelGGL(tick_kernel<kEvalMicro>, dim3(grid), dim3(kTickThreads), 0, st, a); break;
         case kEvalTiny: hipLaunchKernelGGL(tick_kernel<kEvalTiny>, dim3(grid), dim3(kTickThreads), 0, st, a); break;
