@@ -6,7 +6,7 @@
 // resolver; two host round trips) is built for thousands of pods per call; for one pod it is pure
 // latency.  This file is the one-pod path:
 //
-//   tick_kernel   grid = the cluster's 256-node blocks.  Every workgroup evaluates its nodes for the
+//   tick_kernel   grid = the cluster's 1024-node blocks.  Every workgroup evaluates its nodes for the
 //                 pod (fused Filter + Score, the expiries due before the pod applied on the fly from
 //                 a by-value list), reduces its block maximum of the packed key and folds it into one
 //                 u64 with a device-scope atomicMax.  The last workgroup to arrive (atomic counter)
@@ -21,6 +21,7 @@
 namespace ks {
 
 constexpr int kTickThreads = 256;
+constexpr int kTickNodes = 4;  // nodes per thread
 
 __device__ __forceinline__ void copy_segs(const CopySeg* segs, int n, int tid, int nthr) {
     for (int k = 0; k < n; ++k) {
@@ -46,7 +47,6 @@ __global__ __launch_bounds__(kTickThreads) void tick_kernel(const TickArgs A) {
     // beside the evaluation; it arrives like the others, so the bind — which writes the pod's own
     // submitted rows (b_node, b_status) — follows the copy
     const bool copier = (int)blockIdx.x == (int)gridDim.x - 1;
-    const int64_t i = (int64_t)blockIdx.x * kTickThreads + tid;
     uint64_t key = 0;
     if (copier) {
         const uint8_t* base = A.inl;
@@ -62,11 +62,27 @@ __global__ __launch_bounds__(kTickThreads) void tick_kernel(const TickArgs A) {
             }
         }
         __threadfence();
-    } else if (i < A.c.n_nodes) {
-        NodeV v = load_node(A.s, i);
-        for (int e = 0; e < A.n_exp; ++e)
-            if (A.exp[e].node == i) { v.rc -= A.exp[e].req[0]; v.rm -= A.exp[e].req[1]; v.rg -= A.exp[e].req[2]; v.nr -= 1; }
-        key = make_key(eval_t<kMode>(A.c, A.pod, v), (uint32_t)i);
+    } else {
+        // kTickNodes nodes per thread, their loads issued together (fewer workgroups: fewer
+        // arrivals on the two grid-wide atomics)
+        NodeV v[kTickNodes];
+#pragma unroll
+        for (int q = 0; q < kTickNodes; ++q) {
+            const int64_t i = ((int64_t)blockIdx.x * kTickNodes + q) * kTickThreads + tid;
+            v[q] = NodeV{};
+            if (i < A.c.n_nodes) v[q] = load_node(A.s, i);
+        }
+#pragma unroll
+        for (int q = 0; q < kTickNodes; ++q) {
+            const int64_t i = ((int64_t)blockIdx.x * kTickNodes + q) * kTickThreads + tid;
+            if (i >= A.c.n_nodes) continue;
+            for (int e = 0; e < A.n_exp; ++e)
+                if (A.exp[e].node == i) {
+                    v[q].rc -= A.exp[e].req[0]; v[q].rm -= A.exp[e].req[1]; v[q].rg -= A.exp[e].req[2]; v[q].nr -= 1;
+                }
+            const uint64_t k = make_key(eval_t<kMode>(A.c, A.pod, v[q]), (uint32_t)i);
+            key = k > key ? k : key;
+        }
     }
     __shared__ uint64_t wmax[kTickThreads / kWave];
     __shared__ int last;
@@ -142,7 +158,8 @@ hipError_t launch_apply_exp(const NodeSoA& s, uint8_t* expired, const ExpList& l
 }
 
 hipError_t launch_tick(const TickArgs& a, int mode, hipStream_t st) {
-    const int grid = (int)((a.c.n_nodes + kTickThreads - 1) / kTickThreads) + 1;  // + the copy workgroup
+    const int64_t per = (int64_t)kTickThreads * kTickNodes;
+    const int grid = (int)((a.c.n_nodes + per - 1) / per) + 1;  // + the copy workgroup
     switch (mode) {
         case kEvalMicro: hipLaunchKernelGGL(tick_kernel<kEvalMicro>, dim3(grid), dim3(kTickThreads), 0, st, a); break;
         case kEvalTiny: hipLaunchKernelGGL(tick_kernel<kEvalTiny>, dim3(grid), dim3(kTickThreads), 0, st, a); break;
