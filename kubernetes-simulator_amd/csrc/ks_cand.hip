@@ -47,22 +47,46 @@ __device__ __forceinline__ const __attribute__((address_space(1))) T* cg(const T
 // Window: the expiries attached to pods start+1 .. start+nb-1 (exp_off CSR), one slot each; the
 // batch shrinks to the largest prefix whose window fits kWinSlots.  E = the distinct nodes of the
 // slots whose pod was bound Ok before the batch and has not expired; e_idx marks them.
+// Overlap (`spec`): the batch's block lists come from the speculative scan that ran beside the
+// previous batch's resolve, on the node table as it was then.  They are exact for every node the
+// previous batch did not change; the changed ones (its binds and window expiry nodes, written by
+// its commit as `touched`, and the head expiries applied here) join E with no slots, so the
+// candidate lists evaluate them exactly (an E node enters a list when its exact key reaches the
+// list's threshold — the same rule as for the expiry nodes).  The speculative scan covered the
+// pods after the previous batch; if that batch stopped early (this batch starts elsewhere) or the
+// touched nodes overflow E, `rescan` asks the conditional scan on the engine's stream to redo the
+// lists on the current table.  The speculative counters for the next scan are written last.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kPrepThreads) void window_prep_kernel(const EngineArgs* __restrict__ A, int head) {
+__global__ __launch_bounds__(kPrepThreads) void window_prep_kernel(const EngineArgs* __restrict__ A, int head, int spec) {
     const EngineArgs& a = A[0];
     WinWS& ws = *a.sw;
     const int tid = threadIdx.x;
     __shared__ int32_t hk[kEHash], hv[kEHash];
-    __shared__ int32_t cnt[kWinSlots], fill[kWinSlots];
-    __shared__ int32_t s_ne;
+    __shared__ int32_t cnt[kEMax], fill[kEMax];
+    __shared__ int32_t xn[kEMax];  // touched nodes to insert (overlap)
+    __shared__ int32_t s_ne, s_nx;
     const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
     int nb = (int)min<int64_t>(min<int64_t>(a.B, kWinMaxB), end - start);
     if (a.ctr[kCtrErr] != 0 || nb <= 0) {
-        if (tid == 0) { ws.nb = 0; ws.e_cnt = 0; ws.n_e = 0; }
+        if (tid == 0) {
+            ws.nb = 0; ws.e_cnt = 0; ws.n_e = 0; ws.rescan = 0;
+            a.spec_ctr[kCtrStart] = end; a.spec_ctr[kCtrEnd] = end; a.spec_ctr[kCtrErr] = 0;
+        }
         return;
     }
+    const int64_t e0 = a.exp_off[start], e1 = a.exp_off[start + 1];
+    const int64_t e_base = e1;
+    const bool fits_win = tid < nb && a.exp_off[start + tid + 1] - e_base <= kWinSlots;
+    for (int h = tid; h < kEHash; h += kPrepThreads) hk[h] = -1;
+    if (tid == 0) { s_ne = 0; s_nx = 0; }
+    nb = __syncthreads_count(fits_win);  // exp_off is non-decreasing: a prefix of the pods
+    const int e_cnt = (int)(a.exp_off[start + nb] - e_base);
+    // overlap: the lists are usable when the speculative scan covered this batch's pods and the
+    // changed nodes fit E
+    int rescan = 0;
+    if (spec) rescan = start != a.spec_ctr[kCtrStart] || (int64_t)e_cnt + (e1 - e0) + ws.n_touched > kEMax;
+    const bool touch = spec && !rescan;
     if (head) {  // expire_head's work: the expiries due before the batch's first pod
-        const int64_t e0 = a.exp_off[start], e1 = a.exp_off[start + 1];
         for (int64_t e = e0 + tid; e < e1; e += kPrepThreads) {
             const int32_t q = a.exp_pod[e];
             if (a.b_status[q] != 0 || a.expired[q]) continue;
@@ -73,14 +97,11 @@ __global__ __launch_bounds__(kPrepThreads) void window_prep_kernel(const EngineA
             atomicAdd((unsigned long long*)&a.s.rg[nd], (unsigned long long)(-p.req[2]));
             atomicAdd((unsigned long long*)&a.s.nr[nd], (unsigned long long)(-1ll));
             a.expired[q] = 1;
+            if (touch) xn[atomicAdd(&s_nx, 1)] = nd;
         }
     }
-    const int64_t e_base = a.exp_off[start + 1];
-    const bool fits_win = tid < nb && a.exp_off[start + tid + 1] - e_base <= kWinSlots;
-    for (int h = tid; h < kEHash; h += kPrepThreads) hk[h] = -1;
-    if (tid == 0) s_ne = 0;
-    nb = __syncthreads_count(fits_win);  // exp_off is non-decreasing: a prefix of the pods
-    const int e_cnt = (int)(a.exp_off[start + nb] - e_base);
+    if (touch)
+        for (int t = tid; t < ws.n_touched; t += kPrepThreads) xn[atomicAdd(&s_nx, 1)] = ws.touched[t];
     if (tid < nb) {
         ws.win_hi[tid] = tid >= 1 ? (int32_t)(a.exp_off[start + tid + 1] - e_base) : 0;
         const int64_t pos = a.exp_pos[start + tid];
@@ -96,10 +117,10 @@ __global__ __launch_bounds__(kPrepThreads) void window_prep_kernel(const EngineA
         ws.ex_ok[tid] = ok ? 1 : 0;
         if (ok) my_node = a.b_node[q];
     }
-    bool claimed = false;
     if (my_node >= 0) {
         uint32_t h = ehslot(my_node);
-        for (;;) {  // <= kWinSlots distinct nodes < kEHash slots: terminates
+        bool claimed = false;
+        for (;;) {  // <= kEMax distinct nodes < kEHash slots: terminates
             const int32_t prev = atomicCAS(&hk[h], -1, my_node);
             if (prev == -1) { claimed = true; break; }
             if (prev == my_node) break;
@@ -107,6 +128,19 @@ __global__ __launch_bounds__(kPrepThreads) void window_prep_kernel(const EngineA
         }
         my_k = (int32_t)h;  // hash slot; the claiming thread numbers the node
         if (claimed) hv[h] = atomicAdd(&s_ne, 1);
+    }
+    __syncthreads();
+    // the touched nodes after the slot nodes (no slots: E indices n_e_slots ..)
+    const int n_x = s_nx;
+    for (int t = tid; t < n_x; t += kPrepThreads) {
+        const int32_t nd = xn[t];
+        uint32_t h = ehslot(nd);
+        for (;;) {
+            const int32_t prev = atomicCAS(&hk[h], -1, nd);
+            if (prev == -1) { const int k = atomicAdd(&s_ne, 1); hv[h] = k; ws.e_node[k] = nd; break; }
+            if (prev == nd) break;
+            h = (h + 1) & (kEHash - 1);
+        }
     }
     __syncthreads();
     const int n_e = s_ne;
@@ -120,6 +154,7 @@ __global__ __launch_bounds__(kPrepThreads) void window_prep_kernel(const EngineA
     }
     __syncthreads();
     {  // exclusive prefix of the counts (n_e <= kPrepThreads: one per thread)
+        static_assert(kEMax <= kPrepThreads, "one E node per prep thread");
         __shared__ int32_t wsum[kPrepThreads / 64];
         const int lane = tid & 63, wv = tid >> 6;
         const int v = tid < n_e ? cnt[tid] : 0;
@@ -150,7 +185,11 @@ __global__ __launch_bounds__(kPrepThreads) void window_prep_kernel(const EngineA
         }
         a.e_idx[ws.e_node[tid]] = tid;
     }
-    if (tid == 0) { ws.nb = nb; ws.e_cnt = e_cnt; ws.n_e = n_e; ws.nslot = 0; }
+    if (tid == 0) {
+        ws.nb = nb; ws.e_cnt = e_cnt; ws.n_e = n_e; ws.nslot = 0; ws.rescan = rescan;
+        // the next speculative scan: the pods after this batch, if it commits them all
+        a.spec_ctr[kCtrStart] = start + nb; a.spec_ctr[kCtrEnd] = end; a.spec_ctr[kCtrErr] = 0;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -332,8 +371,8 @@ __global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs* __rest
 
 }  // namespace sq
 
-hipError_t launch_window_prep(const EngineArgs* d, bool head, hipStream_t st) {
-    hipLaunchKernelGGL(sq::window_prep_kernel, dim3(1), dim3(sq::kPrepThreads), 0, st, d, head ? 1 : 0);
+hipError_t launch_window_prep(const EngineArgs* d, bool head, bool spec, hipStream_t st) {
+    hipLaunchKernelGGL(sq::window_prep_kernel, dim3(1), dim3(sq::kPrepThreads), 0, st, d, head ? 1 : 0, spec ? 1 : 0);
     return hipGetLastError();
 }
 

@@ -126,9 +126,11 @@ struct ChShared {
     int8_t adm[kB];               // admission of pod j's bind: 1 ok, 0 over capacity, 2 unknown
     uint8_t clcnt[kB], clfl[kB];
     int16_t win_hi[kB], own[kB];
-    int32_t xreq[3][kSlots];
     int16_t xeff[kSlots];         // slot x is applied from pod xeff[x] on
-    int16_t eoff[kSlots + 1], eslot[kSlots];
+    int16_t eoff[kEMax + 1];
+    // E-slot u (E node k's slots are [eoff[k], eoff[k+1]), ascending): {xeff of its slot, the
+    // expiring pod's requests as words} — a replay's expiry event in one 16-byte read
+    int4 erow[kSlots];
     // replayed node (slot = its first binder pod, one 16-byte row): [0, kSeg) segment start pods,
     // [kMOvf] the first pod whose state the slot does not hold, [kMCid] the node's cid (-1: the pod
     // is not a first binder)
@@ -142,8 +144,9 @@ struct ChShared {
         int16_t c[kWaves][kC][2];  // k[.][.][1] == ~0: the lane met an unknown state
     } x;
     int16_t ceix[kCid];           // cid -> the node's index in E, -1 if not an E node
-    int16_t e2c[kSlots];          // E index -> cid, -1: the E node is no candidate of this batch
+    int16_t e2c[kEMax];           // E index -> cid, -1: the E node is no candidate of this batch
     int32_t nbc, cut, fc[2], fs[2];
+    uint64_t chg;                 // chunk rows (slots c0 + j) rewritten since the last full sweep
 #ifdef KS_CHUNK_DIAG
     int8_t why[kB];  // stop reason of a code-1 decision
 #endif
@@ -225,15 +228,16 @@ __device__ __forceinline__ Replayed replay(ChShared& sh, int k, int tb, bool chu
     for (;;) {
         int jb = j >= 0 ? j : (m ? c0 + __builtin_ctzll(m) : INT_MAX);
         if (jb >= i_end) jb = INT_MAX;
-        const int ne = e_u < e_end ? sh.xeff[sh.eslot[e_u]] : INT_MAX;
+        const int4 er = e_u < e_end ? sh.erow[e_u] : make_int4(INT_MAX, 0, 0, 0);
+        const int ne = er.x;
         const int pm01 = pe0 < pe1 ? pe0 : pe1, pm23 = pe2 < pe3 ? pe2 : pe3;
         const int pm = pm01 < pm23 ? pm01 : pm23;
         const int nx = ne < pm ? ne : pm;
         const int lim = jb != INT_MAX ? jb : i_end - 1;
         if (nx <= lim) {  // an expiry effective before the next bind (or before i_end)
             if (ne == nx) {
-                const int x = sh.eslot[e_u++];
-                vrc -= (uint32_t)sh.xreq[0][x]; vrm -= (uint32_t)sh.xreq[1][x]; vrg -= (uint32_t)sh.xreq[2][x]; vnr -= 1;
+                ++e_u;
+                vrc -= (uint32_t)er.y; vrm -= (uint32_t)er.z; vrg -= (uint32_t)er.w; vnr -= 1;
             } else {
                 const bool h0 = pe0 == pm, h1 = !h0 && pe1 == pm, h2 = !h0 && !h1 && pe2 == pm,
                            h3 = !h0 && !h1 && !h2;
@@ -312,6 +316,21 @@ __device__ __forceinline__ uint64_t key_at(const EngineArgs& a, const ChShared& 
     return make_key(eval32<kMode>(a.c, p, n), (uint32_t)sh.cnode[k]);
 }
 
+// Pod i's total + 1 (0: infeasible) on slot sl's node from its row
+template <int kMode>
+__device__ __forceinline__ uint32_t tot_at(const EngineArgs& a, const ChShared& sh, const PodRec& p, int i, int k,
+                                           int sl, const SRow& r) {
+    int s = 0;
+#pragma unroll
+    for (int q = 1; q < kSeg; ++q) s += r.m(q) <= i;
+    const int4 st = *reinterpret_cast<const int4*>(&sh.sst[sl][s][0]);
+    NS32 n;
+    n.ac = sh.rs[0][k]; n.am = sh.rs[1][k]; n.ag = sh.rs[2][k]; n.ap = sh.rs[3][k];
+    n.rc = st.x; n.rm = st.y; n.rg = st.z; n.nr = st.w;
+    n.taint = sh.rt[k]; n.label = sh.rl[k];
+    return eval32<kMode>(a.c, p, n);
+}
+
 // The same, 0 when the float upper bound of the total (prune_tmax: filters ignored, exact slack)
 // says the key stays below lb — most (pod, node) pairs: the full evaluator runs only for the rest.
 template <int kMode>
@@ -371,14 +390,65 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
     // kCidSlots + r (its record read here), so every launch binds at least one pod.
     DG(uint64_t t_setup = dstamp(); uint64_t acc_cd = 0, acc_sw = 0, acc_fin = 0, acc_ph[4] = {0, 0, 0, 0}, acc_cs = 0, acc_rb = 0, acc_cdp = 0; int n_sweeps = 0, n_sonly = 0, n_chunks = 0;)
     const int nslot = ws.nslot < kWinMaxB * kR ? ws.nslot : kWinMaxB * kR;
+    const int nlo = nslot < kCidSlots ? nslot : kCidSlots;
+    // (1) every global read of the setup issued before any is used: one round trip (the lists and
+    // records were written by other workgroups, on other XCDs — each dependent read is a fabric
+    // round trip)
+    static_assert(sizeof(PodRec) == 48, "a pod record is three 16-byte words");
+    uint4 prec[3] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+    int32_t whi = 0, ownv = -1, info = 0, durv = 0;
+    if (tid < nb) {
+        const uint4* pr = reinterpret_cast<const uint4*>(a.pods + start + tid);
+        prec[0] = pr[0]; prec[1] = pr[1]; prec[2] = pr[2];
+        whi = ws.win_hi[tid]; ownv = ws.own[tid]; info = ws.cl_info[tid]; durv = a.dur[start + tid];
+    }
+    int64_t xr0 = 0, xr1 = 0, xr2 = 0;
+    int32_t esl = 0, xq = -1;
+    if (tid < e_cnt) {
+        xr0 = ws.ex_req[tid][0]; xr1 = ws.ex_req[tid][1]; xr2 = ws.ex_req[tid][2]; esl = ws.e_slot[tid];
+        xq = ws.ex_ok[tid] ? ws.ex_q[tid] : -1;  // (for the commit)
+    }
+    static_assert(kEMax <= 2 * kThreads, "two E nodes per thread");
+    int32_t enode[2];  // (for the commit)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) enode[q] = tid + q * kThreads < n_e ? ws.e_node[tid + q * kThreads] : -1;
+    static_assert(kSlots <= kThreads, "one window slot per thread");
+    static_assert(kEMax + 1 <= 3 * kThreads, "three E offsets per thread");
+    int32_t eo[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) eo[q] = tid + q * kThreads <= n_e ? ws.e_off[tid + q * kThreads] : 0;
+    static_assert(kCidSlots <= 2 * kThreads, "two slot records per thread");
+    int32_t snd[2], sex[2];
+    uint4 srec[2][3];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int k = tid + q * kThreads;
+        const bool v = k < nlo;
+        snd[q] = v ? ws.slot_node[k] : -1;
+        sex[q] = v ? ws.slot_eix[k] : -1;
+        const uint4* r = reinterpret_cast<const uint4*>(ws.slot_rec[v ? k : 0]);
+#pragma unroll
+        for (int w = 0; w < 3; ++w) srec[q][w] = v ? r[w] : make_uint4(0, 0, 0, 0);
+    }
+    constexpr int kEntPer = (kB * kR + kThreads - 1) / kThreads;
+    uint64_t ekey[kEntPer];
+    int32_t eslt[kEntPer];
+#pragma unroll
+    for (int q = 0; q < kEntPer; ++q) {  // every kept position (the counts come with the lists)
+        const int idx = tid + q * kThreads, i = idx / kR, r = idx % kR;
+        const bool v = i < nb;
+        ekey[q] = v ? ws.cl_key[i][r] : 0ull;
+        eslt[q] = v ? ws.cl_slot[i][r] : -1;
+    }
+    // (2) the LDS images
     if (tid == 0) { sh.nbc = nb; sh.cut = INT_MAX; sh.fc[0] = sh.fc[1] = INT_MAX; sh.fs[0] = sh.fs[1] = INT_MAX; }
     if (tid < nb) {
-        sh.pod[tid] = a.pods[start + tid];
-        sh.win_hi[tid] = (int16_t)ws.win_hi[tid];
-        sh.own[tid] = (int16_t)ws.own[tid];
-        const int info = ws.cl_info[tid];
+        uint4* pd = reinterpret_cast<uint4*>(&sh.pod[tid]);
+        pd[0] = prec[0]; pd[1] = prec[1]; pd[2] = prec[2];
+        sh.win_hi[tid] = (int16_t)whi;
+        sh.own[tid] = (int16_t)ownv;
         sh.clcnt[tid] = (uint8_t)(info & 0xFF);
-        sh.clfl[tid] = (a.dur[start + tid] > 0 ? kFlRun : 0) | ((info & kClTrunc) ? kFlTrunc : 0) |
+        sh.clfl[tid] = (durv > 0 ? kFlRun : 0) | ((info & kClTrunc) ? kFlTrunc : 0) |
                        ((info & kClFull) ? kFlFull : 0) | ((info & kClOvf) ? kFlOvf : 0);
         sh.adm[tid] = 0;
         sh.wf[tid] = -1;
@@ -386,49 +456,40 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
         sh.smeta[tid][kMCid] = -1;
         sh.code[0][tid] = 0; sh.code[1][tid] = 0;
     }
-    for (int x = tid; x < e_cnt; x += kThreads) {
-        sh.xreq[0][x] = word32(ws.ex_req[x][0]);
-        sh.xreq[1][x] = word32(ws.ex_req[x][1]);
-        sh.xreq[2][x] = word32(ws.ex_req[x][2]);
-        sh.eslot[x] = (int16_t)ws.e_slot[x];
+    // slot x's request words, staged in the cache buffer (idle until the first chunk's cache)
+    int32_t (*xtmp)[4] = reinterpret_cast<int32_t (*)[4]>(&sh.x.k[0][0][0]);
+    static_assert(sizeof(sh.x.k) >= kSlots * 4 * sizeof(int32_t), "slot request staging");
+    if (tid < e_cnt) {
+        xtmp[tid][0] = word32(xr0); xtmp[tid][1] = word32(xr1); xtmp[tid][2] = word32(xr2);
     }
-    for (int k = tid; k <= n_e; k += kThreads) {
-        sh.eoff[k] = (int16_t)ws.e_off[k];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const int k = tid + q * kThreads;
+        if (k <= n_e) sh.eoff[k] = (int16_t)eo[q];
         if (k < n_e) sh.e2c[k] = -1;
     }
-    // slot records (16 bytes per thread and step); the other cids inert
     for (int k = tid; k < kCid; k += kThreads) { sh.ceix[k] = -1; sh.cnode[k] = -1; }
     __syncthreads();
     DG(uint64_t ts1 = dstamp();)
     // slot i is applied from the first pod i >= 1 with win_hi[i] > x
     for (int i = tid + 1; i < nb; i += kThreads)
         for (int x = sh.win_hi[i - 1]; x < sh.win_hi[i]; ++x) sh.xeff[x] = (int16_t)i;
-    const int nlo = nslot < kCidSlots ? nslot : kCidSlots;
-    for (int k = tid; k < nlo; k += kThreads) {
-        const int32_t nd = ws.slot_node[k];
-        const int ex = ws.slot_eix[k];
-        sh.cnode[k] = nd;
-        sh.ceix[k] = (int16_t)ex;
-        if (ex >= 0) sh.e2c[ex] = (int16_t)k;
-        store_prec(sh, k, reinterpret_cast<const uint4*>(ws.slot_rec[k]));
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {  // slot records; the other cids inert
+        const int k = tid + q * kThreads;
+        if (k < nlo) {
+            sh.cnode[k] = snd[q];
+            sh.ceix[k] = (int16_t)sex[q];
+            if (sex[q] >= 0) sh.e2c[sex[q]] = (int16_t)k;
+            store_prec(sh, k, srec[q]);
+        }
     }
     for (int k = tid; k < kCid; k += kThreads)
         if (k >= nlo) store_book(sh, k);
-    // every entry's key and slot loaded before any is used (one round of loads in flight)
-    constexpr int kEntPer = (kB * kR + kThreads - 1) / kThreads;
-    uint64_t ekey[kEntPer];
-    int32_t eslt[kEntPer];
 #pragma unroll
     for (int q = 0; q < kEntPer; ++q) {
         const int idx = tid + q * kThreads, i = idx / kR, r = idx % kR;
-        const bool v = i < nb && r < sh.clcnt[i];
-        ekey[q] = v ? ws.cl_key[i][r] : 0ull;
-        eslt[q] = v ? ws.cl_slot[i][r] : -1;
-    }
-#pragma unroll
-    for (int q = 0; q < kEntPer; ++q) {
-        const int idx = tid + q * kThreads, i = idx / kR, r = idx % kR;
-        if (eslt[q] < 0) continue;
+        if (i >= nb || r >= sh.clcnt[i] || eslt[q] < 0) continue;
         const uint64_t key = ekey[q];
         const int sl = eslt[q];
         int cid = sl;
@@ -451,6 +512,10 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
     __syncthreads();
     nb = sh.nbc < nb ? sh.nbc : nb;
     const int ncid = kCid;  // (inert cids have no events: skipped by every loop)
+    if (tid < e_cnt && tid < sh.eoff[n_e]) {  // E-slot tid is window slot esl
+        const int32_t* q = xtmp[esl];
+        sh.erow[tid] = make_int4(sh.xeff[esl], q[0], q[1], q[2]);
+    }
     DG(uint64_t ts2 = dstamp(); uint64_t sub_k = 0;)
     __syncthreads();
 
@@ -622,8 +687,15 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
         }
         __syncthreads();
         DG(uint64_t tx = dstamp(); acc_cs += tx - t1;)
-        // (2b) full sweeps from the guess
+        // (2b) full sweeps from the guess.  The first evaluates every (pod, chunk row) pair and
+        // keeps the totals (tt, in the idle cache buffer: 16-bit totals, 8 KB); later sweeps
+        // re-evaluate only the rows phase B rewrote (chg), one wave-uniform row per step, and read
+        // the rest
+        uint16_t (*tt)[kC] = reinterpret_cast<uint16_t (*)[kC]>(&sh.x.k[0][0][0]);
+        static_assert(sizeof(sh.x.k) >= kC * kC * sizeof(uint16_t), "per-pair totals");
         int par = 0, lo = c0, fsv = INT_MAX;
+        bool fresh = true;
+        if (tid == 0) sh.chg = 0ull;
         for (;;) {
             DG(++n_sweeps; uint64_t q0 = dstamp();)
             // A: the guesses' chunk binds (pod c0 + jr on thread 8 jr: spread over the waves)
@@ -649,13 +721,35 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                     if (!(KS_CHUNK_ABL & 2) && (sh.dirty[wcur] || sh.smeta[j][kMCid] != wcur)) {
                         sh.dirty[wcur] = 0;
                         (void)replay(sh, wcur, tb, true, c0, c0, j, c1);
+                        if (!fresh) atomicOr((unsigned long long*)&sh.chg, 1ull << jr);
                     }
                 } else {
+                    if (!fresh && sh.smeta[j][kMCid] >= 0) atomicOr((unsigned long long*)&sh.chg, 1ull << jr);
                     sh.smeta[j][kMCid] = -1;
                 }
             }
             __syncthreads();
             DG(uint64_t q2 = dstamp(); acc_ph[1] += q2 - q1;)
+            if (!fresh) {  // C1: the rewritten rows, wave-uniform (row = the wave's k-th changed row, lane = pod)
+                const uint64_t chg = sh.chg;
+                if (chg) {
+                    const int i = c0 + lane;
+                    const bool li = i < c1 && i >= lo;
+                    const PodRec p = sh.pod[li ? i : c0];
+                    int kx = 0;
+                    for (uint64_t m = chg; m; m &= m - 1, ++kx) {
+                        if ((kx & (kWaves - 1)) != wave) continue;
+                        const int jr = __builtin_ctzll(m);
+                        const SRow r = srow(sh, c0 + jr);
+                        const int k = r.m(kMCid);
+                        const bool v = li && jr < lane;
+                        uint32_t t = 0;
+                        if (v && k >= 0 && r.m(kMOvf) > i) t = tot_at<kMode>(a, sh, p, i, k, c0 + jr, r);
+                        if (v) tt[lane][jr] = (uint16_t)t;
+                    }
+                }
+                __syncthreads();
+            }
             // C: the pods c0 + g and c0 + 63 - g on the 16 lanes of group g — together 63 rows
             // (chunk binders before them), four per lane, so every wave evaluates the same
             {
@@ -722,8 +816,15 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                             continue;
                         }
                         if (KS_CHUNK_ABL & 1) continue;
-                        const uint64_t key = key_at<kMode>(a, sh, isA[q] ? pA : pB, i, k,
-                                                           c0 + (isA[q] ? rr : rr - g), r[q]);
+                        const int jr = isA[q] ? rr : rr - g;
+                        uint32_t t;
+                        if (fresh) {
+                            t = tot_at<kMode>(a, sh, isA[q] ? pA : pB, i, k, c0 + jr, r[q]);
+                            tt[i - c0][jr] = (uint16_t)t;
+                        } else {
+                            t = tt[i - c0][jr];
+                        }
+                        const uint64_t key = make_key(t, (uint32_t)sh.cnode[k]);
                         if (isA[q]) { if (key > dkA) { dkA = key; dcA = k; } }
                         else if (key > dkB) { dkB = key; dcB = k; }
                     }
@@ -806,9 +907,10 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
             // No barrier here: the next round's accumulators (par ^ 1) are only written after its
             // phase-A barrier, which tid 0 reaches after this reset; this round's (par) are reset
             // two rounds on, after every thread has passed the next phase-A barrier.
-            if (tid == 0) { sh.fc[par ^ 1] = INT_MAX; sh.fs[par ^ 1] = INT_MAX; }
+            if (tid == 0) { sh.fc[par ^ 1] = INT_MAX; sh.fs[par ^ 1] = INT_MAX; sh.chg = 0ull; }
             DG(acc_ph[3] += dstamp() - q3;)
             par ^= 1;
+            fresh = false;
             if (fcv == INT_MAX || fcv >= fsv) break;
             lo = fcv + 1;
         }
@@ -879,8 +981,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
         const int x = sh.own[tid];
         if (ok && (sh.clfl[tid] & kFlRun) && x >= 0 && x < h_end) gptr(a.expired)[j] = 1;
     }
-    for (int x = tid; x < h_end; x += kThreads)
-        if (ws.ex_ok[x]) gptr(a.expired)[ws.ex_q[x]] = 1;
+    if (tid < h_end && xq >= 0) gptr(a.expired)[xq] = 1;  // (h_end <= e_cnt <= kSlots <= kThreads)
     for (int k = tid; k < ncid; k += kThreads) {
         if (sh.ceix[k] >= 0 || sh.fhead[k] >= 0) {
             const NS32 v = replay(sh, k, tb, false, 0, 0, -1, c).v;
@@ -889,20 +990,48 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
         }
     }
     // E nodes that are no candidate of this batch: their expiries before pod c - 1's bind here
-    for (int k = tid; k < n_e; k += kThreads) {
-        const int32_t n = ws.e_node[k];
+    // (requests from the LDS words: exact, an admitted request is below its capacity < 2^32)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int k = tid + q * kThreads;
+        if (k >= n_e) continue;
+        const int32_t n = enode[q];
         if (sh.e2c[k] < 0) {
             int64_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
             for (int u = sh.eoff[k]; u < sh.eoff[k + 1]; ++u) {
-                const int x = sh.eslot[u];
-                if (x >= h_end) break;  // ascending
-                d0 += ws.ex_req[x][0]; d1 += ws.ex_req[x][1]; d2 += ws.ex_req[x][2]; d3 += 1;
+                const int4 r = sh.erow[u];
+                if (r.x >= c) break;  // ascending; slot < win_hi[c - 1] <=> applied from a pod < c
+                d0 += use64(r.y); d1 += use64(r.z); d2 += use64(r.w); d3 += 1;
             }
-            if (d3) { a.s.rc[n] -= d0; a.s.rm[n] -= d1; a.s.rg[n] -= d2; a.s.nr[n] -= d3; }
+            if (d3) {  // (no other thread touches the node: fire-and-forget atomics, no read back)
+                atomicAdd((unsigned long long*)&a.s.rc[n], (unsigned long long)-d0);
+                atomicAdd((unsigned long long*)&a.s.rm[n], (unsigned long long)-d1);
+                atomicAdd((unsigned long long*)&a.s.rg[n], (unsigned long long)-d2);
+                atomicAdd((unsigned long long*)&a.s.nr[n], (unsigned long long)-d3);
+            }
         }
         a.e_idx[n] = -1;
     }
-    for (int k = tid; k < nslot; k += kThreads) a.n_slot[ws.slot_node[k]] = -1;
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+        if (tid + q * kThreads < nlo) a.n_slot[snd[q]] = -1;
+    for (int k = nlo + tid; k < nslot; k += kThreads) a.n_slot[ws.slot_node[k]] = -1;
+    // the nodes this batch changed — its binds' nodes (every cid with a final bind) and its window's
+    // expiry nodes — for the next batch's overlapped scan (ks_cand.hip window_prep_kernel)
+    {
+        WinWS& wo = *a.sw;
+        if (tid == 0) sh.nbc = 0;
+        __syncthreads();
+        for (int k = tid; k < ncid; k += kThreads)
+            if (sh.fhead[k] >= 0) wo.touched[atomicAdd(&sh.nbc, 1)] = sh.cnode[k];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int k = tid + q * kThreads;
+            if (k < n_e && sh.eoff[k + 1] > sh.eoff[k]) wo.touched[atomicAdd(&sh.nbc, 1)] = enode[q];
+        }
+        __syncthreads();
+        if (tid == 0) wo.n_touched = sh.nbc;
+    }
     if (tid == 0) {
         a.ctr[kCtrStart] = start + c;
         const bool err = stop_code == 2 || stop_code == 3;

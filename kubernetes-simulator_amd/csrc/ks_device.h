@@ -553,6 +553,8 @@ constexpr int kWinSlots = 512;
 constexpr int kChR = 24;    // static candidates kept per pod
 constexpr int kRecDw = 20;  // a candidate node's record, dwords (the widest format: ten int64, ks_cand.hip)
 constexpr int kSlotMax = 1536;  // distinct candidate nodes per batch (the sequential resolver's slots)
+constexpr int kEMax = 1024;     // E nodes per batch: the window's expiry nodes + the overlap's touched nodes
+constexpr int kTouchMax = kWinMaxB + kWinSlots;  // nodes a batch changes: its binds + its window's expiry nodes
 enum : int32_t { kClTrunc = 1 << 8, kClFull = 1 << 9, kClOvf = 1 << 10 };
 struct WinWS {
     int32_t nb, e_cnt, n_e, pad_;
@@ -561,8 +563,10 @@ struct WinWS {
     int32_t ex_q[kWinSlots];              // slot -> expiring pod
     int32_t ex_ok[kWinSlots];             // pre-batch pod bound Ok and not expired yet
     int64_t ex_req[kWinSlots][3];
-    int32_t e_node[kWinSlots];            // distinct nodes of the pre-batch expiries (E)
-    int32_t e_off[kWinSlots + 1];         // E node k's slots: e_slot[e_off[k] .. e_off[k+1]) ascending
+    // E: the distinct nodes of the pre-batch expiries, then (overlapped scan) the nodes changed since
+    // the scan read the node table, with no slots
+    int32_t e_node[kEMax];
+    int32_t e_off[kEMax + 1];             // E node k's slots: e_slot[e_off[k] .. e_off[k+1]) ascending
     int32_t e_slot[kWinSlots];
     // pod i's static candidates, sorted descending
     uint64_t cl_key[kWinMaxB][kChR];
@@ -576,6 +580,11 @@ struct WinWS {
     int32_t slot_node[kSlotMax];
     int32_t slot_eix[kSlotMax];           // the node's index in E, -1 if not an E node
     uint32_t slot_rec[kSlotMax][kRecDw];  // the node's record at the batch start (narrow: 12 dwords)
+    // overlap (scan of batch k+1 beside the resolve of batch k): the nodes batch k changed (its
+    // binds, its window's expiry nodes), written by its commit; and whether batch k+1's lists must
+    // be rescanned (the speculative scan covered other pods, or the touched nodes overflow E)
+    int32_t touched[kTouchMax];
+    int32_t n_touched, rescan;
 };
 
 // Arguments of the batch kernels (expire_head / scan / resolve).
@@ -601,6 +610,8 @@ struct EngineArgs {
     WinWS* sw;               // batch window workspace (nullptr unless allocated)
     int32_t* e_idx;          // [n_pad] node -> index in the window's E, -1 otherwise
     int32_t* n_slot;         // [n_pad] node -> its candidate slot in this batch, -1 otherwise
+    int64_t* spec_ctr;       // the speculative scan's counters (window prep writes: the next batch
+                             // if this one commits all its pods)
 };
 
 // Launchers and limits (defined in ks_kernels.hip).  The batch launchers take a device array of
@@ -612,7 +623,9 @@ int block_nodes();
 hipError_t launch_expire_head(const EngineArgs* d, int S, hipStream_t st);
 // scan of each scenario's blocks [blk_lo, blk_lo + blk_n); grid x = the largest blk_n
 // key16: every total + 1 < 2^16 (scan_kernel's 16-bit key table)
-hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int mode, bool key16, hipStream_t st);
+// cond: only when the window workspace's rescan flag is set (the overlap's fallback)
+hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int mode, bool key16, hipStream_t st,
+                       bool cond = false);
 // per scenario and pod b < batch size: exact top-L over nl sorted lists
 // lists[b*pod_stride + k*list_stride] into out (lists == nullptr: the scenario's own block lists
 // into its candidate lists)
@@ -626,13 +639,16 @@ hipError_t launch_resolve(const EngineArgs* d, int S, int mode, hipStream_t st);
 hipError_t launch_resolve_small(const EngineArgs* d, int S, int mode, hipStream_t st);
 int small_resolver_max_batch();
 int small_resolver_max_nodes();
-// the chunk resolver (ks_chunk.hip): one engine (S = 1), batches of <= kWinMaxB pods, evaluator
-// modes >= kEvalNarrow (node state in int32) and every total + 1 < 2^16; its batch is
-// launch_window_prep(head) -> scan -> launch_merge_cl -> launch_chunk_only
+// the chunk resolver (ks_chunk.hip): one engine (S = 1), batches of <= kWinMaxB pods, node state in
+// 32-bit words (scaled capacities < 2^32 - 1) and every total + 1 < 2^16; its batch is
+// launch_window_prep(head) -> scan -> launch_merge_cl -> launch_chunk_only, or with the overlap
+// launch_window_prep(head, spec) -> conditional scan -> merge_cl -> chunk, the next batch's scan
+// on a second stream beside the chunk kernel (its commit writes the touched nodes)
 hipError_t launch_chunk_only(const EngineArgs* d, int mode, hipStream_t st);
 // the batch window (expiries of the batch's pods, the node set E): the resolvers' first kernel;
-// head: also apply the expiries due before the batch's first pod (expire_head's work)
-hipError_t launch_window_prep(const EngineArgs* d, bool head, hipStream_t st);
+// head: also apply the expiries due before the batch's first pod (expire_head's work); spec: the
+// batch's lists come from the speculative scan (the touched nodes join E, or a rescan is flagged)
+hipError_t launch_window_prep(const EngineArgs* d, bool head, bool spec, hipStream_t st);
 // merge + candidate lists (ks_cand.hip): per pod the merge kernel's exact top-L over its lists, then
 // its static candidates and their slots
 hipError_t launch_merge_cl(const EngineArgs* d, int mode, int B, const uint64_t* lists, int64_t pod_stride,

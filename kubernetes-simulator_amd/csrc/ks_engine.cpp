@@ -191,6 +191,14 @@ struct ks_engine {
     int64_t* h_ctr = nullptr;  // pinned
     ks::EngineArgs* d_args = nullptr;  // the kernels' argument record (device)
     ks::EngineArgs* h_args = nullptr;  // its pinned host staging
+    // overlap of the next batch's scan with the chunk resolver (chunk class, one shard): a second
+    // stream, the speculative scan's argument record (ctr = d_spec) and counters, two events
+    bool overlap = true;
+    hipStream_t st2 = nullptr;
+    hipEvent_t ev_ml = nullptr, ev_sc = nullptr;
+    int64_t* d_spec = nullptr;
+    ks::EngineArgs* d_args_spec = nullptr;
+    ks::EngineArgs* h_args_spec = nullptr;
     // group membership (ks_group_add): stream, counters and argument slots belong to the group
     ks_group* group = nullptr;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -261,6 +269,7 @@ ks::EngineArgs make_args(ks_engine* e) {
     a.sw = e->d_sweep;
     a.e_idx = e->d_eidx;
     a.n_slot = e->d_nslot;
+    a.spec_ctr = e->d_spec;
     return a;
 }
 
@@ -463,6 +472,7 @@ ks_status ks_create(const ks_config* cfg, ks_engine** out) {
     ks_engine* e = nullptr;
     const ks_status v = engine_init(cfg, &e);
     if (v != KS_OK) return v;
+    if (const char* ov = std::getenv("KS_OVERLAP")) e->overlap = ov[0] != '0';  // A/B switch
     hipError_t r = hipSetDevice(e->device);
     if (r == hipSuccess) r = hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking);
     if (r == hipSuccess) r = hipMalloc(&e->d_ctr, 32 * sizeof(int64_t));
@@ -509,6 +519,12 @@ void engine_free(ks_engine* e) {
     if (e->d_sweep) (void)hipFree(e->d_sweep);
     if (e->d_eidx) (void)hipFree(e->d_eidx);
     if (e->d_nslot) (void)hipFree(e->d_nslot);
+    if (e->st2) { (void)hipStreamSynchronize(e->st2); (void)hipStreamDestroy(e->st2); }
+    if (e->ev_ml) (void)hipEventDestroy(e->ev_ml);
+    if (e->ev_sc) (void)hipEventDestroy(e->ev_sc);
+    if (e->d_spec) (void)hipFree(e->d_spec);
+    if (e->d_args_spec) (void)hipFree(e->d_args_spec);
+    if (e->h_args_spec) (void)hipHostFree(e->h_args_spec);
     if (e->d_usage) (void)hipFree(e->d_usage);
     if (e->stage) (void)hipHostFree(e->stage);
     if (e->segs) (void)hipHostFree(e->segs);
@@ -1102,6 +1118,24 @@ static ks_status ensure_window_ws(ks_engine* e) {
     HIPCHK(e, hipMemsetAsync(e->d_eidx, 0xFF, sizeof(int32_t) * e->n_pad, e->st));
     HIPCHK(e, hipMalloc(&e->d_nslot, sizeof(int32_t) * e->n_pad));
     HIPCHK(e, hipMemsetAsync(e->d_nslot, 0xFF, sizeof(int32_t) * e->n_pad, e->st));
+    HIPCHK(e, hipMalloc(&e->d_spec, 8 * sizeof(int64_t)));
+    HIPCHK(e, hipMemsetAsync(e->d_spec, 0, 8 * sizeof(int64_t), e->st));
+    HIPCHK(e, hipMalloc(&e->d_args_spec, sizeof(ks::EngineArgs)));
+    HIPCHK(e, hipHostMalloc(&e->h_args_spec, sizeof(ks::EngineArgs), hipHostMallocDefault));
+    {   // the speculative scan's stream leaves a few CUs free: the chunk kernel's workgroup needs a
+        // whole CU's LDS, and a scan grid that fills every CU would hold it back to the scan's end
+        int cus = 0;
+        HIPCHK(e, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device));
+        const int reserve = cus > 32 ? 8 : 0;
+        std::vector<uint32_t> mask((cus + 31) / 32, 0u);
+        for (int c = reserve; c < cus; c++) mask[c / 32] |= 1u << (c % 32);
+        if (reserve > 0)
+            HIPCHK(e, hipExtStreamCreateWithCUMask(&e->st2, (uint32_t)mask.size(), mask.data()));
+        else
+            HIPCHK(e, hipStreamCreateWithFlags(&e->st2, hipStreamNonBlocking));
+    }
+    HIPCHK(e, hipEventCreateWithFlags(&e->ev_ml, hipEventDisableTiming));
+    HIPCHK(e, hipEventCreateWithFlags(&e->ev_sc, hipEventDisableTiming));
     return KS_OK;
 }
 
@@ -1125,6 +1159,17 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
     const bool fused = which == kResolveChunk;
     HIPCHK(e, hipMemcpyAsync(e->d_ctr, e->h_ctr, 5 * sizeof(int64_t), hipMemcpyHostToDevice, st));
     HIPCHK(e, hipMemcpyAsync(e->d_args, e->h_args, sizeof(ks::EngineArgs), hipMemcpyHostToDevice, st));
+    // the overlap (chunk class, one shard, not profiling): batch b + 1's scan on st2 beside batch
+    // b's chunk kernel, over the pods after batch b (the speculative counters window prep writes)
+    // (large clusters: measured slower — C5 3.6 vs 4.0x10^5 pods/s: the speculative scan is longer
+    // than the resolve it hides behind, and its early-stop rescans land on the critical path)
+    const bool overlap = fused && e->overlap && e->world * e->vsh == 1 && !e->profiling && e->d_args_spec &&
+                         e->nblk <= 1024;
+    if (overlap) {
+        *e->h_args_spec = *e->h_args;
+        e->h_args_spec->ctr = e->d_spec;
+        HIPCHK(e, hipMemcpyAsync(e->d_args_spec, e->h_args_spec, sizeof(ks::EngineArgs), hipMemcpyHostToDevice, st));
+    }
     HIPCHK(e, hipEventRecord(e->ev[0], st));
     const ks::EngineArgs* d = e->d_args;
     int64_t start = e->done;
@@ -1146,10 +1191,14 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
             }
             // the chunk resolver's chain is fused: window prep with the head's expiries, the scan,
             // merge with the candidate lists, the resolver (four launches per batch)
+            // overlap: batch b > 0 of this pass takes the speculative scan's lists (a conditional
+            // rescan when they do not fit, ks_cand.hip window_prep_kernel)
+            const bool spec = overlap && b > 0;
+            if (spec) HIPCHK(e, hipStreamWaitEvent(st, e->ev_sc, 0));
             if (ev[0]) HIPCHK(e, hipEventRecord(ev[0], st));
-            HIPCHK(e, fused ? ks::launch_window_prep(d, true, st) : ks::launch_expire_head(d, 1, st));
+            HIPCHK(e, fused ? ks::launch_window_prep(d, true, spec, st) : ks::launch_expire_head(d, 1, st));
             if (ev[1]) HIPCHK(e, hipEventRecord(ev[1], st));
-            HIPCHK(e, ks::launch_scan(d, 1, e->blk_n, e->B, e->PG, e->mode, key16(e), st));
+            HIPCHK(e, ks::launch_scan(d, 1, e->blk_n, e->B, e->PG, e->mode, key16(e), st, spec));
             if (ev[2]) HIPCHK(e, hipEventRecord(ev[2], st));
             const int G = e->world * e->vsh;
             const int64_t L = ks::kTopL, BL = (int64_t)e->B * L;
@@ -1181,7 +1230,13 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
                                 : ks::launch_merge(d, 1, e->B, e->cand_all, L, G, BL, e->cand, G, st));
             }
             if (ev[3]) HIPCHK(e, hipEventRecord(ev[3], st));
+            if (overlap && b + 1 < nbat) HIPCHK(e, hipEventRecord(e->ev_ml, st));
             HIPCHK(e, fused ? ks::launch_chunk_only(d, e->mode, st) : launch_resolver(d, 1, e->mode, which, st));
+            if (overlap && b + 1 < nbat) {  // the next batch's scan, once this batch's lists are merged
+                HIPCHK(e, hipStreamWaitEvent(e->st2, e->ev_ml, 0));
+                HIPCHK(e, ks::launch_scan(e->d_args_spec, 1, e->blk_n, e->B, e->PG, e->mode, key16(e), e->st2));
+                HIPCHK(e, hipEventRecord(e->ev_sc, e->st2));
+            }
             if (ev[4]) HIPCHK(e, hipEventRecord(ev[4], st));
             launches++;
         }

@@ -121,10 +121,12 @@ __global__ __launch_bounds__(256) void expire_head_kernel(const EngineArgs* __re
 // KT: the key table's word, uint16_t when every total + 1 < 2^16 (the host's check on the scorer
 // weights) — half the LDS per workgroup, so more workgroups fit a CU.
 template <int kMode, typename KT>
-__global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict__ A, int xcd) {
+__global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict__ A, int xcd, int cond) {
     extern __shared__ uint32_t kv_raw[];
     KT* const kv = reinterpret_cast<KT*>(kv_raw);  // [PG][kBlockNodes]: total+1 per (pod, node of the block)
     const EngineArgs a = A[blockIdx.z];
+    // cond: the overlap's fallback scan, needed only when window prep flagged a rescan
+    if (cond && *(volatile const int32_t*)&a.sw->rescan == 0) return;
     const int64_t start = sload(a.ctr + kCtrStart), end = sload(a.ctr + kCtrEnd);
     if (sload(a.ctr + kCtrErr) != 0) return;
     const int64_t nb = min<int64_t>(a.B, end - start);
@@ -1189,16 +1191,17 @@ hipError_t launch_expire_head(const EngineArgs* d, int S, hipStream_t st) {
 }
 
 template <typename KT>
-static void launch_scan_t(const EngineArgs* d, const dim3& g, size_t lds, int mode, int xcd, hipStream_t st) {
+static void launch_scan_t(const EngineArgs* d, const dim3& g, size_t lds, int mode, int xcd, int cond, hipStream_t st) {
     switch (mode) {
-        case kEvalMicro: hipLaunchKernelGGL((scan_kernel<kEvalMicro, KT>), g, dim3(kBlockNodes), lds, st, d, xcd); break;
-        case kEvalTiny: hipLaunchKernelGGL((scan_kernel<kEvalTiny, KT>), g, dim3(kBlockNodes), lds, st, d, xcd); break;
-        case kEvalNarrow: hipLaunchKernelGGL((scan_kernel<kEvalNarrow, KT>), g, dim3(kBlockNodes), lds, st, d, xcd); break;
-        default: hipLaunchKernelGGL((scan_kernel<kEvalWide, KT>), g, dim3(kBlockNodes), lds, st, d, xcd); break;
+        case kEvalMicro: hipLaunchKernelGGL((scan_kernel<kEvalMicro, KT>), g, dim3(kBlockNodes), lds, st, d, xcd, cond); break;
+        case kEvalTiny: hipLaunchKernelGGL((scan_kernel<kEvalTiny, KT>), g, dim3(kBlockNodes), lds, st, d, xcd, cond); break;
+        case kEvalNarrow: hipLaunchKernelGGL((scan_kernel<kEvalNarrow, KT>), g, dim3(kBlockNodes), lds, st, d, xcd, cond); break;
+        default: hipLaunchKernelGGL((scan_kernel<kEvalWide, KT>), g, dim3(kBlockNodes), lds, st, d, xcd, cond); break;
     }
 }
 
-hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int mode, bool key16, hipStream_t st) {
+hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int mode, bool key16, hipStream_t st,
+                       bool cond) {
     if (blk_n > 0 && S > 0) {
         // one (block, pod group) item per workgroup; one engine: the XCD-aware 1-D deal
         const int groups = (B + PG - 1) / PG;
@@ -1206,9 +1209,9 @@ hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int
         const bool xcd = S == 1;
         const dim3 g = xcd ? dim3((unsigned)(((int64_t)blk_n * groups + 7) / 8 * 8), 1, 1) : dim3(blk_n, groups, S);
         if (key16)
-            launch_scan_t<uint16_t>(d, g, lds, mode, xcd ? 1 : 0, st);
+            launch_scan_t<uint16_t>(d, g, lds, mode, xcd ? 1 : 0, cond ? 1 : 0, st);
         else
-            launch_scan_t<uint32_t>(d, g, lds, mode, xcd ? 1 : 0, st);
+            launch_scan_t<uint32_t>(d, g, lds, mode, xcd ? 1 : 0, cond ? 1 : 0, st);
     }
     return hipGetLastError();
 }

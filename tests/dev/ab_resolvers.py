@@ -1,6 +1,7 @@
 """A/B of the resolvers on the C3 bench workload (and C5 with --c5): per-launch resolve / scan /
 other device time (HIP events), pods per launch, wall pods/s and a CRC of the binds (must agree).
-    python tests/dev/ab_resolvers.py [--c5] [one_pod chunk chunk@256 ...]   (@B = batch)"""
+    python tests/dev/ab_resolvers.py [--c5] [--noprof] [one_pod chunk chunk@256 ...]   (@B = batch)
+--noprof: no per-kernel events (the overlapped chain runs; only the wall rate and CRC mean anything)"""
 import os, sys, time, zlib
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -25,7 +26,8 @@ for rep in range(2):
         eng.load_nodes(enc["alloc"], enc["taint"], enc["label"])
         eng.submit(enc["pods"])
         eng.step(32768)
-        eng.set_profiling(True)
+        if "--noprof" not in sys.argv:  # (profiling times each kernel: no overlap)
+            eng.set_profiling(True)
         t = time.perf_counter(); b = eng.step(65536); dt = time.perf_counter() - t
         st = eng.last_step_stats()
         nl = max(st["launches"], 1)
