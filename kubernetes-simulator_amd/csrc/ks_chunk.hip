@@ -516,11 +516,11 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
         const int32_t* q = xtmp[esl];
         sh.erow[tid] = make_int4(sh.xeff[esl], q[0], q[1], q[2]);
     }
-    DG(uint64_t ts2 = dstamp(); uint64_t sub_k = 0;)
+    DG(uint64_t ts2 = dstamp(); uint64_t cs_e = 0, cs_r = 0, cs_x = 0;)
     __syncthreads();
 
     // ---- chunks
-    DG(uint64_t ts3 = dstamp(); uint64_t sub1 = ts1 - t_setup, sub2 = ts2 - ts1, sub3 = ts3 - ts2; t_setup = ts3 - t_setup;)
+    DG(uint64_t ts3 = dstamp(); (void)ts1; (void)ts2; t_setup = ts3 - t_setup;)
     int committed = nb, stop_code = 0, tb = 0;
     for (int c0 = 0; c0 < nb; c0 += kC) {
         const int c1 = nb < c0 + kC ? nb : c0 + kC;
@@ -778,6 +778,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                         }
                 }
                 const int rowsh = lane & ~7;
+                DG(uint64_t c_a = dstamp(); cs_e += c_a - q2;)
                 int rfree = kR;
                 uint32_t efree = 0u;
 #pragma unroll
@@ -829,6 +830,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                         else if (key > dkB) { dkB = key; dcB = k; }
                     }
                 }
+                DG(uint64_t c_b = dstamp(); cs_r += c_b - c_a;)
                 if ((sub & 7) == 0 && acth) {  // pre-chunk nodes: the best one not rebound before the pod
                     const int pi = ih - c0;
                     const uint64_t below = (1ull << pi) - 1ull;
@@ -855,6 +857,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
                     if (okA > dkA) { dkA = okA; dcA = ocA; }
                     if (okB > dkB) { dkB = okB; dcB = ocB; }
                 }
+                DG(cs_x += dstamp() - c_b;)
                 const int gsh = lane & ~(G - 1);
                 const bool bad = half ? ((__ballot(badB) >> gsh) & 0xFFFFu) != 0 : ((__ballot(badA) >> gsh) & 0xFFFFu) != 0;
                 const uint64_t dk = half ? dkB : dkA;
@@ -1061,8 +1064,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
         for (int q = 0; q < 4; ++q) atomicAdd(&d[24 + q], acc_ph[q]);
         atomicAdd(&d[28], (unsigned long long)n_sonly);
         atomicAdd(&d[15], acc_cs);
-        // d[29] low: loads, high: E inserts + list keys
-        atomicAdd(&d[29], sub1 + (sub_k << 32)); atomicAdd(&d[30], sub2); atomicAdd(&d[31], sub3);
+            atomicAdd(&d[29], cs_e); atomicAdd(&d[30], cs_r); atomicAdd(&d[31], cs_x);
     }
 #endif
 }

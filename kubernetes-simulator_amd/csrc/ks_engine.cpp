@@ -1194,9 +1194,11 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
             // overlap: batch b > 0 of this pass takes the speculative scan's lists (a conditional
             // rescan when they do not fit, ks_cand.hip window_prep_kernel)
             const bool spec = overlap && b > 0;
-            if (spec) HIPCHK(e, hipStreamWaitEvent(st, e->ev_sc, 0));
             if (ev[0]) HIPCHK(e, hipEventRecord(ev[0], st));
             HIPCHK(e, fused ? ks::launch_window_prep(d, true, spec, st) : ks::launch_expire_head(d, 1, st));
+            // (window prep reads no list: the join with the speculative scan goes after it, before
+            // the conditional rescan that may rewrite the lists and the merge that reads them)
+            if (spec) HIPCHK(e, hipStreamWaitEvent(st, e->ev_sc, 0));
             if (ev[1]) HIPCHK(e, hipEventRecord(ev[1], st));
             HIPCHK(e, ks::launch_scan(d, 1, e->blk_n, e->B, e->PG, e->mode, key16(e), st, spec));
             if (ev[2]) HIPCHK(e, hipEventRecord(ev[2], st));

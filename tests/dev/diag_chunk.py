@@ -31,7 +31,7 @@ print("cycles per launch: setup %.0f, cache %.0f, sweeps %.0f (%.0f per sweep), 
     d[16] / L, d[17] / L, d[18] / L, d[18] / max(d[7], 1), d[19] / L, d[20] / L))
 print("exclusion-only rounds/launch %.1f; phases, cycles per round (both kinds): A marks %.0f, B replay %.0f, C decide %.0f, D converge %.0f" % ((d[28] / L,) + tuple(d[24 + q] / max(d[7] + d[28], 1) for q in range(4))))
 print("phase C per exclusion-only round %.0f, per full sweep %.0f cycles; B per full sweep %.0f" % (d[15] / max(d[28], 1), d[26] / max(d[7], 1), d[25] / max(d[7], 1)))
-print("setup split: pod/E init %.0f, slot records + entries %.0f, sync %.0f" % (
-    (d[29] & 0xFFFFFFFF) / L, d[30] / L, d[31] / L))
+print("phase C split per full sweep (wave 0, C1 and entries / rows / cached D + reduce): %.0f / %.0f / %.0f cycles" % (
+    d[29] / max(d[7], 1), d[30] / max(d[7], 1), d[31] / max(d[7], 1)))
 nl = max(st["launches"], 1)
 print(f"resolve {st['resolve_ms'] / nl * 1e3:.1f} us/launch (prep + cl + chunk kernels), scan {st['scan_ms'] / nl * 1e3:.1f}, other {st['other_ms'] / nl * 1e3:.1f}")
