@@ -57,7 +57,8 @@ __device__ __forceinline__ const __attribute__((address_space(1))) T* cg(const T
 // touched nodes overflow E, `rescan` asks the conditional scan on the engine's stream to redo the
 // lists on the current table.  The speculative counters for the next scan are written last.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kPrepThreads) void window_prep_kernel(const EngineArgs* __restrict__ A, int head, int spec) {
+__global__ __launch_bounds__(kPrepThreads) void window_prep_kernel(const EngineArgs* __restrict__ A, int head, int spec,
+                                                                    int slot) {
     const EngineArgs& a = A[0];
     WinWS& ws = *a.sw;
     const int tid = threadIdx.x;
@@ -66,11 +67,16 @@ __global__ __launch_bounds__(kPrepThreads) void window_prep_kernel(const EngineA
     __shared__ int32_t xn[kEMax];  // touched nodes to insert (overlap)
     __shared__ int32_t s_ne, s_nx;
     const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
+    // the speculative counters, double-buffered by batch parity: this batch writes `slot` (read by
+    // the next batch's speculative scan, which may still run while the batch after writes the
+    // other), and checks the previous batch's
+    int64_t* const spec_out = a.spec_ctr + kSpecStride * slot;
+    const int64_t* const spec_in = a.spec_ctr + kSpecStride * (slot ^ 1);
     int nb = (int)min<int64_t>(min<int64_t>(a.B, kWinMaxB), end - start);
     if (a.ctr[kCtrErr] != 0 || nb <= 0) {
         if (tid == 0) {
             ws.nb = 0; ws.e_cnt = 0; ws.n_e = 0; ws.rescan = 0;
-            a.spec_ctr[kCtrStart] = end; a.spec_ctr[kCtrEnd] = end; a.spec_ctr[kCtrErr] = 0;
+            spec_out[kCtrStart] = end; spec_out[kCtrEnd] = end; spec_out[kCtrErr] = 0;
         }
         return;
     }
@@ -84,7 +90,7 @@ __global__ __launch_bounds__(kPrepThreads) void window_prep_kernel(const EngineA
     // overlap: the lists are usable when the speculative scan covered this batch's pods and the
     // changed nodes fit E
     int rescan = 0;
-    if (spec) rescan = start != a.spec_ctr[kCtrStart] || (int64_t)e_cnt + (e1 - e0) + ws.n_touched > kEMax;
+    if (spec) rescan = start != spec_in[kCtrStart] || (int64_t)e_cnt + (e1 - e0) + ws.n_touched > kEMax;
     const bool touch = spec && !rescan;
     if (head) {  // expire_head's work: the expiries due before the batch's first pod
         for (int64_t e = e0 + tid; e < e1; e += kPrepThreads) {
@@ -188,7 +194,7 @@ __global__ __launch_bounds__(kPrepThreads) void window_prep_kernel(const EngineA
     if (tid == 0) {
         ws.nb = nb; ws.e_cnt = e_cnt; ws.n_e = n_e; ws.nslot = 0; ws.rescan = rescan;
         // the next speculative scan: the pods after this batch, if it commits them all
-        a.spec_ctr[kCtrStart] = start + nb; a.spec_ctr[kCtrEnd] = end; a.spec_ctr[kCtrErr] = 0;
+        spec_out[kCtrStart] = start + nb; spec_out[kCtrEnd] = end; spec_out[kCtrErr] = 0;
     }
 }
 
@@ -371,8 +377,9 @@ __global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs* __rest
 
 }  // namespace sq
 
-hipError_t launch_window_prep(const EngineArgs* d, bool head, bool spec, hipStream_t st) {
-    hipLaunchKernelGGL(sq::window_prep_kernel, dim3(1), dim3(sq::kPrepThreads), 0, st, d, head ? 1 : 0, spec ? 1 : 0);
+hipError_t launch_window_prep(const EngineArgs* d, bool head, bool spec, int slot, hipStream_t st) {
+    hipLaunchKernelGGL(sq::window_prep_kernel, dim3(1), dim3(sq::kPrepThreads), 0, st, d, head ? 1 : 0, spec ? 1 : 0,
+                       slot & 1);
     return hipGetLastError();
 }
 

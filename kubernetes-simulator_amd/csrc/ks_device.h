@@ -554,7 +554,8 @@ constexpr int kChR = 24;    // static candidates kept per pod
 constexpr int kRecDw = 20;  // a candidate node's record, dwords (the widest format: ten int64, ks_cand.hip)
 constexpr int kSlotMax = 1536;  // distinct candidate nodes per batch (the sequential resolver's slots)
 constexpr int kEMax = 1024;     // E nodes per batch: the window's expiry nodes + the overlap's touched nodes
-constexpr int kTouchMax = kWinMaxB + kWinSlots;  // nodes a batch changes: its binds + its window's expiry nodes
+constexpr int kTouchMax = kWinMaxB + kWinSlots;
+constexpr int kSpecStride = 8;  // int64 counters per speculative set  // nodes a batch changes: its binds + its window's expiry nodes
 enum : int32_t { kClTrunc = 1 << 8, kClFull = 1 << 9, kClOvf = 1 << 10 };
 struct WinWS {
     int32_t nb, e_cnt, n_e, pad_;
@@ -610,8 +611,8 @@ struct EngineArgs {
     WinWS* sw;               // batch window workspace (nullptr unless allocated)
     int32_t* e_idx;          // [n_pad] node -> index in the window's E, -1 otherwise
     int32_t* n_slot;         // [n_pad] node -> its candidate slot in this batch, -1 otherwise
-    int64_t* spec_ctr;       // the speculative scan's counters (window prep writes: the next batch
-                             // if this one commits all its pods)
+    int64_t* spec_ctr;       // the speculative scan's counters, two sets of kSpecStride (window prep
+                             // writes: the next batch if this one commits all its pods)
 };
 
 // Launchers and limits (defined in ks_kernels.hip).  The batch launchers take a device array of
@@ -648,7 +649,9 @@ hipError_t launch_chunk_only(const EngineArgs* d, int mode, hipStream_t st);
 // the batch window (expiries of the batch's pods, the node set E): the resolvers' first kernel;
 // head: also apply the expiries due before the batch's first pod (expire_head's work); spec: the
 // batch's lists come from the speculative scan (the touched nodes join E, or a rescan is flagged)
-hipError_t launch_window_prep(const EngineArgs* d, bool head, bool spec, hipStream_t st);
+// slot: the speculative counters' buffer this batch writes (batch parity; the previous batch's is
+// slot ^ 1)
+hipError_t launch_window_prep(const EngineArgs* d, bool head, bool spec, int slot, hipStream_t st);
 // merge + candidate lists (ks_cand.hip): per pod the merge kernel's exact top-L over its lists, then
 // its static candidates and their slots
 hipError_t launch_merge_cl(const EngineArgs* d, int mode, int B, const uint64_t* lists, int64_t pod_stride,

@@ -197,7 +197,7 @@ struct ks_engine {
     hipStream_t st2 = nullptr;
     hipEvent_t ev_ml = nullptr, ev_sc = nullptr;
     int64_t* d_spec = nullptr;
-    ks::EngineArgs* d_args_spec = nullptr;
+    ks::EngineArgs* d_args_spec = nullptr;  // [2]: ctr = d_spec + kSpecStride * parity
     ks::EngineArgs* h_args_spec = nullptr;
     // group membership (ks_group_add): stream, counters and argument slots belong to the group
     ks_group* group = nullptr;
@@ -1118,10 +1118,10 @@ static ks_status ensure_window_ws(ks_engine* e) {
     HIPCHK(e, hipMemsetAsync(e->d_eidx, 0xFF, sizeof(int32_t) * e->n_pad, e->st));
     HIPCHK(e, hipMalloc(&e->d_nslot, sizeof(int32_t) * e->n_pad));
     HIPCHK(e, hipMemsetAsync(e->d_nslot, 0xFF, sizeof(int32_t) * e->n_pad, e->st));
-    HIPCHK(e, hipMalloc(&e->d_spec, 8 * sizeof(int64_t)));
-    HIPCHK(e, hipMemsetAsync(e->d_spec, 0, 8 * sizeof(int64_t), e->st));
-    HIPCHK(e, hipMalloc(&e->d_args_spec, sizeof(ks::EngineArgs)));
-    HIPCHK(e, hipHostMalloc(&e->h_args_spec, sizeof(ks::EngineArgs), hipHostMallocDefault));
+    HIPCHK(e, hipMalloc(&e->d_spec, 2 * ks::kSpecStride * sizeof(int64_t)));
+    HIPCHK(e, hipMemsetAsync(e->d_spec, 0, 2 * ks::kSpecStride * sizeof(int64_t), e->st));
+    HIPCHK(e, hipMalloc(&e->d_args_spec, 2 * sizeof(ks::EngineArgs)));
+    HIPCHK(e, hipHostMalloc(&e->h_args_spec, 2 * sizeof(ks::EngineArgs), hipHostMallocDefault));
     {   // the speculative scan's stream leaves a few CUs free: the chunk kernel's workgroup needs a
         // whole CU's LDS, and a scan grid that fills every CU would hold it back to the scan's end
         int cus = 0;
@@ -1166,9 +1166,11 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
     const bool overlap = fused && e->overlap && e->world * e->vsh == 1 && !e->profiling && e->d_args_spec &&
                          e->nblk <= 1024;
     if (overlap) {
-        *e->h_args_spec = *e->h_args;
-        e->h_args_spec->ctr = e->d_spec;
-        HIPCHK(e, hipMemcpyAsync(e->d_args_spec, e->h_args_spec, sizeof(ks::EngineArgs), hipMemcpyHostToDevice, st));
+        for (int k = 0; k < 2; k++) {
+            e->h_args_spec[k] = *e->h_args;
+            e->h_args_spec[k].ctr = e->d_spec + ks::kSpecStride * k;
+        }
+        HIPCHK(e, hipMemcpyAsync(e->d_args_spec, e->h_args_spec, 2 * sizeof(ks::EngineArgs), hipMemcpyHostToDevice, st));
     }
     HIPCHK(e, hipEventRecord(e->ev[0], st));
     const ks::EngineArgs* d = e->d_args;
@@ -1195,7 +1197,7 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
             // rescan when they do not fit, ks_cand.hip window_prep_kernel)
             const bool spec = overlap && b > 0;
             if (ev[0]) HIPCHK(e, hipEventRecord(ev[0], st));
-            HIPCHK(e, fused ? ks::launch_window_prep(d, true, spec, st) : ks::launch_expire_head(d, 1, st));
+            HIPCHK(e, fused ? ks::launch_window_prep(d, true, spec, (int)(b & 1), st) : ks::launch_expire_head(d, 1, st));
             // (window prep reads no list: the join with the speculative scan goes after it, before
             // the conditional rescan that may rewrite the lists and the merge that reads them)
             if (spec) HIPCHK(e, hipStreamWaitEvent(st, e->ev_sc, 0));
@@ -1236,7 +1238,7 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
             HIPCHK(e, fused ? ks::launch_chunk_only(d, e->mode, st) : launch_resolver(d, 1, e->mode, which, st));
             if (overlap && b + 1 < nbat) {  // the next batch's scan, once this batch's lists are merged
                 HIPCHK(e, hipStreamWaitEvent(e->st2, e->ev_ml, 0));
-                HIPCHK(e, ks::launch_scan(e->d_args_spec, 1, e->blk_n, e->B, e->PG, e->mode, key16(e), e->st2));
+                HIPCHK(e, ks::launch_scan(e->d_args_spec + (b & 1), 1, e->blk_n, e->B, e->PG, e->mode, key16(e), e->st2));
                 HIPCHK(e, hipEventRecord(e->ev_sc, e->st2));
             }
             if (ev[4]) HIPCHK(e, hipEventRecord(ev[4], st));
