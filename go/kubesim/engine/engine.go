@@ -133,6 +133,27 @@ func (e *Engine) Close() {
 	runtime.SetFinalizer(e, nil)
 }
 
+// CommUniqueID makes the RCCL communicator id rank 0 broadcasts to the others (ks_comm_unique_id).
+func CommUniqueID() ([]byte, error) {
+	id := make([]byte, C.KS_COMM_ID_BYTES)
+	if rc := C.ks_comm_unique_id((*C.uint8_t)(unsafe.Pointer(&id[0]))); rc != C.KS_OK {
+		return nil, status(nil, rc)
+	}
+	return id, nil
+}
+
+// Shard makes this engine rank `rank` of `world` node-sharded engines (one per GPU, ks_shard):
+// each scans its node range and the per-pod candidate lists are all-gathered over RCCL once per
+// batch; every rank loads the whole cluster and submits the same pods, and all binds are
+// identical.  Call before LoadNodes.
+func (e *Engine) Shard(world, rank int, id []byte, vshards int) error {
+	if len(id) != C.KS_COMM_ID_BYTES {
+		return errors.Errorf("communicator id: %d bytes, want %d", len(id), C.KS_COMM_ID_BYTES)
+	}
+	rc := C.ks_shard(e.h, C.int32_t(world), C.int32_t(rank), (*C.uint8_t)(unsafe.Pointer(&id[0])), C.int32_t(vshards))
+	return status(e, rc)
+}
+
 // LoadNodes loads the cluster once: alloc = n*4 {milli cpu, milli memory, milli gpu, pods}
 // (-1 = key absent), taint / label = dictionary bitmasks (Dicts).
 func (e *Engine) LoadNodes(alloc []int64, taint, label []uint64) error {

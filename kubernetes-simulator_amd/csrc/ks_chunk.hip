@@ -22,6 +22,7 @@
 #include <climits>
 
 #include "ks_device.h"
+#include "ks_scan.h"
 
 namespace ks {
 namespace chk {
@@ -32,6 +33,7 @@ constexpr int kB = kWinMaxB;  // pods per batch
 constexpr int kC = 64;          // pods per chunk: one lane each
 constexpr int kR = kChR;        // static candidates kept per pod
 constexpr int kCid = 1024;      // candidate ids per batch (the batch's candidate slots)
+constexpr int kMaxPGScan = 32;  // pods per scan group (the host's PG bound, ks_kernels.hip kMaxPG)
 constexpr int kCidSlots = kCid - kR;  // slots that are cids; the rest: pod 0's private cids
 constexpr int kSlots = kWinSlots;
 constexpr int kSeg = 5;         // stored state segments per replayed node within a chunk
@@ -373,8 +375,7 @@ __device__ __forceinline__ void store_prec(ChShared& sh, int k, const uint4* r) 
 }
 
 template <int kMode>
-__global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArgs* __restrict__ A) {
-    __shared__ ChShared sh;
+__device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChShared& sh) {
     const EngineArgs& a = A[0];
     const WinWS& ws = *a.sw;
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid >> 6;
@@ -1069,10 +1070,59 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
 #endif
 }
 
+template <int kMode>
+__global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArgs* __restrict__ A) {
+    __shared__ ChShared sh;
+    chunk_body<kMode>(A, sh);
+}
+
+// The chunk kernel with the next batch's scan fused in (the overlap on one stream): workgroup 0
+// resolves the batch; the others — one per CU, the resolver's LDS footprint fixes that — scan the
+// speculative pods (As: counters window prep wrote) in the resolver's LDS image, two (node block,
+// pod group) items at a time, one per 256-thread half, items w, w + W, ... of the batch's
+// block-major item list.  The scan reads node records the resolver may be committing: only
+// nodes the batch touches, which the next batch re-evaluates (ks_cand.hip window_prep_kernel).
+template <int kMode>
+__global__ __launch_bounds__(kThreads) void chunk_scan_kernel(const EngineArgs* __restrict__ A,
+                                                              const EngineArgs* __restrict__ As) {
+    __shared__ ChShared sh;
+    if (blockIdx.x == 0) {
+        chunk_body<kMode>(A, sh);
+        return;
+    }
+    static_assert(kThreads == 2 * scn::kNodes, "two scan groups per workgroup");
+    const EngineArgs& a = As[0];
+    const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
+    const int64_t nb = min<int64_t>(a.B, end - start);
+    if (a.ctr[kCtrErr] != 0 || nb <= 0) return;
+    const int groups = (int)((nb + a.PG - 1) / a.PG);
+    const int64_t tot = (int64_t)a.blk_n * groups;
+    const int half = threadIdx.x / scn::kNodes, lt = threadIdx.x % scn::kNodes;
+    uint16_t* kv = reinterpret_cast<uint16_t*>(&sh) + (size_t)half * a.PG * scn::kNodes;
+    const int64_t W = 2 * ((int64_t)gridDim.x - 1), w = 2 * ((int64_t)blockIdx.x - 1);
+    for (int64_t r = w; r < tot; r += W) {  // (uniform: r is the workgroup's first item this round)
+        if (r != w) __syncthreads();         // the previous round's extraction has read kv
+        const int64_t it = r + half;
+        scn::scan_item<kMode, uint16_t>(a, kv, start, nb, groups, it, it < tot, lt);
+    }
+}
+static_assert(sizeof(ChShared) >= 2 * kMaxPGScan * scn::kNodes * sizeof(uint16_t), "two 16-bit key tables");
+
 }  // namespace chk
 
 // the chunk resolver proper (its window and candidate lists: launch_window_prep(head) and
 // launch_merge_cl, ks_cand.hip)
+hipError_t launch_chunk_scan(const EngineArgs* d, const EngineArgs* ds, int workers, int mode, hipStream_t st) {
+    const dim3 g(1 + workers);
+    switch (mode) {
+        case kEvalMicro: hipLaunchKernelGGL(chk::chunk_scan_kernel<kEvalMicro>, g, dim3(chk::kThreads), 0, st, d, ds); break;
+        case kEvalTiny: hipLaunchKernelGGL(chk::chunk_scan_kernel<kEvalTiny>, g, dim3(chk::kThreads), 0, st, d, ds); break;
+        case kEvalNarrow: hipLaunchKernelGGL(chk::chunk_scan_kernel<kEvalNarrow>, g, dim3(chk::kThreads), 0, st, d, ds); break;
+        default: hipLaunchKernelGGL(chk::chunk_scan_kernel<kEvalWide>, g, dim3(chk::kThreads), 0, st, d, ds); break;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_chunk_only(const EngineArgs* d, int mode, hipStream_t st) {
     switch (mode) {
         case kEvalMicro: hipLaunchKernelGGL(chk::resolve_chunk_kernel<kEvalMicro>, dim3(1), dim3(chk::kThreads), 0, st, d); break;

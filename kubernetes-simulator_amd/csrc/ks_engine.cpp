@@ -191,11 +191,10 @@ struct ks_engine {
     int64_t* h_ctr = nullptr;  // pinned
     ks::EngineArgs* d_args = nullptr;  // the kernels' argument record (device)
     ks::EngineArgs* h_args = nullptr;  // its pinned host staging
-    // overlap of the next batch's scan with the chunk resolver (chunk class, one shard): a second
-    // stream, the speculative scan's argument record (ctr = d_spec) and counters, two events
+    // overlap of the next batch's scan with the chunk resolver (chunk class, one shard): the
+    // speculative scan's argument records (ctr = d_spec + parity) and counters, its workgroups
     bool overlap = true;
-    hipStream_t st2 = nullptr;
-    hipEvent_t ev_ml = nullptr, ev_sc = nullptr;
+    int scan_workers = 0;
     int64_t* d_spec = nullptr;
     ks::EngineArgs* d_args_spec = nullptr;  // [2]: ctr = d_spec + kSpecStride * parity
     ks::EngineArgs* h_args_spec = nullptr;
@@ -519,9 +518,6 @@ void engine_free(ks_engine* e) {
     if (e->d_sweep) (void)hipFree(e->d_sweep);
     if (e->d_eidx) (void)hipFree(e->d_eidx);
     if (e->d_nslot) (void)hipFree(e->d_nslot);
-    if (e->st2) { (void)hipStreamSynchronize(e->st2); (void)hipStreamDestroy(e->st2); }
-    if (e->ev_ml) (void)hipEventDestroy(e->ev_ml);
-    if (e->ev_sc) (void)hipEventDestroy(e->ev_sc);
     if (e->d_spec) (void)hipFree(e->d_spec);
     if (e->d_args_spec) (void)hipFree(e->d_args_spec);
     if (e->h_args_spec) (void)hipHostFree(e->h_args_spec);
@@ -1122,20 +1118,12 @@ static ks_status ensure_window_ws(ks_engine* e) {
     HIPCHK(e, hipMemsetAsync(e->d_spec, 0, 2 * ks::kSpecStride * sizeof(int64_t), e->st));
     HIPCHK(e, hipMalloc(&e->d_args_spec, 2 * sizeof(ks::EngineArgs)));
     HIPCHK(e, hipHostMalloc(&e->h_args_spec, 2 * sizeof(ks::EngineArgs), hipHostMallocDefault));
-    {   // the speculative scan's stream leaves a few CUs free: the chunk kernel's workgroup needs a
-        // whole CU's LDS, and a scan grid that fills every CU would hold it back to the scan's end
+    {   // the fused scan's workgroups: one per CU beside the resolver's (the resolver's LDS
+        // footprint allows one workgroup per CU)
         int cus = 0;
         HIPCHK(e, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device));
-        const int reserve = cus > 32 ? 8 : 0;
-        std::vector<uint32_t> mask((cus + 31) / 32, 0u);
-        for (int c = reserve; c < cus; c++) mask[c / 32] |= 1u << (c % 32);
-        if (reserve > 0)
-            HIPCHK(e, hipExtStreamCreateWithCUMask(&e->st2, (uint32_t)mask.size(), mask.data()));
-        else
-            HIPCHK(e, hipStreamCreateWithFlags(&e->st2, hipStreamNonBlocking));
+        e->scan_workers = std::max(1, cus - 1);
     }
-    HIPCHK(e, hipEventCreateWithFlags(&e->ev_ml, hipEventDisableTiming));
-    HIPCHK(e, hipEventCreateWithFlags(&e->ev_sc, hipEventDisableTiming));
     return KS_OK;
 }
 
@@ -1159,12 +1147,12 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
     const bool fused = which == kResolveChunk;
     HIPCHK(e, hipMemcpyAsync(e->d_ctr, e->h_ctr, 5 * sizeof(int64_t), hipMemcpyHostToDevice, st));
     HIPCHK(e, hipMemcpyAsync(e->d_args, e->h_args, sizeof(ks::EngineArgs), hipMemcpyHostToDevice, st));
-    // the overlap (chunk class, one shard, not profiling): batch b + 1's scan on st2 beside batch
-    // b's chunk kernel, over the pods after batch b (the speculative counters window prep writes)
-    // (large clusters: measured slower — C5 3.6 vs 4.0x10^5 pods/s: the speculative scan is longer
-    // than the resolve it hides behind, and its early-stop rescans land on the critical path)
+    // the overlap (chunk class, one shard, 16-bit keys, not profiling): batch b + 1's scan fused
+    // into batch b's chunk kernel, over the pods after batch b (the speculative counters window
+    // prep writes).  Large clusters keep the plain chain: their scan is longer than the resolve it
+    // would hide behind (C5: 0.33 vs 0.09 ms), and in the fused kernel it runs one workgroup per CU
     const bool overlap = fused && e->overlap && e->world * e->vsh == 1 && !e->profiling && e->d_args_spec &&
-                         e->nblk <= 1024;
+                         key16(e) && e->nblk <= 1024;
     if (overlap) {
         for (int k = 0; k < 2; k++) {
             e->h_args_spec[k] = *e->h_args;
@@ -1198,9 +1186,6 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
             const bool spec = overlap && b > 0;
             if (ev[0]) HIPCHK(e, hipEventRecord(ev[0], st));
             HIPCHK(e, fused ? ks::launch_window_prep(d, true, spec, (int)(b & 1), st) : ks::launch_expire_head(d, 1, st));
-            // (window prep reads no list: the join with the speculative scan goes after it, before
-            // the conditional rescan that may rewrite the lists and the merge that reads them)
-            if (spec) HIPCHK(e, hipStreamWaitEvent(st, e->ev_sc, 0));
             if (ev[1]) HIPCHK(e, hipEventRecord(ev[1], st));
             HIPCHK(e, ks::launch_scan(d, 1, e->blk_n, e->B, e->PG, e->mode, key16(e), st, spec));
             if (ev[2]) HIPCHK(e, hipEventRecord(ev[2], st));
@@ -1234,13 +1219,10 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
                                 : ks::launch_merge(d, 1, e->B, e->cand_all, L, G, BL, e->cand, G, st));
             }
             if (ev[3]) HIPCHK(e, hipEventRecord(ev[3], st));
-            if (overlap && b + 1 < nbat) HIPCHK(e, hipEventRecord(e->ev_ml, st));
-            HIPCHK(e, fused ? ks::launch_chunk_only(d, e->mode, st) : launch_resolver(d, 1, e->mode, which, st));
-            if (overlap && b + 1 < nbat) {  // the next batch's scan, once this batch's lists are merged
-                HIPCHK(e, hipStreamWaitEvent(e->st2, e->ev_ml, 0));
-                HIPCHK(e, ks::launch_scan(e->d_args_spec + (b & 1), 1, e->blk_n, e->B, e->PG, e->mode, key16(e), e->st2));
-                HIPCHK(e, hipEventRecord(e->ev_sc, e->st2));
-            }
+            if (overlap && b + 1 < nbat)  // the resolver with the next batch's scan beside it
+                HIPCHK(e, ks::launch_chunk_scan(d, e->d_args_spec + (b & 1), e->scan_workers, e->mode, st));
+            else
+                HIPCHK(e, fused ? ks::launch_chunk_only(d, e->mode, st) : launch_resolver(d, 1, e->mode, which, st));
             if (ev[4]) HIPCHK(e, hipEventRecord(ev[4], st));
             launches++;
         }

@@ -28,6 +28,7 @@
 #include <algorithm>
 
 #include "ks_device.h"
+#include "ks_scan.h"
 
 namespace ks {
 
@@ -38,10 +39,6 @@ constexpr int kL = kTopL;                // candidate list length per pod
 #define KS_MAX_PG 32
 #endif
 constexpr int kMaxPG = KS_MAX_PG;        // pods per scan workgroup (LDS key table rows)
-#ifndef KS_SCAN_UNROLL
-#define KS_SCAN_UNROLL 4
-#endif
-constexpr int kScanUnroll = KS_SCAN_UNROLL;  // pods evaluated together per scan loop step
 constexpr int kResolveThreads = 1024;    // 16 waves
 constexpr int kOwnerWave0 = 3;           // waves 3..15 own the touched entries, except
 #ifndef KS_WRITER_WAVE
@@ -149,89 +146,7 @@ __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict_
         if ((int)blockIdx.x >= a.blk_n || (int)blockIdx.y >= groups) return;  // scenarios may differ in size
         it_lo = (int64_t)blockIdx.x * groups + blockIdx.y;
     }
-    const int64_t it_hi = it_lo + 1;
-    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
-#ifdef KS_SCAN_STAMPS  // diagnostic: evaluation / extraction cycles of wave 0, ctr[20] / ctr[21]
-    uint64_t st0;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st0)::"memory");
-#endif
-    int cur = -1, blk = 0;
-    uint32_t blk_base = 0;
-    bool valid = false;
-    NodeV n{};
-    for (int64_t it = it_lo; it < it_hi; ++it) {
-    const int bx = (int)(it / groups), pg0 = (int)(it - (int64_t)bx * groups) * a.PG;
-    if (it != it_lo) __syncthreads();  // the previous item's extraction has read kv
-    if (bx != cur) {
-        cur = bx;
-        blk = a.blk_lo + bx;
-        blk_base = (uint32_t)blk * kBlockNodes;
-        const int64_t node = (int64_t)blk_base + threadIdx.x;
-        valid = node < a.c.n_nodes;
-        n = NodeV{};
-        if (node < (int64_t)a.c.nwb * kWave) n = load_node(a.s, node);
-    }
-    const int np = (int)min<int64_t>(a.PG, nb - pg0);
-    const PodRec* pp = a.pods + start + pg0;
-    int b = 0;
-    // kScanUnroll pods at a time: their scalar loads share one wait and the independent
-    // evaluations interleave (instruction-level parallelism within the wave)
-    for (; b + kScanUnroll <= np; b += kScanUnroll) {
-        PodRec p[kScanUnroll];
-#pragma unroll
-        for (int u = 0; u < kScanUnroll; ++u) p[u] = sload(pp + b + u);  // uniform: SGPRs, scalar cache
-#pragma unroll
-        for (int u = 0; u < kScanUnroll; ++u) {
-            const uint32_t t = eval_t<kMode>(a.c, p[u], n);  // branch-free; padding lanes discarded
-            kv[(b + u) * kBlockNodes + threadIdx.x] = (KT)(valid ? t : 0u);
-        }
-    }
-    for (; b < np; ++b) {
-        const PodRec p = sload(pp + b);
-        const uint32_t t = eval_t<kMode>(a.c, p, n);
-        kv[b * kBlockNodes + threadIdx.x] = (KT)(valid ? t : 0u);
-    }
-    __syncthreads();
-#ifdef KS_SCAN_STAMPS
-    uint64_t st1;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st1)::"memory");
-#endif
-    for (int b = wave; b < np; b += kScanWaves) {
-        uint32_t v[kScanWaves];
-#pragma unroll
-        for (int u = 0; u < kScanWaves; ++u) v[u] = (uint32_t)kv[b * kBlockNodes + u * kWave + lane];  // node u*64 + lane
-        auto out = gptr(a.lists) + ((int64_t)(pg0 + b) * a.nblk + blk) * kL;  // global_: not in lgkmcnt
-        int cnt = 0;
-        for (int r = 0; r < kL && cnt < kL; ++r) {
-            uint32_t lm = v[0];
-#pragma unroll
-            for (int u = 1; u < kScanWaves; ++u) lm = lm > v[u] ? lm : v[u];
-            const uint32_t m = wave_max_u32(lm);
-            if (m == 0) break;
-            int below = cnt;  // nodes of this class before (u, lane) in node order
-#pragma unroll
-            for (int u = 0; u < kScanWaves; ++u) {
-                const uint64_t mask = __ballot(v[u] == m);
-                if (v[u] == m) {
-                    const int rank = below + popc_below(mask, lane);
-                    if (rank < kL) out[rank] = make_key(m, blk_base + u * kWave + lane);
-                    v[u] = 0;
-                }
-                below += __popcll(mask);
-            }
-            cnt = below;
-        }
-        if (lane >= cnt && lane < kL) out[lane] = 0ull;
-    }
-    }  // work items
-#ifdef KS_SCAN_STAMPS
-    uint64_t st2;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st2)::"memory");
-    if (threadIdx.x == 0) {
-        atomicAdd((unsigned long long*)a.ctr + 20, (unsigned long long)(st1 - st0));
-        atomicAdd((unsigned long long*)a.ctr + 21, (unsigned long long)(st2 - st1));
-    }
-#endif
+    scn::scan_item<kMode, KT>(a, kv, start, nb, groups, it_lo, true, threadIdx.x);
 }
 
 // ------------------------------------------------------------------------------------------
