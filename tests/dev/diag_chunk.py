@@ -16,7 +16,8 @@ enc = encode.encode_trace(tr)
 eng = Engine(tick_seconds=10, filter_mode=1, filters=7, scorers=((1, 1, 0), (2, 1, 0)), engine_flags=64)
 eng.load_nodes(enc["alloc"], enc["taint"], enc["label"])
 eng.submit(enc["pods"])
-eng.set_profiling(True)
+if "--noprof" not in sys.argv:  # (profiling times each kernel: no overlap)
+    eng.set_profiling(True)
 eng.step(32768)
 c0 = eng.debug_counters().copy()
 t = time.perf_counter(); eng.step(32768); dt = time.perf_counter() - t
