@@ -29,7 +29,8 @@ namespace sq {
 constexpr int kL = kTopL;
 constexpr int kR = kChR;
 constexpr int kPrepThreads = 1024;
-constexpr int kEHashLog2 = 11, kEHash = 1 << kEHashLog2;
+constexpr int kEHashLog2 = 12, kEHash = 1 << kEHashLog2;
+static_assert(2 * kEMax <= kEHash, "E hash load <= 1/2");
 constexpr int kClBuf = 256;
 static_assert(kR <= kWave, "one candidate per lane");
 static_assert(kWinSlots <= kPrepThreads, "one window slot per prep thread");
@@ -63,7 +64,7 @@ __global__ __launch_bounds__(kPrepThreads) void window_prep_kernel(const EngineA
     WinWS& ws = *a.sw;
     const int tid = threadIdx.x;
     __shared__ int32_t hk[kEHash], hv[kEHash];
-    __shared__ int32_t cnt[kEMax], fill[kEMax];
+    __shared__ int32_t cnt[kWinSlots], fill[kWinSlots];
     __shared__ int32_t xn[kEMax];  // touched nodes to insert (overlap)
     __shared__ int32_t s_ne, s_nx;
     const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
@@ -75,7 +76,7 @@ __global__ __launch_bounds__(kPrepThreads) void window_prep_kernel(const EngineA
     int nb = (int)min<int64_t>(min<int64_t>(a.B, kWinMaxB), end - start);
     if (a.ctr[kCtrErr] != 0 || nb <= 0) {
         if (tid == 0) {
-            ws.nb = 0; ws.e_cnt = 0; ws.n_e = 0; ws.rescan = 0;
+            ws.nb = 0; ws.e_cnt = 0; ws.n_e = 0; ws.n_es = 0; ws.rescan = 0;
             spec_out[kCtrStart] = end; spec_out[kCtrEnd] = end; spec_out[kCtrErr] = 0;
         }
         return;
@@ -106,8 +107,9 @@ __global__ __launch_bounds__(kPrepThreads) void window_prep_kernel(const EngineA
             if (touch) xn[atomicAdd(&s_nx, 1)] = nd;
         }
     }
-    if (touch)
+    if (touch) {
         for (int t = tid; t < ws.n_touched; t += kPrepThreads) xn[atomicAdd(&s_nx, 1)] = ws.touched[t];
+    }
     if (tid < nb) {
         ws.win_hi[tid] = tid >= 1 ? (int32_t)(a.exp_off[start + tid + 1] - e_base) : 0;
         const int64_t pos = a.exp_pos[start + tid];
@@ -136,7 +138,8 @@ __global__ __launch_bounds__(kPrepThreads) void window_prep_kernel(const EngineA
         if (claimed) hv[h] = atomicAdd(&s_ne, 1);
     }
     __syncthreads();
-    // the touched nodes after the slot nodes (no slots: E indices n_e_slots ..)
+    const int n_es = s_ne;  // the slot nodes; the touched nodes after them (no slots)
+    __syncthreads();
     const int n_x = s_nx;
     for (int t = tid; t < n_x; t += kPrepThreads) {
         const int32_t nd = xn[t];
@@ -150,7 +153,7 @@ __global__ __launch_bounds__(kPrepThreads) void window_prep_kernel(const EngineA
     }
     __syncthreads();
     const int n_e = s_ne;
-    if (tid < n_e) { cnt[tid] = 0; fill[tid] = 0; }
+    if (tid < n_es) { cnt[tid] = 0; fill[tid] = 0; }
     __syncthreads();
     int k_of = -1;
     if (my_node >= 0) {
@@ -159,11 +162,10 @@ __global__ __launch_bounds__(kPrepThreads) void window_prep_kernel(const EngineA
         atomicAdd(&cnt[k_of], 1);
     }
     __syncthreads();
-    {  // exclusive prefix of the counts (n_e <= kPrepThreads: one per thread)
-        static_assert(kEMax <= kPrepThreads, "one E node per prep thread");
+    {  // exclusive prefix of the slot nodes' counts (n_es <= kWinSlots: one per thread)
         __shared__ int32_t wsum[kPrepThreads / 64];
         const int lane = tid & 63, wv = tid >> 6;
-        const int v = tid < n_e ? cnt[tid] : 0;
+        const int v = tid < n_es ? cnt[tid] : 0;
         int incl = v;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -174,14 +176,14 @@ __global__ __launch_bounds__(kPrepThreads) void window_prep_kernel(const EngineA
         __syncthreads();
         int base = 0;
         for (int g = 0; g < wv; ++g) base += wsum[g];
-        if (tid < n_e) ws.e_off[tid] = base + incl - v;
-        if (tid == n_e - 1) ws.e_off[n_e] = base + incl;
-        if (n_e == 0 && tid == 0) ws.e_off[0] = 0;
+        if (tid < n_es) ws.e_off[tid] = base + incl - v;
+        if (tid == n_es - 1) ws.e_off[n_es] = base + incl;
+        if (n_es == 0 && tid == 0) ws.e_off[0] = 0;
     }
     __syncthreads();
     if (my_node >= 0) ws.e_slot[ws.e_off[k_of] + atomicAdd(&fill[k_of], 1)] = tid;  // slot x == tid
     __syncthreads();
-    if (tid < n_e) {  // each node's few slots ascending
+    if (tid < n_es) {  // each node's few slots ascending
         const int lo = ws.e_off[tid], hi = ws.e_off[tid + 1];
         for (int u = lo + 1; u < hi; ++u) {
             const int32_t x = ws.e_slot[u];
@@ -189,10 +191,10 @@ __global__ __launch_bounds__(kPrepThreads) void window_prep_kernel(const EngineA
             while (v >= lo && ws.e_slot[v] > x) { ws.e_slot[v + 1] = ws.e_slot[v]; --v; }
             ws.e_slot[v + 1] = x;
         }
-        a.e_idx[ws.e_node[tid]] = tid;
     }
+    for (int k = tid; k < n_e; k += kPrepThreads) a.e_idx[ws.e_node[k]] = k;
     if (tid == 0) {
-        ws.nb = nb; ws.e_cnt = e_cnt; ws.n_e = n_e; ws.nslot = 0; ws.rescan = rescan;
+        ws.nb = nb; ws.e_cnt = e_cnt; ws.n_e = n_e; ws.n_es = n_es; ws.nslot = 0; ws.rescan = rescan;
         // the next speculative scan: the pods after this batch, if it commits them all
         spec_out[kCtrStart] = start + nb; spec_out[kCtrEnd] = end; spec_out[kCtrErr] = 0;
     }
@@ -234,11 +236,12 @@ __device__ __forceinline__ void cand_list(const EngineArgs& a, WinWS& ws, int i,
     const uint64_t last = cand[kL - 1];
     const bool full = last != 0;
     const uint64_t thr = full ? last : 1ull;
-    const int hi = ws.win_hi[i], n_e = ws.n_e;
+    const int hi = ws.win_hi[i], n_e = ws.n_e, n_es = ws.n_es;
     for (int k = tid; k < n_e; k += nthr) {
         const int32_t n = ws.e_node[k];
         NodeV v = load_node(a.s, n);
-        for (int u = ws.e_off[k], ue = ws.e_off[k + 1]; u < ue; ++u) {
+        const int ue = k < n_es ? ws.e_off[k + 1] : 0;
+        for (int u = k < n_es ? ws.e_off[k] : 0; u < ue; ++u) {
             const int x = ws.e_slot[u];
             if (x >= hi) break;  // ascending
             v.rc -= ws.ex_req[x][0]; v.rm -= ws.ex_req[x][1]; v.rg -= ws.ex_req[x][2]; v.nr -= 1;

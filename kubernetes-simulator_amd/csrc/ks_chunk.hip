@@ -129,7 +129,8 @@ struct ChShared {
     uint8_t clcnt[kB], clfl[kB];
     int16_t win_hi[kB], own[kB];
     int16_t xeff[kSlots];         // slot x is applied from pod xeff[x] on
-    int16_t eoff[kEMax + 1];
+    int16_t eoff[kSlots + 1];     // slot-E node k's slots: [eoff[k], eoff[k+1]) (E nodes without
+                                  // slots — the overlap's touched nodes — are plain nodes here)
     // E-slot u (E node k's slots are [eoff[k], eoff[k+1]), ascending): {xeff of its slot, the
     // expiring pod's requests as words} — a replay's expiry event in one 16-byte read
     int4 erow[kSlots];
@@ -146,7 +147,7 @@ struct ChShared {
         int16_t c[kWaves][kC][2];  // k[.][.][1] == ~0: the lane met an unknown state
     } x;
     int16_t ceix[kCid];           // cid -> the node's index in E, -1 if not an E node
-    int16_t e2c[kEMax];           // E index -> cid, -1: the E node is no candidate of this batch
+    int16_t e2c[kSlots];          // slot-E index -> cid, -1: the E node is no candidate of this batch
     int32_t nbc, cut, fc[2], fs[2];
     uint64_t chg;                 // chunk rows (slots c0 + j) rewritten since the last full sweep
 #ifdef KS_CHUNK_DIAG
@@ -382,7 +383,7 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
     const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
     int nb = ws.nb;
     if (a.ctr[kCtrErr] != 0 || nb <= 0) return;
-    const int n_e = ws.n_e, e_cnt = ws.e_cnt;
+    const int n_e = ws.n_es, n_eall = ws.n_e, e_cnt = ws.e_cnt;  // (n_e: the slot-E nodes)
 
     // ---- setup: pods, window, candidate ids, records.  The candidate ids are the batch's
     // candidate slots (ks_cand.hip cand_list: one per distinct node of the lists, claimed through
@@ -409,15 +410,15 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
         xr0 = ws.ex_req[tid][0]; xr1 = ws.ex_req[tid][1]; xr2 = ws.ex_req[tid][2]; esl = ws.e_slot[tid];
         xq = ws.ex_ok[tid] ? ws.ex_q[tid] : -1;  // (for the commit)
     }
-    static_assert(kEMax <= 2 * kThreads, "two E nodes per thread");
-    int32_t enode[2];  // (for the commit)
+    static_assert(kEMax <= 4 * kThreads, "four E nodes per thread");
+    int32_t enode[4];  // (for the commit: e_idx reset; [0] the slot-E node tid's expiries)
 #pragma unroll
-    for (int q = 0; q < 2; ++q) enode[q] = tid + q * kThreads < n_e ? ws.e_node[tid + q * kThreads] : -1;
+    for (int q = 0; q < 4; ++q) enode[q] = tid + q * kThreads < n_eall ? ws.e_node[tid + q * kThreads] : -1;
     static_assert(kSlots <= kThreads, "one window slot per thread");
-    static_assert(kEMax + 1 <= 3 * kThreads, "three E offsets per thread");
-    int32_t eo[3];
+    static_assert(kSlots + 1 <= 2 * kThreads, "two E offsets per thread");
+    int32_t eo[2];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) eo[q] = tid + q * kThreads <= n_e ? ws.e_off[tid + q * kThreads] : 0;
+    for (int q = 0; q < 2; ++q) eo[q] = tid + q * kThreads <= n_e ? ws.e_off[tid + q * kThreads] : 0;
     static_assert(kCidSlots <= 2 * kThreads, "two slot records per thread");
     int32_t snd[2], sex[2];
     uint4 srec[2][3];
@@ -427,6 +428,7 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
         const bool v = k < nlo;
         snd[q] = v ? ws.slot_node[k] : -1;
         sex[q] = v ? ws.slot_eix[k] : -1;
+        if (sex[q] >= n_e) sex[q] = -1;  // an E node without slots: no events here
         const uint4* r = reinterpret_cast<const uint4*>(ws.slot_rec[v ? k : 0]);
 #pragma unroll
         for (int w = 0; w < 3; ++w) srec[q][w] = v ? r[w] : make_uint4(0, 0, 0, 0);
@@ -464,7 +466,7 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
         xtmp[tid][0] = word32(xr0); xtmp[tid][1] = word32(xr1); xtmp[tid][2] = word32(xr2);
     }
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
+    for (int q = 0; q < 2; ++q) {
         const int k = tid + q * kThreads;
         if (k <= n_e) sh.eoff[k] = (int16_t)eo[q];
         if (k < n_e) sh.e2c[k] = -1;
@@ -498,7 +500,8 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
             if (i > 0) { atomicMin(&sh.nbc, i); continue; }
             cid = kCidSlots + r;  // pod 0's private cid
             const int32_t nd = key_node(key);
-            const int ex = a.e_idx[nd];
+            int ex = a.e_idx[nd];
+            if (ex >= n_e) ex = -1;  // (an E node without slots)
             sh.cnode[cid] = nd;
             sh.ceix[cid] = (int16_t)ex;
             if (ex >= 0) sh.e2c[ex] = (int16_t)cid;
@@ -993,29 +996,27 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
             a.s.rc[n] = use64(v.rc); a.s.rm[n] = use64(v.rm); a.s.rg[n] = use64(v.rg); a.s.nr[n] = v.nr;
         }
     }
-    // E nodes that are no candidate of this batch: their expiries before pod c - 1's bind here
-    // (requests from the LDS words: exact, an admitted request is below its capacity < 2^32)
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int k = tid + q * kThreads;
-        if (k >= n_e) continue;
-        const int32_t n = enode[q];
-        if (sh.e2c[k] < 0) {
-            int64_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
-            for (int u = sh.eoff[k]; u < sh.eoff[k + 1]; ++u) {
-                const int4 r = sh.erow[u];
-                if (r.x >= c) break;  // ascending; slot < win_hi[c - 1] <=> applied from a pod < c
-                d0 += use64(r.y); d1 += use64(r.z); d2 += use64(r.w); d3 += 1;
-            }
-            if (d3) {  // (no other thread touches the node: fire-and-forget atomics, no read back)
-                atomicAdd((unsigned long long*)&a.s.rc[n], (unsigned long long)-d0);
-                atomicAdd((unsigned long long*)&a.s.rm[n], (unsigned long long)-d1);
-                atomicAdd((unsigned long long*)&a.s.rg[n], (unsigned long long)-d2);
-                atomicAdd((unsigned long long*)&a.s.nr[n], (unsigned long long)-d3);
-            }
+    // slot-E nodes that are no candidate of this batch: their expiries before pod c - 1's bind
+    // here (requests from the LDS words: exact, an admitted request is below its capacity < 2^32)
+    static_assert(kSlots <= kThreads, "one slot-E node per thread");
+    if (tid < n_e && sh.e2c[tid] < 0) {
+        const int32_t n = enode[0];
+        int64_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+        for (int u = sh.eoff[tid]; u < sh.eoff[tid + 1]; ++u) {
+            const int4 r = sh.erow[u];
+            if (r.x >= c) break;  // ascending; slot < win_hi[c - 1] <=> applied from a pod < c
+            d0 += use64(r.y); d1 += use64(r.z); d2 += use64(r.w); d3 += 1;
         }
-        a.e_idx[n] = -1;
+        if (d3) {  // (no other thread touches the node: fire-and-forget atomics, no read back)
+            atomicAdd((unsigned long long*)&a.s.rc[n], (unsigned long long)-d0);
+            atomicAdd((unsigned long long*)&a.s.rm[n], (unsigned long long)-d1);
+            atomicAdd((unsigned long long*)&a.s.rg[n], (unsigned long long)-d2);
+            atomicAdd((unsigned long long*)&a.s.nr[n], (unsigned long long)-d3);
+        }
     }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)  // every E node's index mark
+        if (tid + q * kThreads < n_eall) a.e_idx[enode[q]] = -1;
 #pragma unroll
     for (int q = 0; q < 2; ++q)
         if (tid + q * kThreads < nlo) a.n_slot[snd[q]] = -1;
@@ -1028,11 +1029,7 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
         __syncthreads();
         for (int k = tid; k < ncid; k += kThreads)
             if (sh.fhead[k] >= 0) wo.touched[atomicAdd(&sh.nbc, 1)] = sh.cnode[k];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int k = tid + q * kThreads;
-            if (k < n_e && sh.eoff[k + 1] > sh.eoff[k]) wo.touched[atomicAdd(&sh.nbc, 1)] = enode[q];
-        }
+        if (tid < n_e) wo.touched[atomicAdd(&sh.nbc, 1)] = enode[0];  // (every slot-E node has slots)
         __syncthreads();
         if (tid == 0) wo.n_touched = sh.nbc;
     }
@@ -1082,6 +1079,10 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
 // pod group) items at a time, one per 256-thread half, items w, w + W, ... of the batch's
 // block-major item list.  The scan reads node records the resolver may be committing: only
 // nodes the batch touches, which the next batch re-evaluates (ks_cand.hip window_prep_kernel).
+// (Leaving the batch's candidate slots out of these lists, so that the next batch's top-L holds no
+// node the batch could bind, was measured worse: those nodes then all join the next batch's E,
+// enough of them reach its lists' thresholds to overflow the candidate slots, and the batches
+// commit ~104 pods instead of ~181.)
 template <int kMode>
 __global__ __launch_bounds__(kThreads) void chunk_scan_kernel(const EngineArgs* __restrict__ A,
                                                               const EngineArgs* __restrict__ As) {

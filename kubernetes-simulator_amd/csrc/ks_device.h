@@ -553,12 +553,12 @@ constexpr int kWinSlots = 512;
 constexpr int kChR = 24;    // static candidates kept per pod
 constexpr int kRecDw = 20;  // a candidate node's record, dwords (the widest format: ten int64, ks_cand.hip)
 constexpr int kSlotMax = 1536;  // distinct candidate nodes per batch (the sequential resolver's slots)
-constexpr int kEMax = 1024;     // E nodes per batch: the window's expiry nodes + the overlap's touched nodes
+constexpr int kEMax = 2048;     // E nodes per batch: the window's expiry nodes + the overlap's touched nodes
 constexpr int kTouchMax = kWinMaxB + kWinSlots;
 constexpr int kSpecStride = 8;  // int64 counters per speculative set  // nodes a batch changes: its binds + its window's expiry nodes
 enum : int32_t { kClTrunc = 1 << 8, kClFull = 1 << 9, kClOvf = 1 << 10 };
 struct WinWS {
-    int32_t nb, e_cnt, n_e, pad_;
+    int32_t nb, e_cnt, n_e, n_es;         // E nodes; the first n_es have window slots (<= kWinSlots)
     int32_t win_hi[kWinMaxB];             // pod i: expiry slots < win_hi[i] are applied before it binds
     int32_t own[kWinMaxB];                // pod i's own expiry slot in the window, or -1
     int32_t ex_q[kWinSlots];              // slot -> expiring pod
@@ -567,7 +567,7 @@ struct WinWS {
     // E: the distinct nodes of the pre-batch expiries, then (overlapped scan) the nodes changed since
     // the scan read the node table, with no slots
     int32_t e_node[kEMax];
-    int32_t e_off[kEMax + 1];             // E node k's slots: e_slot[e_off[k] .. e_off[k+1]) ascending
+    int32_t e_off[kWinSlots + 1];         // E node k < n_es: its slots e_slot[e_off[k] .. e_off[k+1]) ascending
     int32_t e_slot[kWinSlots];
     // pod i's static candidates, sorted descending
     uint64_t cl_key[kWinMaxB][kChR];

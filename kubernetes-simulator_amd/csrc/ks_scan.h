@@ -22,9 +22,11 @@ __device__ __forceinline__ int popc_below(uint64_t mask, int lane) { return __po
 // threads lt = 0..255 of one group; kv: the group's [PG][256] table.  has == false: this group has
 // no item this round — it only takes part in the workgroup barrier (one, between the evaluation
 // and the extraction; the caller separates items by another).
+// excl (nullable): nodes with excl[n] >= 0 are left out of the lists (the overlap's speculative
+// scan: the current batch's candidate slots, which join the next batch's E instead)
 template <int kMode, typename KT>
 __device__ __forceinline__ void scan_item(const EngineArgs& a, KT* kv, int64_t start, int64_t nb, int groups, int64_t it,
-                                          bool has, int lt) {
+                                          bool has, int lt, const int32_t* excl = nullptr) {
     const int lane = lt & (kWave - 1), wave = lt >> 6;
     int pg0 = 0, np = 0, blk = 0;
     uint32_t blk_base = 0;
@@ -34,9 +36,10 @@ __device__ __forceinline__ void scan_item(const EngineArgs& a, KT* kv, int64_t s
         blk = a.blk_lo + bx;
         blk_base = (uint32_t)blk * kNodes;
         const int64_t node = (int64_t)blk_base + lt;
-        const bool valid = node < a.c.n_nodes;
+        bool valid = node < a.c.n_nodes;
         NodeV n{};
         if (node < (int64_t)a.c.nwb * kWave) n = load_node(a.s, node);
+        if (excl && valid && excl[node] >= 0) valid = false;
         np = (int)min<int64_t>(a.PG, nb - pg0);
         const PodRec* pp = a.pods + start + pg0;
         int b = 0;
