@@ -132,7 +132,8 @@ def stream_copy_gbs(device: int, mib: int = 2048, reps: int = 10):
 # chain: expire_head -> scan -> merge -> resolve_kernel
 BATCH_KERNELS = {"ks::expire_head_kernel": "expire_head", "ks::sq::window_prep_kernel": "expire_head",
                  "ks::scan_kernel": "scan", "ks::merge_kernel": "merge", "ks::sq::merge_cl_kernel": "merge",
-                 "ks::resolve_kernel": "resolve", "ks::chk::resolve_chunk_kernel": "resolve"}
+                 "ks::resolve_kernel": "resolve", "ks::chk::resolve_chunk_kernel": "resolve",
+                 "ks::chk::chunk_scan_kernel": "resolve"}  # (the resolver with the next batch's scan fused in)
 
 
 def load_traffic(config: str = "c3"):

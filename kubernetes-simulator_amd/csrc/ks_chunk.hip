@@ -1076,7 +1076,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
 // The chunk kernel with the next batch's scan fused in (the overlap on one stream): workgroup 0
 // resolves the batch; the others — one per CU, the resolver's LDS footprint fixes that — scan the
 // speculative pods (As: counters window prep wrote) in the resolver's LDS image, two (node block,
-// pod group) items at a time, one per 256-thread half, items w, w + W, ... of the batch's
+// pod group) items at a time, one per 256-thread half, from its XCD's share of the batch's
 // block-major item list.  The scan reads node records the resolver may be committing: only
 // nodes the batch touches, which the next batch re-evaluates (ks_cand.hip window_prep_kernel).
 // (Leaving the batch's candidate slots out of these lists, so that the next batch's top-L holds no
@@ -1100,11 +1100,16 @@ __global__ __launch_bounds__(kThreads) void chunk_scan_kernel(const EngineArgs* 
     const int64_t tot = (int64_t)a.blk_n * groups;
     const int half = threadIdx.x / scn::kNodes, lt = threadIdx.x % scn::kNodes;
     uint16_t* kv = reinterpret_cast<uint16_t*>(&sh) + (size_t)half * a.PG * scn::kNodes;
-    const int64_t W = 2 * ((int64_t)gridDim.x - 1), w = 2 * ((int64_t)blockIdx.x - 1);
-    for (int64_t r = w; r < tot; r += W) {  // (uniform: r is the workgroup's first item this round)
-        if (r != w) __syncthreads();         // the previous round's extraction has read kv
+    // XCD-aware deal (blocks b and b + 8 share an XCD): XCD x = b % 8 takes the contiguous item
+    // range [x per, (x + 1) per) — whole node blocks with their pod groups — shared by its
+    // workgroups, so a node block's records come from HBM once and from that XCD's L2 after
+    const int x = (int)(blockIdx.x % 8), j = (int)(blockIdx.x / 8) - (x == 0 ? 1 : 0);  // (block 0: the resolver)
+    const int nx = (int)((gridDim.x - x + 7) / 8) - (x == 0 ? 1 : 0);                  // workgroups of XCD x
+    const int64_t per = (tot + 7) / 8, lo = x * per, hi = min<int64_t>(tot, lo + per);
+    for (int64_t r = lo + 2 * (int64_t)j; r < hi; r += 2 * (int64_t)nx) {  // (uniform per workgroup)
+        if (r != lo + 2 * (int64_t)j) __syncthreads();  // the previous round's extraction has read kv
         const int64_t it = r + half;
-        scn::scan_item<kMode, uint16_t>(a, kv, start, nb, groups, it, it < tot, lt);
+        scn::scan_item<kMode, uint16_t>(a, kv, start, nb, groups, it, it < hi, lt);
     }
 }
 static_assert(sizeof(ChShared) >= 2 * kMaxPGScan * scn::kNodes * sizeof(uint16_t), "two 16-bit key tables");

@@ -1122,7 +1122,7 @@ static ks_status ensure_window_ws(ks_engine* e) {
         // footprint allows one workgroup per CU)
         int cus = 0;
         HIPCHK(e, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device));
-        e->scan_workers = std::max(1, cus - 1);
+        e->scan_workers = std::max(15, cus - 1);  // (>= 15: every XCD deals its share to at least one)
     }
     return KS_OK;
 }
