@@ -222,36 +222,29 @@ __device__ __forceinline__ void put_rec(uint32_t* o, const NodeV& v) {
     o[8] = (uint32_t)v.taint; o[9] = (uint32_t)(v.taint >> 32); o[10] = (uint32_t)v.label; o[11] = (uint32_t)(v.label >> 32);
 }
 
+// E-node keys per merge_cl thread (E node tid + q * threads)
+constexpr int kEPer = kEMax / 256;
+
 // Pod i's static candidates from its merged top-L `cand` (LDS or global), by one workgroup: the
-// kept entries (sorted, <= kR) with their slots
+// kept entries (sorted, <= kR) with their slots.  ek: this thread's E-node keys (computed before
+// the merge, so their dependent reads overlap the block lists'), 0 = none.
 template <int kMode>
-__device__ __forceinline__ void cand_list(const EngineArgs& a, WinWS& ws, int i, const uint64_t* cand) {
-    const int tid = threadIdx.x, nthr = blockDim.x;
-    const int64_t start = a.ctr[kCtrStart];
+__device__ __forceinline__ void cand_list(const EngineArgs& a, WinWS& ws, int i, const uint64_t* cand,
+                                          const uint64_t (&ek)[kEPer]) {
+    const int tid = threadIdx.x;
     __shared__ uint64_t buf[kClBuf];
     __shared__ int cnt;
     if (tid == 0) cnt = 0;
     __syncthreads();
-    const PodRec p = a.pods[start + i];
     const uint64_t last = cand[kL - 1];
     const bool full = last != 0;
     const uint64_t thr = full ? last : 1ull;
-    const int hi = ws.win_hi[i], n_e = ws.n_e, n_es = ws.n_es;
-    for (int k = tid; k < n_e; k += nthr) {
-        const int32_t n = ws.e_node[k];
-        NodeV v = load_node(a.s, n);
-        const int ue = k < n_es ? ws.e_off[k + 1] : 0;
-        for (int u = k < n_es ? ws.e_off[k] : 0; u < ue; ++u) {
-            const int x = ws.e_slot[u];
-            if (x >= hi) break;  // ascending
-            v.rc -= ws.ex_req[x][0]; v.rm -= ws.ex_req[x][1]; v.rg -= ws.ex_req[x][2]; v.nr -= 1;
-        }
-        const uint64_t key = make_key(eval_t<kMode>(a.c, p, v), (uint32_t)n);
-        if (key >= thr) {
+#pragma unroll
+    for (int q = 0; q < kEPer; ++q)
+        if (ek[q] != 0 && ek[q] >= thr) {
             const int pos = atomicAdd(&cnt, 1);
-            if (pos < kClBuf) buf[pos] = key;
+            if (pos < kClBuf) buf[pos] = ek[q];
         }
-    }
     if (tid < kL) {
         const uint64_t x = cand[tid];
         if (x != 0 && a.e_idx[key_node(x)] < 0) {
@@ -274,6 +267,11 @@ __device__ __forceinline__ void cand_list(const EngineArgs& a, WinWS& ws, int i,
         const bool valid = lane < (n < kR ? n : kR);
         const uint64_t me = valid ? kept[lane] : 0ull;
         const int32_t nd = key_node(me);
+        // the record and E index read before the claim (a claimer needs them; the reads overlap
+        // the claim's round trip)
+        NodeV rec{};
+        int32_t eix = -1;
+        if (valid) { rec = load_node(a.s, nd); eix = a.e_idx[nd]; }
         int sl = valid ? atomicCAS(&a.n_slot[nd], -1, kSlotPending) : 0;
         const bool claim = valid && sl == -1;
         const uint64_t cm = __ballot(claim);
@@ -287,8 +285,8 @@ __device__ __forceinline__ void cand_list(const EngineArgs& a, WinWS& ws, int i,
             sl = base + __popcll(cm & ((1ull << lane) - 1ull));
             ws.slot_node[sl] = nd;
             if (sl < kSlotMax) {
-                put_rec(ws.slot_rec[sl], load_node(a.s, nd));
-                ws.slot_eix[sl] = a.e_idx[nd];
+                put_rec(ws.slot_rec[sl], rec);
+                ws.slot_eix[sl] = eix;
             }
             atomicExch(&a.n_slot[nd], sl);
         }
@@ -336,7 +334,42 @@ __global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs* __rest
     for (int k = 0; k < kL; ++k) top[k] = 0;
     const uint64_t* lists = src + (int64_t)b * pod_stride;
     const int nthr = blockDim.x, nwav = nthr / kWave;
-    for (int blk = tid; blk < nl; blk += nthr) {
+    // independent reads first: this thread's first block list, then the E nodes' keys (dependent
+    // chains: node, slots, expiring requests) while it is in flight
+    uint64_t lv0[kL];
+    const bool has0 = tid < nl;
+    {
+        const ulonglong2* lp = reinterpret_cast<const ulonglong2*>(lists + (int64_t)(has0 ? tid : 0) * list_stride);
+#pragma unroll
+        for (int k = 0; k < kL / 2; ++k) {
+            const ulonglong2 w = has0 ? lp[k] : make_ulonglong2(0, 0);
+            lv0[2 * k] = w.x;
+            lv0[2 * k + 1] = w.y;
+        }
+    }
+    uint64_t ek[kEPer];
+    {
+        const int64_t start = a.ctr[kCtrStart];
+        const PodRec p = a.pods[start + b];
+        const int hi = ws.win_hi[b], n_e = ws.n_e, n_es = ws.n_es;
+#pragma unroll
+        for (int q = 0; q < kEPer; ++q) {
+            const int k = tid + q * nthr;
+            ek[q] = 0;
+            if (k >= n_e) continue;
+            const int32_t n = ws.e_node[k];
+            NodeV v = load_node(a.s, n);
+            const int ue = k < n_es ? ws.e_off[k + 1] : 0;
+            for (int u = k < n_es ? ws.e_off[k] : 0; u < ue; ++u) {
+                const int x = ws.e_slot[u];
+                if (x >= hi) break;  // ascending
+                v.rc -= ws.ex_req[x][0]; v.rm -= ws.ex_req[x][1]; v.rg -= ws.ex_req[x][2]; v.nr -= 1;
+            }
+            ek[q] = make_key(eval_t<kMode>(a.c, p, v), (uint32_t)n);
+        }
+    }
+    if (has0) topl_insert(top, lv0);
+    for (int blk = tid + nthr; blk < nl; blk += nthr) {
         const ulonglong2* lp = reinterpret_cast<const ulonglong2*>(lists + (int64_t)blk * list_stride);
         uint64_t lv[kL];
 #pragma unroll
@@ -375,7 +408,7 @@ __global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs* __rest
         }
     }
     __syncthreads();
-    cand_list<kMode>(a, ws, b, pc);
+    cand_list<kMode>(a, ws, b, pc, ek);
 }
 
 }  // namespace sq
@@ -388,6 +421,7 @@ hipError_t launch_window_prep(const EngineArgs* d, bool head, bool spec, int slo
 
 hipError_t launch_merge_cl(const EngineArgs* d, int mode, int B, const uint64_t* lists, int64_t pod_stride,
                            int32_t nl, int64_t list_stride, int nl_max, hipStream_t st) {
+    static_assert(sq::kEPer * 256 >= kEMax, "E keys per thread at 256 threads");
     const dim3 g(B), t(nl_max > 1024 ? 1024 : 256);
     switch (mode) {
         case kEvalMicro: hipLaunchKernelGGL(sq::merge_cl_kernel<kEvalMicro>, g, t, 0, st, d, lists, pod_stride, nl, list_stride); break;
