@@ -628,8 +628,8 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
             const uint64_t below = (1ull << lane) - 1ull;
             // the lane's entries no pre-chunk bind took, in list order (static in the chunk): the
             // list in the cache phase's (idle) buffer, its first eight in registers
-            int16_t* al = reinterpret_cast<int16_t*>(&sh.x.k[0][0][0]) + lane * kR;
-            static_assert(sizeof(sh.x.k) >= kC * kR * sizeof(int16_t), "avail lists");
+            uint32_t* al = reinterpret_cast<uint32_t*>(&sh.x.k[0][0][0]) + lane * kR;
+            static_assert(sizeof(sh.x.k) >= kC * kR * sizeof(uint32_t), "avail lists");
             int na = 0;
             {
                 uint32_t e[kR];
@@ -643,36 +643,56 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
                 for (int r = 0; r < kR; ++r) fh[r] = sh.fhead[r < nc ? (e[r] >> 16) : 0];
 #pragma unroll
                 for (int r = 0; r < kR; ++r) {  // compacted without branches
-                    al[na] = (int16_t)(e[r] >> 16);
+                    al[na] = e[r];
                     na += (r < nc && fh[r] < 0) ? 1 : 0;
                 }
             }
             static_assert(kR % 4 == 0 && kR > 8, "entry rows in 16-byte reads; two probe stages");
             int rg[kR];
+            uint32_t rt[kR];  // (cid, total) words
 #pragma unroll
-            for (int q = 0; q < kR; ++q) rg[q] = q < na ? al[q] : 0;
+            for (int q = 0; q < kR; ++q) {
+                rt[q] = q < na ? al[q] : 0u;
+                rg[q] = (int)(rt[q] >> 16);
+            }
+            // the guess also takes the pod's cached pre-chunk D (the best node bound before the
+            // chunk, on its replayed state) when it beats the static pick — fewer full sweeps
+            // correct it (the guess only seeds the sweeps: any guess gives the sequential result)
+            const bool dok = c0 > 0 && i < c1 && !sh.cdbad[lane];
+            const uint64_t d1 = dok ? sh.cd1[lane] : 0ull, d2 = dok ? sh.cd2[lane] : 0ull;
+            const int dc1 = d1 ? sh.cd1c[lane] : 0, dc2 = d2 ? sh.cd2c[lane] : 0;
             int cur = -1, lo_l = 0;
             for (;;) {
                 DG(++n_sonly;)
                 const bool act = lane >= lo_l && nc > 0;
                 int nw = act ? -1 : cur;
+                uint32_t nwt = 0;
+                uint64_t m1, m2;
                 {  // probe the first eight (every lane, unconditional loads), then the rest if needed
                     uint64_t cm[8];
 #pragma unroll
                     for (int q = 0; q < 8; ++q) cm[q] = sh.cmask[rg[q]];
+                    m1 = sh.cmask[dc1]; m2 = sh.cmask[dc2];
 #pragma unroll
                     for (int q = 7; q >= 0; --q)  // the lowest free entry wins
-                        if (act && q < na && (cm[q] & below) == 0) nw = rg[q];
+                        if (act && q < na && (cm[q] & below) == 0) { nw = rg[q]; nwt = rt[q]; }
                 }
                 if (__ballot(act && nw < 0 && na > 8)) {
                     uint64_t cm[kR - 8];
 #pragma unroll
                     for (int q = 8; q < kR; ++q) cm[q - 8] = sh.cmask[rg[q]];
                     int nw2 = -1;
+                    uint32_t nwt2 = 0;
 #pragma unroll
                     for (int q = kR - 1; q >= 8; --q)
-                        if (q < na && (cm[q - 8] & below) == 0) nw2 = rg[q];
-                    if (act && nw < 0) nw = nw2;
+                        if (q < na && (cm[q - 8] & below) == 0) { nw2 = rg[q]; nwt2 = rt[q]; }
+                    if (act && nw < 0) { nw = nw2; nwt = nwt2; }
+                }
+                if (act && d1) {
+                    const uint64_t dk = !(m1 & below) ? d1 : ((d2 && !(m2 & below)) ? d2 : 0ull);
+                    const int dc = !(m1 & below) ? dc1 : dc2;
+                    const uint64_t sk = nw >= 0 ? cl_key(sh, nwt) : 0ull;
+                    if (dk > sk) nw = dc;
                 }
                 const bool ch = nw != cur;
                 const uint64_t chm = __ballot(ch);
