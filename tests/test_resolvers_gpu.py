@@ -97,3 +97,47 @@ def test_chunk_decimal_memory_class():
     tr = tracegen.c3q_trace(n_nodes=2000, n_pods=8000)
     assert int(np.max(tr["nodes"]["alloc"][:, 1])) == 512 * (1 << 30) * 1000  # 512Gi: 2^31 after the gcd
     _run(tr, "feeds_all_lrba", 8000, 0, 0, (2500, 5500))
+
+
+# ---- the overlap (next batch's scan fused into the chunk kernel, ks_engine.cpp step loop) ------
+def _engine_env(tr, enc, mode, overlap, **kw):
+    import os
+    old = os.environ.get("KS_OVERLAP")
+    os.environ["KS_OVERLAP"] = "1" if overlap else "0"  # read once, at engine creation
+    try:
+        return make_engine(tr, enc, mode, **kw)
+    finally:
+        if old is None:
+            del os.environ["KS_OVERLAP"]
+        else:
+            os.environ["KS_OVERLAP"] = old
+
+
+@pytest.mark.parametrize("case", ["c2", "dense_expiries"])
+def test_overlap_on_and_off_bind_identically_and_match_oracle(case):
+    """The speculative lists (stale for the nodes the previous batch touched, which join E) and
+    the conditional rescan after early stops: the overlapped chain gives the plain chain's binds,
+    statuses and usage, and the oracle's."""
+    if case == "c2":
+        tr = tracegen.c2_trace(n_pods=12_000)
+        mode, ticks, chunks = "feeds_all_lrba", 12_000, (5000, 7000)
+    else:
+        tr = small_trace(11, n_nodes=2000, n_pods=6000, taints=False, selectors=False, tolerations=False)
+        tr["pods"]["phase_sec"][:] = 1 + (np.arange(len(tr["pods"]["phase_sec"])) % 12)
+        mode, ticks, chunks = "feeds_all_lrba", 6000, (1500,) * 4
+    enc = encoded(tr)
+    ora = make_oracle(tr, mode)
+    ora.submit(tr)
+    ob, orc = oracle_run(ora, ticks)
+    assert orc == 0
+    for overlap in (False, True):  # (the chunk resolver forced: these clusters are the small class)
+        eng = _engine_env(tr, enc, mode, overlap, batch_pods=192, engine_flags=RESOLVERS["chunk"])
+        eng.submit(enc["pods"])
+        got = []
+        for c in chunks:
+            eb, erc = engine_run(eng, c, c)
+            got.append(eb)
+            assert erc == 0
+        assert_same_binds(np.concatenate(got), ob)
+        np.testing.assert_array_equal(eng.usage(), ora.usage())
+        eng.close()
