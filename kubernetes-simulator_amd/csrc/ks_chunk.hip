@@ -40,6 +40,7 @@ constexpr int kSeg = 5;         // stored state segments per replayed node withi
 constexpr int kPend = 4;        // pending own expiries per replayed node
 constexpr int kWaves = kThreads / kWave;
 constexpr int16_t kNoSeg = INT16_MAX;
+constexpr int kNoOwn = 0x7FFF;  // (brow: no own expiry in the window)
 constexpr int kMOvf = kSeg, kMCid = kSeg + 1;
 static_assert(kSeg + 2 <= 8, "slot row");
 static_assert(kB <= 256 && kB % kC == 0, "chunks of one wave");
@@ -146,6 +147,8 @@ struct ChShared {
         uint64_t k[kWaves][kC][2];
         int16_t c[kWaves][kC][2];  // k[.][.][1] == ~0: the lane met an unknown state
     } x;
+    uint32_t brow[kC][4];         // chunk pod c0 + r: request words (saturated), key mask | run << 3 |
+                                  // own expiry's pod (kNoOwn: none) << 16
     int16_t ceix[kCid];           // cid -> the node's index in E, -1 if not an E node
     int16_t e2c[kSlots];          // slot-E index -> cid, -1: the E node is no candidate of this batch
     int32_t nbc, cut, fc[2], fs[2];
@@ -257,22 +260,35 @@ __device__ __forceinline__ Replayed replay(ChShared& sh, int k, int tb, bool chu
         const bool fin = j >= 0;
         if (fin) j = sh.fnext[j];
         else m &= m - 1;
-        const PodRec& p = sh.pod[jb];
+        // the bind's request words, key mask, run flag and own-expiry pod: a chunk bind's from its
+        // 16-byte row (one read), a final bind's from the pod record
+        uint32_t q0, q1, q2, meta;
+        if (!fin) {
+            const uint4 br = *reinterpret_cast<const uint4*>(&sh.brow[jb - c0][0]);
+            q0 = br.x; q1 = br.y; q2 = br.z; meta = br.w;
+        } else {
+            const PodRec& p = sh.pod[jb];
+            q0 = (uint32_t)p.req[0]; q1 = (uint32_t)p.req[1]; q2 = (uint32_t)p.req[2];
+            const int x = sh.own[jb];
+            meta = (uint32_t)p.keymask | ((sh.clfl[jb] & kFlRun) ? 8u : 0u) |
+                   ((uint32_t)(x >= 0 ? (int)sh.xeff[x] : kNoOwn) << 16);
+        }
         bool ok;
         if (fin) {
             ok = sh.adm[jb] == 1;
-        } else {  // CreatePod admission (kubesim/node/node.go:44-47)
+        } else {  // CreatePod admission (kubesim/node/node.go:44-47); saturated words: a request
+                  // >= 2^32 - 1 exceeds every capacity (< 2^32 - 1) as its int64 value would
             ok = !lost && vnr < ap;
-            if (p.keymask & 1) ok &= (int64_t)vrc + p.req[0] <= ac64;
-            if (p.keymask & 2) ok &= (int64_t)vrm + p.req[1] <= am64;
-            if (p.keymask & 4) ok &= (int64_t)vrg + p.req[2] <= ag64;
+            if (meta & 1) ok &= (int64_t)vrc + q0 <= ac64;
+            if (meta & 2) ok &= (int64_t)vrm + q1 <= am64;
+            if (meta & 4) ok &= (int64_t)vrg + q2 <= ag64;
             sh.adm[jb] = lost ? 2 : (ok ? 1 : 0);
         }
-        if (ok && (sh.clfl[jb] & kFlRun)) {
-            vrc += (uint32_t)p.req[0]; vrm += (uint32_t)p.req[1]; vrg += (uint32_t)p.req[2]; vnr += 1;
+        if (ok && (meta & 8)) {
+            vrc += q0; vrm += q1; vrg += q2; vnr += 1;
             KS_STORE(jb + 1);
-            const int x = sh.own[jb];
-            if (x >= 0) KS_PUSH(sh.xeff[x], jb);
+            const int oe = (int)(meta >> 16);
+            if (oe != kNoOwn) KS_PUSH(oe, jb);
         }
     }
 #undef KS_STORE
@@ -617,6 +633,16 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
 
         // (2) sweeps
         DG(uint64_t t1 = dstamp(); acc_cd += t1 - t0;)
+        if (wave == 1 && c0 + lane < c1) {  // the chunk's bind rows (beside the guess in wave 0)
+            const int i = c0 + lane;
+            const PodRec& p = sh.pod[i];
+            const int x = sh.own[i];
+            auto word = [](int64_t q) { return (uint32_t)(q < 0xFFFFFFFFll ? q : 0xFFFFFFFFll); };
+            *reinterpret_cast<uint4*>(&sh.brow[lane][0]) =
+                make_uint4(word(p.req[0]), word(p.req[1]), word(p.req[2]),
+                           (uint32_t)p.keymask | ((sh.clfl[i] & kFlRun) ? 8u : 0u) |
+                               ((uint32_t)(x >= 0 ? (int)sh.xeff[x] : kNoOwn) << 16));
+        }
         // (2a) The guess: exclusion-only rounds (w_i = the first static candidate no earlier pod
         // takes; no evaluation, no replay) to their fixed point — the sequential greedy over the
         // lists, without the piles a cold start makes (every pod on its own best node).  One wave,
