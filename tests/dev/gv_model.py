@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--skip", type=int, default=8000)
     ap.add_argument("--L", type=int, default=8)
     ap.add_argument("--chunks", default="256,64,32")
+    ap.add_argument("--guess", default="none", help="none | excl | dx (chunk seeds, as the kernel's guess)")
+    ap.add_argument("--T", type=int, default=3, help="dx: taken entries evaluated per pod")
     a = ap.parse_args()
     tr = tracegen.c3_trace(n_nodes=a.nodes, n_pods=a.pods)
     enc = encode.encode_trace(tr)
@@ -193,6 +195,65 @@ def main():
 
         nd = sum(1 for i in range(B) if f_at(truth, i, {int(x): int(np.nonzero(truth == x)[0][0]) for x in truth}, states(truth))[1])
         dwins.append(nd)
+        def guess(w, c0, c1):
+            """the kernel's chunk guess: exclusion rounds (+ pre-chunk D; dx: + in-chunk D, approx)"""
+            pre = set(int(x) for x in w[:c0] if x >= 0)
+            wp = w.copy()
+            wp[c0:] = -1
+            stp = states(wp)
+            cd = []
+            for i in range(c0, c1):
+                ks = sorted(((key1(s0 + i, n, stp[n][i]), n) for n in pre), reverse=True)[:2]
+                cd.append([(k, n) for k, n in ks if k > 0])
+            al = [[(k, x) for k, x in cl[i] if x not in pre] for i in range(c0, c1)]
+            base = {}
+
+            def approx(i, n, binders):
+                s = (stp[n][i] if n in stp else e_state(n, i)).copy()  # expiries by pod i's tick
+                for j in binders:
+                    s[:3] += req[s0 + j]
+                    s[3] += 1
+                return key1(s0 + i, n, s)
+
+            C = c1 - c0
+            cur = [-1] * C
+            lo = 0
+            while True:
+                nwv = list(cur)
+                for li in range(lo, C):
+                    i = c0 + li
+                    taken = {}
+                    for lj in range(li):
+                        if cur[lj] >= 0:
+                            taken.setdefault(cur[lj], []).append(c0 + lj)
+                    sk, nw = 0, -1
+                    cands = []
+                    for k, x in al[li]:
+                        if x not in taken:
+                            sk, nw = k, x
+                            break
+                        cands.append(x)
+                    best = sk
+                    d = [(k, n) for k, n in cd[li] if n not in taken]
+                    if d and d[0][0] > best:
+                        best, nw = d[0]
+                    if a.guess == "dx":
+                        ex = cands[:a.T]
+                        if cd[li] and cd[li][0][1] in taken:
+                            ex.append(cd[li][0][1])
+                        for x in ex:
+                            k = approx(i, x, taken[x])
+                            if k > best:
+                                best, nw = k, x
+                    nwv[li] = nw
+                ch = [li for li in range(C) if nwv[li] != cur[li]]
+                cur = nwv
+                if not ch:
+                    break
+                lo = ch[0] + 1
+            return np.array(cur)
+
+        sweeps_g = []
         for C in chunks:
             w = np.full(B, -1)
             sweeps = pairs = 0
@@ -201,6 +262,23 @@ def main():
                 # cached contribution of nodes bound before the chunk: one pass per chunk
                 pairs += (c1 - c0) * len(set(w[:c0].tolist()))
                 lo = c0  # pods >= lo are recomputed
+                if a.guess != "none":
+                    w[c0:c1] = guess(w, c0, c1)
+                    if os.environ.get("GV_DEBUG"):
+                        pre = set(int(x) for x in truth[:c0])
+                        for i in range(c0, c1):
+                            if w[i] != truth[i]:
+                                tn = int(truth[i])
+                                print(f"  miss pod {i}: guess {w[i]} truth {tn} pre {tn in pre} "
+                                      f"in-chunk-before {tn in set(truth[c0:i].tolist())} in cl {tn in [x for _, x in cl[i]]} "
+                                      f"cl rank {[x for _, x in cl[i]].index(tn) if tn in [x for _, x in cl[i]] else -1}")
+                                stt_t = states(truth)
+                                print(f"    true key {key1(s0+i, tn, stt_t[tn][i]) >> 32} snap key {key1(s0+i, tn, snap[:, tn]) >> 32} "
+                                      f"guess-node true key {key1(s0+i, int(w[i]), stt_t[int(w[i])][i]) >> 32 if int(w[i]) in stt_t else key1(s0+i, int(w[i]), e_state(int(w[i]), i)) >> 32} "
+                                      f"binders {[j for j in range(c0, i) if truth[j] == tn]} guess binders {[j for j in range(c0, i) if w[j] == tn]} "
+                                      f"cl {[(k >> 32, x) for k, x in cl[i][:6]]}")
+                                break
+                    sweeps_g.append(0)
                 while True:
                     first = {}
                     for i, x in enumerate(w[:c1]):
@@ -212,6 +290,8 @@ def main():
                         nw[i] = f_at(w, i, first, stt)[0]
                         pairs += sum(1 for n, fi in first.items() if c0 <= fi < i)
                     sweeps += 1
+                    if a.guess != "none":
+                        sweeps_g[-1] += 1
                     ch = np.nonzero(nw[c0:c1] != w[c0:c1])[0]
                     w = nw
                     if len(ch) == 0:
@@ -220,12 +300,16 @@ def main():
             assert (w == truth).all(), "fixed point differs from the sequential result"
             res[C]["sweeps"].append(sweeps)
             res[C]["pairs"].append(pairs)
+            res[C].setdefault("per_chunk", []).extend(sweeps_g)
+            sweeps_g.clear()
         print(f"batch {b}: E {len(E)}, rebinds {rebinds[-1]}, D wins {dwins[-1]}, " +
               ", ".join(f"C={C}: {res[C]['sweeps'][-1]} sweeps {res[C]['pairs'][-1]} pairs" for C in chunks), flush=True)
     cl = np.array(clen)
     print(f"cl length mean {cl.mean():.1f} p99 {np.percentile(cl, 99):.0f} max {cl.max()}; rebinds/batch {np.mean(rebinds):.1f}; D wins/batch {np.mean(dwins):.1f}")
     for C in chunks:
-        print(f"C={C}: sweeps/batch {np.mean(res[C]['sweeps']):.1f}, D pairs/batch {np.mean(res[C]['pairs']):.0f}")
+        pc = res[C].get("per_chunk", [])
+        print(f"C={C}: sweeps/batch {np.mean(res[C]['sweeps']):.1f}, D pairs/batch {np.mean(res[C]['pairs']):.0f}" +
+              (f", full sweeps per chunk {np.mean(pc):.2f} (hist {np.bincount(pc).tolist()})" if pc else ""))
 
 
 if __name__ == "__main__":
