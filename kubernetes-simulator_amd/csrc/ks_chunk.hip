@@ -95,6 +95,12 @@ __device__ __forceinline__ uint32_t eval32(const Cfg& c, const PodRec& p, const 
     if constexpr (kMode == kEvalWide) return eval_t<kEvalWide>(c, p, wide_node(n));
     else return eval_t<kMode>(c, p, n);
 }
+template <int kMode>
+__device__ __forceinline__ PruneF prune32(const Cfg& c, const NS32& n) {
+    if constexpr (kMode == kEvalWide) return prune_prep(c, wide_node(n));
+    else return prune_prep_t<kMode>(c, n);
+}
+
 __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
     const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
     const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
@@ -344,6 +350,26 @@ __device__ __forceinline__ uint32_t tot_at(const EngineArgs& a, const ChShared& 
     return eval32<kMode>(a.c, p, n);
 }
 
+// The same, 0 when the float upper bound of the total (prune_tmax: filters ignored, exact slack)
+// says the key stays below lb — most (pod, node) pairs: the full evaluator runs only for the rest.
+template <int kMode>
+__device__ __forceinline__ uint64_t key_at_lb(const EngineArgs& a, const ChShared& sh, const PodRec& p, int i, int k,
+                                              int sl, const SRow& r, uint64_t lb) {
+    int s = 0;
+#pragma unroll
+    for (int q = 1; q < kSeg; ++q) s += r.m(q) <= i;
+    const int4 st = *reinterpret_cast<const int4*>(&sh.sst[sl][s][0]);
+    NS32 n;
+    n.ac = sh.rs[0][k]; n.am = sh.rs[1][k]; n.ag = sh.rs[2][k]; n.ap = sh.rs[3][k];
+    n.rc = st.x; n.rm = st.y; n.rg = st.z; n.nr = st.w;
+    const uint32_t node = (uint32_t)sh.cnode[k];
+    n.taint = 0; n.label = 0;
+    const PruneF f = prune32<kMode>(a.c, n);
+    if (!f.live || make_key(prune_tmax(a.c, f, (float)p.req[0], (float)p.req[1]) + 1u, node) < lb) return 0;
+    n.taint = sh.rt[k]; n.label = sh.rl[k];
+    return make_key(eval32<kMode>(a.c, p, n), node);
+}
+
 __device__ __forceinline__ uint64_t cl_key(const ChShared& sh, uint32_t e) {
     return ((uint64_t)(e & 0xFFFFu) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)sh.cnode[e >> 16]);
 }
@@ -573,10 +599,13 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
                         const int k = r[q].m(kMCid);
                         if (k < 0 || !li) continue;
                         if (r[q].m(kMOvf) <= i) { bad = true; continue; }
-                        // (the exact key always: a float-bound prune first saved nothing — in
+                        // the exact key (keys below lbc dropped); the wide evaluator first tries
+                        // the float bound — for the 32-bit evaluators the prune saved nothing: in
                         // SIMT the evaluation runs whenever one lane passes, and these nodes, the
-                        // batch's earlier winners, are near the top of most pods' lists)
-                        uint64_t key = key_at<kMode>(a, sh, p, i, k, j, r[q]);
+                        // batch's earlier winners, are near the top of most pods' lists
+                        uint64_t key;
+                        if constexpr (kMode == kEvalWide) key = key_at_lb<kMode>(a, sh, p, i, k, j, r[q], lbc);
+                        else key = key_at<kMode>(a, sh, p, i, k, j, r[q]);
                         key = key < lbc ? 0ull : key;
                         if (key > k1) { k2 = k1; q2 = q1; k1 = key; q1 = (int16_t)k; }
                         else if (key > k2) { k2 = key; q2 = (int16_t)k; }
