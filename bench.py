@@ -227,6 +227,8 @@ def main():
     ap.add_argument("--no-c5", action="store_true", help="c3: skip the C5 node-sharded leg")
     ap.add_argument("--no-dropin", action="store_true", help="c3: skip the drop-in Run-loop leg")
     ap.add_argument("--no-c3q", action="store_true", help="c3: skip the decimal-SI memory (C3q) leg")
+    ap.add_argument("--no-c4", action="store_true", help="c3: skip the C4 what-if scenario leg")
+    ap.add_argument("--c4-steps", type=int, default=2, help="c3: timed steps of the C4 leg")
     ap.add_argument("--c5-steps", type=int, default=4, help="c3: timed steps of the C5 leg")
     ap.add_argument("--c5-timeout", type=float, default=240.0,
                     help="c3: seconds the C5 leg may take before it is abandoned (the C3 line still prints)")
@@ -314,6 +316,14 @@ def main():
     eng.close()
     dropin = dropin_leg(trace, enc, scorers, local) if rank == 0 and not args.no_dropin else None
     c3q = c3q_leg(args, scorers, local) if rank == 0 and not args.no_c3q else None
+    # C4 (BASELINE configs[3]) on every rank: disjoint scenario ranges, weak scaling
+    c4 = None
+    if not args.no_c4:
+        try:
+            c4 = c4_leg(args, rank, world, local, dist)
+        except Exception as ex:  # never fatal to the headline line
+            log(f"[rank {rank}] C4 leg failed: {ex!r}")
+            c4 = {"error": repr(ex)[:500]}
     line = None
 
     if rank == 0:
@@ -359,6 +369,7 @@ def main():
                                     "24 B/node copy to the host; digest = every tick of the last step's window"},
             "dropin": dropin,
             "c3q": c3q,
+            "c4": c4,
             "c5_sharded": None,
             "cpu_baseline": cpu,
             "host": {"cpu": platform.processor() or platform.machine(), "nproc": os.cpu_count()},
@@ -463,9 +474,7 @@ def dropin_leg(trace, enc, scorers, device, per_tick=4000, probe_ticks=400, wind
 
 
 def main_c4(args):
-    """BASELINE.json configs[3]: `scenarios` independent clusters (2k nodes, 10k-pod traces each,
-    seed 0x5EED0004 ^ s) stepped together through ks_group_step; ranks take disjoint scenario
-    ranges (weak scaling, no collective).  A step = `pods-per-step` ticks of every scenario."""
+    """--config c4: the C4 leg alone, printed as the line."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = _device(int(os.environ.get("LOCAL_RANK", "0")))
@@ -473,11 +482,26 @@ def main_c4(args):
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")
+    line = c4_leg(args, rank, world, local, dist, steps=args.steps, warmup=args.warmup)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def c4_leg(args, rank, world, local, dist, steps=None, warmup=None):
+    """BASELINE.json configs[3]: `scenarios` independent clusters (2k nodes, 10k-pod traces each,
+    seed 0x5EED0004 ^ s) stepped together through ks_group_step; ranks take disjoint scenario
+    ranges (weak scaling, no collective).  A step = `pods-per-step` ticks of every scenario (at most
+    the trace / (steps + warmup)).  Part of the default run (the line's "c4" key)
+    with 2 timed steps; --config c4 prints it alone.  Returns rank 0's dict (None elsewhere)."""
     from kubesim_amd import encode, tracegen
     from kubesim_amd.engine import Group
+    steps = args.c4_steps if steps is None else steps
+    warmup = 1 if warmup is None else warmup
     per = args.scenarios // world
     lo = rank * per
-    S_pps = min(args.pods_per_step, args.scenario_pods // max(args.steps + args.warmup, 1))
+    S_pps = min(args.pods_per_step, args.scenario_pods // max(steps + warmup, 1))
     t0 = time.perf_counter()
     g = Group(per, device=local)
     scorers = ((1, 1, 0), (2, 1, 0))
@@ -488,7 +512,7 @@ def main_c4(args):
         e.load_nodes(enc["alloc"], enc["taint"], enc["label"])
         e.submit(enc["pods"])
     log(f"[rank {rank}] {per} scenarios ready in {time.perf_counter() - t0:.1f}s; {S_pps} ticks per step")
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         g.step(S_pps)
 
     def barrier():
@@ -504,9 +528,9 @@ def main_c4(args):
     barrier()
     t_start = time.perf_counter()
     binds, dev_ms, launches, aborted = 0, 0.0, 0, 0
-    for k in range(args.steps):
+    for k in range(steps):
         _, cnt, st, stats = g.step(S_pps)
-        log(f"[rank {rank}] step {k}: {stats['step_ms']:.1f} device ms, {stats['launches']} batch rounds")
+        log(f"[rank {rank}] C4 step {k}: {stats['step_ms']:.1f} device ms, {stats['launches']} batch rounds")
         binds += int(cnt.sum())
         dev_ms += stats["step_ms"]
         launches += stats["launches"]
@@ -522,28 +546,26 @@ def main_c4(args):
         c = torch.tensor([binds], dtype=torch.float64)
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
         total = int(c.item())
-    if rank == 0:
-        evals = total * args.scenario_nodes
-        line = {
-            "metric": "pod-node Filter+Score evals/sec and pods bound/sec (C4 what-if scenarios)",
-            "value": evals / t_el, "unit": "evals/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": t_el * 1e3 / args.steps, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "int64",
-            "data": "synthetic (tracegen C4, seed 0x5EED0004 ^ scenario)",
-            "config": {"workload": "C4: independent what-if scenarios, Filter(fit+taint+selector) -> "
-                                   "Score(LR+BA) -> argmax -> bind per scenario, one launch per kernel",
-                       "scenarios": per * world, "nodes_per_scenario": args.scenario_nodes,
-                       "pods_per_scenario": args.scenario_pods, "ticks_per_step": S_pps,
-                       "parallelism": f"scenarios/{world}"},
-            "pods_per_s": total / t_el,
-            "kernels": {"batch_rounds_per_step": launches / args.steps,
-                        "device_ms_per_step": dev_ms / args.steps},
-            "aborted_scenarios": aborted,
-        }
-        print(json.dumps(line), flush=True)
     g.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    if rank != 0:
+        return None
+    evals = total * args.scenario_nodes
+    return {
+        "metric": "pod-node Filter+Score evals/sec and pods bound/sec (C4 what-if scenarios)",
+        "value": evals / t_el, "unit": "evals/s", "n_gpus": world, "steps": steps,
+        "warmup": warmup, "ms_per_step": t_el * 1e3 / steps, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+        "data": "synthetic (tracegen C4, seed 0x5EED0004 ^ scenario)",
+        "config": {"workload": "C4: independent what-if scenarios, Filter(fit+taint+selector) -> "
+                               "Score(LR+BA) -> argmax -> bind per scenario, one launch per kernel",
+                   "scenarios": per * world, "nodes_per_scenario": args.scenario_nodes,
+                   "pods_per_scenario": args.scenario_pods, "ticks_per_step": S_pps,
+                   "parallelism": f"scenarios/{world}"},
+        "pods_per_s": total / t_el,
+        "kernels": {"batch_rounds_per_step": launches / steps,
+                    "device_ms_per_step": dev_ms / steps},
+        "aborted_scenarios": aborted,
+    }
 
 
 def c5_leg(args, rank, world, local, dist, steps=None, warmup=1, line=None):

@@ -147,6 +147,7 @@ func CommUniqueID() ([]byte, error) {
 // batch; every rank loads the whole cluster and submits the same pods, and all binds are
 // identical.  Call before LoadNodes.
 func (e *Engine) Shard(world, rank int, id []byte, vshards int) error {
+	defer runtime.KeepAlive(e) // e.h must outlive the C call (the finalizer runs ks_destroy)
 	if len(id) != C.KS_COMM_ID_BYTES {
 		return errors.Errorf("communicator id: %d bytes, want %d", len(id), C.KS_COMM_ID_BYTES)
 	}
@@ -157,6 +158,7 @@ func (e *Engine) Shard(world, rank int, id []byte, vshards int) error {
 // LoadNodes loads the cluster once: alloc = n*4 {milli cpu, milli memory, milli gpu, pods}
 // (-1 = key absent), taint / label = dictionary bitmasks (Dicts).
 func (e *Engine) LoadNodes(alloc []int64, taint, label []uint64) error {
+	defer runtime.KeepAlive(e) // e.h must outlive the C call (the finalizer runs ks_destroy)
 	n := len(taint)
 	if len(alloc) != 4*n || len(label) != n {
 		return strongerrors.InvalidArgument(errors.New("LoadNodes: alloc must hold 4 values per node"))
@@ -212,6 +214,7 @@ func u8p(s []uint8) *C.uint8_t {
 
 // SubmitPods appends pods to the FIFO (submit + podQueue.append, kubesim/kubesim.go:126-139).
 func (e *Engine) SubmitPods(p *Pods) error {
+	defer runtime.KeepAlive(e) // e.h must outlive the C call (the finalizer runs ks_destroy)
 	m := len(p.Arrival)
 	if m == 0 {
 		return nil
@@ -236,14 +239,21 @@ type Bind struct {
 }
 
 // Queued is the number of submitted pods not popped yet.
-func (e *Engine) Queued() int64 { return int64(C.ks_queued_pods(e.h)) }
+func (e *Engine) Queued() int64 {
+	defer runtime.KeepAlive(e)
+	return int64(C.ks_queued_pods(e.h))
+}
 
 // Tick is the engine's current tick.
-func (e *Engine) Tick() int64 { return int64(C.ks_current_tick(e.h)) }
+func (e *Engine) Tick() int64 {
+	defer runtime.KeepAlive(e)
+	return int64(C.ks_current_tick(e.h))
+}
 
 // Step advances `ticks` ticks of Run's loop (at most one bind per tick).  Binds made before an
 // aborting error (NotFound / InvalidArgument) are returned with the error.
 func (e *Engine) Step(ticks int64) ([]Bind, error) {
+	defer runtime.KeepAlive(e) // e.h must outlive the C call (the finalizer runs ks_destroy)
 	cap := ticks
 	if q := e.Queued(); q < cap {
 		cap = q
@@ -268,6 +278,7 @@ func (e *Engine) Step(ticks int64) ([]Bind, error) {
 // FilterMask is api.Filter over every node for queued pod `pod` (ks_filter): one byte per
 // loaded node.
 func (e *Engine) FilterMask(pod int64) ([]uint8, error) {
+	defer runtime.KeepAlive(e) // e.h must outlive the C call (the finalizer runs ks_destroy)
 	mask := make([]uint8, e.n+1)
 	return mask[:e.n], status(e, C.ks_filter(e.h, C.int64_t(pod), u8p(mask)))
 }
@@ -275,6 +286,7 @@ func (e *Engine) FilterMask(pod int64) ([]uint8, error) {
 // Scores is the aggregated score of every loaded node for queued pod `pod` (-1 = no entry,
 // ks_score).
 func (e *Engine) Scores(pod int64) ([]int64, error) {
+	defer runtime.KeepAlive(e) // e.h must outlive the C call (the finalizer runs ks_destroy)
 	s := make([]int64, e.n+1)
 	return s[:e.n], status(e, C.ks_score(e.h, C.int64_t(pod), i64p(s)))
 }
@@ -282,6 +294,7 @@ func (e *Engine) Scores(pod int64) ([]int64, error) {
 // UsageAt is Σ Pod.ResourceUsage per node at tick t <= Tick() (3 per loaded node: cpu, memory,
 // gpu milli).
 func (e *Engine) UsageAt(t int64) ([]int64, error) {
+	defer runtime.KeepAlive(e) // e.h must outlive the C call (the finalizer runs ks_destroy)
 	u := make([]int64, 3*e.n+1)
 	return u[:3*e.n], status(e, C.ks_usage_at(e.h, C.int64_t(t), i64p(u)))
 }
@@ -291,6 +304,7 @@ func (e *Engine) Nodes() int { return e.n }
 
 // PodLookup is Node.GetPod by key (kubesim/node/node.go:62-75): the FIFO index stored there.
 func (e *Engine) PodLookup(node int32, key int64) (int64, error) {
+	defer runtime.KeepAlive(e) // e.h must outlive the C call (the finalizer runs ks_destroy)
 	var q C.int64_t
 	err := status(e, C.ks_pod_lookup(e.h, C.int32_t(node), C.int64_t(key), &q))
 	return int64(q), err
@@ -298,6 +312,7 @@ func (e *Engine) PodLookup(node int32, key int64) (int64, error) {
 
 // NodePods is Node.GetPodList (kubesim/node/node.go:77-82): FIFO indices, one per key.
 func (e *Engine) NodePods(node int32) ([]int64, error) {
+	defer runtime.KeepAlive(e) // e.h must outlive the C call (the finalizer runs ks_destroy)
 	var n C.int64_t
 	if err := status(e, C.ks_node_pods(e.h, C.int32_t(node), nil, 0, &n)); err != nil {
 		return nil, err
@@ -325,6 +340,7 @@ type PodInfo struct {
 
 // PodStatus returns the status of FIFO pods [lo, lo+n).
 func (e *Engine) PodStatus(lo, n int64) ([]PodInfo, error) {
+	defer runtime.KeepAlive(e) // e.h must outlive the C call (the finalizer runs ks_destroy)
 	out := make([]C.ks_pod_info, n+1)
 	if err := status(e, C.ks_pod_status(e.h, C.int64_t(lo), C.int64_t(n), &out[0])); err != nil {
 		return nil, err

@@ -102,8 +102,11 @@ enum { KS_ENGINE_FORCE_WIDE = 1, KS_ENGINE_NO_TINY = 2, KS_ENGINE_NO_MICRO = 4,
         * flags exist to test them against each other): ONE_POD = the role-split one-pod-per-
         * barrier resolver; CHUNK = chunked Jacobi sweeps in one workgroup's LDS (ks_step only,
         * evaluator modes >= narrow, totals < 2^16).  Bits 16, 32 and 128 (the retired pair, sweep
-        * and sequential resolvers) are rejected. */
-       KS_ENGINE_ONE_POD_RESOLVER = 8, KS_ENGINE_CHUNK_RESOLVER = 64 };
+        * and sequential resolvers) are rejected.
+        * NO_OVERLAP: the chunk resolver's batches run the plain chain (each batch's scan before its
+        * resolve) instead of fusing the next batch's speculative scan into the resolve launch — the
+        * same binds; for A/B timing and to test the two chains against each other. */
+       KS_ENGINE_ONE_POD_RESOLVER = 8, KS_ENGINE_CHUNK_RESOLVER = 64, KS_ENGINE_NO_OVERLAP = 256 };
 
 typedef struct {
     int64_t pod;    /* FIFO index (submission order) */
@@ -249,6 +252,8 @@ typedef struct {
 ks_status ks_pod_status(ks_engine* eng, int64_t pod_lo, int64_t n, ks_pod_info* out);
 
 int64_t ks_current_tick(const ks_engine* eng);
+/* the configured tick in seconds (ks_config.tick_seconds); -1 for NULL */
+int32_t ks_tick_seconds(const ks_engine* eng);
 int64_t ks_queued_pods(const ks_engine* eng);
 const char* ks_last_error(const ks_engine* eng);
 

@@ -16,7 +16,10 @@
  *   ks_trace_submit   a built-in submitter that replays an encoded trace by arrival tick.
  *
  * Errors are Run's: the first non-OK status of ks_submit_pods / ks_step stops the loop and is
- * returned; the binds made before it are in out[0 .. *n_out).
+ * returned; the binds made before it are in out[0 .. *n_out).  A submitter or submit error at tick
+ * t with window > 1 first steps the ticks before t (Run had scheduled them before it called the
+ * submitters at t).  Submitters get clock_seconds = tick * tick_seconds (the start clock is the
+ * caller's: kubesim.go:94-97 adds it).
  */
 #ifndef KS_KUBESIM_H
 #define KS_KUBESIM_H
@@ -70,6 +73,9 @@ ks_local_exchange* ks_local_exchange_create(int32_t world);
 void ks_local_exchange_destroy(ks_local_exchange* x);
 ks_status ks_local_allgather(void* user /* ks_local_exchange* */, int32_t rank, int32_t world, void* buf,
                              int64_t bytes_per_rank);
+/* A rank whose step failed before it reached the exchange would leave the others waiting: its
+ * driver calls this, and every current and later ks_local_allgather on x returns KS_EDEVICE. */
+void ks_local_exchange_abort(ks_local_exchange* x);
 
 #ifdef __cplusplus
 }

@@ -98,6 +98,24 @@ struct DVec {
     }
 };
 
+// (finish tick, pod) min-heap whose array can be walked: the entries due by a tick are the heap's
+// top subtree (flush_expiries visits them without copying or popping the heap)
+struct PendingHeap : std::priority_queue<std::pair<int64_t, int64_t>, std::vector<std::pair<int64_t, int64_t>>,
+                                         std::greater<std::pair<int64_t, int64_t>>> {
+    template <class F>
+    void for_each_due(int64_t t, F&& f) const {
+        std::vector<size_t> st;
+        if (!c.empty() && c[0].first <= t) st.push_back(0);
+        while (!st.empty()) {
+            const size_t i = st.back();
+            st.pop_back();
+            f(c[i].second);
+            for (size_t k = 2 * i + 1; k <= 2 * i + 2 && k < c.size(); k++)
+                if (c[k].first <= t) st.push_back(k);
+        }
+    }
+};
+
 }  // namespace
 
 struct ks_engine {
@@ -124,9 +142,7 @@ struct ks_engine {
     std::vector<int64_t> h_exp_off{0};
     std::vector<int32_t> h_dur;
     std::vector<int32_t> h_total_sec;  // Σ phase seconds, int32 wrapping (Pod.totalSeconds)
-    std::priority_queue<std::pair<int64_t, int64_t>, std::vector<std::pair<int64_t, int64_t>>,
-                        std::greater<std::pair<int64_t, int64_t>>>
-        pending;  // (finish tick, pod) not yet attached to a later pod
+    PendingHeap pending;  // (finish tick, pod) not yet attached to a later pod
     int64_t P = 0, F = 0;
     int64_t last_arrival = 0;
     int64_t scale[3] = {1, 1, 1};   // device unit of cpu / memory / gpu, in milli-units
@@ -429,7 +445,7 @@ ks_status engine_init(const ks_config* cfg, ks_engine** out) {
     if (cfg->batch_pods < 0 || cfg->batch_pods > kMaxBatch) return KS_EINVAL;
     if (cfg->engine_flags &
         ~(uint32_t)(KS_ENGINE_FORCE_WIDE | KS_ENGINE_NO_TINY | KS_ENGINE_NO_MICRO | KS_ENGINE_ONE_POD_RESOLVER |
-                    KS_ENGINE_CHUNK_RESOLVER))
+                    KS_ENGINE_CHUNK_RESOLVER | KS_ENGINE_NO_OVERLAP))
         return KS_EINVAL;
     int64_t const_total = 0, w_lr = 0, w_ba = 0;
     for (int i = 0; i < cfg->n_scorers; i++) {
@@ -452,6 +468,7 @@ ks_status engine_init(const ks_config* cfg, ks_engine** out) {
     e->device = cfg->device;
     e->B = cfg->batch_pods ? cfg->batch_pods : kDefaultBatch;
     e->flags = cfg->engine_flags;
+    e->overlap = !(cfg->engine_flags & KS_ENGINE_NO_OVERLAP);
     e->dc.filter_feeds = cfg->filter_mode == KS_FILTER_FEEDS_SCORE;
     e->dc.filters = cfg->filters;
     e->dc.has_scorers = cfg->n_scorers > 0;
@@ -471,7 +488,6 @@ ks_status ks_create(const ks_config* cfg, ks_engine** out) {
     ks_engine* e = nullptr;
     const ks_status v = engine_init(cfg, &e);
     if (v != KS_OK) return v;
-    if (const char* ov = std::getenv("KS_OVERLAP")) e->overlap = ov[0] != '0';  // A/B switch
     hipError_t r = hipSetDevice(e->device);
     if (r == hipSuccess) r = hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking);
     if (r == hipSuccess) r = hipMalloc(&e->d_ctr, 32 * sizeof(int64_t));
@@ -1136,7 +1152,9 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
         e->tick = t_end;
         return KS_OK;
     }
-    if (p_hi == e->done + 1 && !e->group && e->world * e->vsh == 1 && e->n > 0 && !e->profiling) {
+    // (an explicitly forced resolver keeps one-pod steps on that resolver: its A/B tests)
+    if (p_hi == e->done + 1 && !e->group && e->world * e->vsh == 1 && e->n > 0 && !e->profiling &&
+        !(e->flags & (KS_ENGINE_CHUNK_RESOLVER | KS_ENGINE_ONE_POD_RESOLVER))) {
         ks_status rc = KS_OK;
         if (tick_step(e, t_end, out, cap, n_out, &rc)) return rc;
     }
@@ -1569,13 +1587,7 @@ static ks_status flush_expiries(ks_engine* e) {
         };
         if (e->done < e->P)
             for (int64_t u = e->h_exp_off[e->done]; u < e->h_exp_off[e->done + 1]; u++) add(e->h_exp_pod[u]);
-        if (!e->pending.empty() && e->pending.top().first <= e->tick) {
-            auto pq = e->pending;
-            while (!pq.empty() && pq.top().first <= e->tick) {
-                add(pq.top().second);
-                pq.pop();
-            }
-        }
+        e->pending.for_each_due(e->tick, add);
         if ((int)qs.size() <= ks::kTickMaxExp) {
             if (!qs.empty()) {
                 ks::ExpList L{};
@@ -1791,6 +1803,7 @@ ks_status ks_pod_status(ks_engine* e, int64_t pod_lo, int64_t n, ks_pod_info* ou
 }
 
 int64_t ks_current_tick(const ks_engine* e) { return e ? e->tick : -1; }
+int32_t ks_tick_seconds(const ks_engine* e) { return e ? e->cfg.tick_seconds : -1; }
 int64_t ks_queued_pods(const ks_engine* e) { return e ? e->P - e->done : -1; }
 const char* ks_last_error(const ks_engine* e) { return e ? e->errmsg.c_str() : "null engine"; }
 

@@ -43,6 +43,7 @@ ks_status ks_run(ks_engine* eng, int64_t ticks, int64_t window, int32_t n_submit
     std::vector<int64_t> arr;
     std::vector<int32_t> off;
     const int64_t start = ks_current_tick(eng);
+    const int64_t tick_s = ks_tick_seconds(eng);
     int64_t tick = start, stepped = start;
     ks_status rc = KS_OK;
     auto step = [&](int64_t k) -> ks_status {
@@ -57,7 +58,7 @@ ks_status ks_run(ks_engine* eng, int64_t ticks, int64_t window, int32_t n_submit
         tick++;
         for (int32_t s = 0; s < n_submitters && rc == KS_OK; s++) {  // kubesim.go:126-139, registration order
             ks_pods p{};
-            rc = fns[s](users[s], tick, 0, &p);
+            rc = fns[s](users[s], tick, tick * tick_s, &p);  // clock = start + tick * tick (kubesim.go:94-97)
             if (rc != KS_OK || p.m == 0) continue;
             // the pods arrive at this tick; phase CSR rebased to 0
             arr.assign(p.m, tick);
@@ -66,7 +67,14 @@ ks_status ks_run(ks_engine* eng, int64_t ticks, int64_t window, int32_t n_submit
             rc = ks_submit_pods(eng, p.m, arr.data(), p.req, p.keymask, p.tol, p.sel, off.data(), p.phase_sec,
                                 p.phase_use, p.flags, p.key_id);
         }
-        if (rc != KS_OK) break;
+        if (rc != KS_OK) {
+            // Run would have scheduled every tick before this one before calling the submitters at
+            // it: the window's ticks (stepped, tick) are stepped first; the submit error is returned
+            // (a step error before it wins, as it would have stopped Run sooner)
+            const ks_status r = step(tick - 1 - stepped);
+            if (r != KS_OK) rc = r;
+            break;
+        }
         if (tick - stepped >= window) rc = step(tick - stepped);  // window 1: scheduleOne every tick
     }
     if (rc == KS_OK) rc = step(tick - stepped);
@@ -85,6 +93,7 @@ struct ks_local_exchange {
     std::vector<uint8_t> buf;
     int32_t arrived = 0, left = 0;
     uint64_t gen = 0;
+    bool aborted = false;  // ks_local_exchange_abort: every wait ends with KS_EDEVICE
 };
 
 extern "C" {
@@ -98,14 +107,24 @@ ks_local_exchange* ks_local_exchange_create(int32_t world) {
 
 void ks_local_exchange_destroy(ks_local_exchange* x) { delete x; }
 
+void ks_local_exchange_abort(ks_local_exchange* x) {
+    if (!x) return;
+    std::lock_guard<std::mutex> lk(x->mu);
+    x->aborted = true;
+    x->cv.notify_all();
+}
+
 // Two phases per exchange: every rank deposits its slice, the last depositor releases them all;
-// every rank copies the whole array out, the last to leave opens the next exchange.
+// every rank copies the whole array out, the last to leave opens the next exchange.  A rank that
+// fails before its deposit would leave the others waiting: its driver aborts the exchange, which
+// ends every current and later wait with KS_EDEVICE (the engines' steps then fail, sticky).
 ks_status ks_local_allgather(void* user, int32_t rank, int32_t world, void* buf, int64_t bytes_per_rank) {
     ks_local_exchange* x = static_cast<ks_local_exchange*>(user);
     if (!x || world != x->world || rank < 0 || rank >= world || bytes_per_rank < 0) return KS_EINVAL;
     uint8_t* b = static_cast<uint8_t*>(buf);
     std::unique_lock<std::mutex> lk(x->mu);
-    x->cv.wait(lk, [&] { return x->left == 0; });  // the previous exchange has been read by everyone
+    x->cv.wait(lk, [&] { return x->left == 0 || x->aborted; });  // the previous exchange has been read by everyone
+    if (x->aborted) return KS_EDEVICE;
     const uint64_t g = x->gen;
     if ((int64_t)x->buf.size() < bytes_per_rank * world) x->buf.resize(bytes_per_rank * world);
     std::memcpy(x->buf.data() + rank * bytes_per_rank, b + rank * bytes_per_rank, bytes_per_rank);
@@ -115,7 +134,8 @@ ks_status ks_local_allgather(void* user, int32_t rank, int32_t world, void* buf,
         x->gen++;
         x->cv.notify_all();
     } else {
-        x->cv.wait(lk, [&] { return x->gen != g; });
+        x->cv.wait(lk, [&] { return x->gen != g || x->aborted; });
+        if (x->gen == g) return KS_EDEVICE;  // aborted before every rank deposited
     }
     std::memcpy(b, x->buf.data(), bytes_per_rank * world);
     if (--x->left == 0) x->cv.notify_all();

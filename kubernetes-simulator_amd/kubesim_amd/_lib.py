@@ -24,6 +24,7 @@ KS_ENGINE_NO_TINY = 2
 KS_ENGINE_NO_MICRO = 4
 KS_ENGINE_ONE_POD_RESOLVER = 8
 KS_ENGINE_CHUNK_RESOLVER = 64
+KS_ENGINE_NO_OVERLAP = 256
 KS_SELFTEST_LR_MICRO = 0
 
 STATUS_NAMES = {KS_OK: "OK", KS_EINVAL: "InvalidArgument", KS_ENOTFOUND: "NotFound",
@@ -31,7 +32,7 @@ STATUS_NAMES = {KS_OK: "OK", KS_EINVAL: "InvalidArgument", KS_ENOTFOUND: "NotFou
 
 # every symbol include/*.h declares
 EXPORTED_SYMBOLS = ("ks_create", "ks_destroy", "ks_load_nodes", "ks_submit_pods", "ks_step",
-                    "ks_filter", "ks_score", "ks_usage", "ks_current_tick", "ks_queued_pods",
+                    "ks_filter", "ks_score", "ks_usage", "ks_current_tick", "ks_tick_seconds", "ks_queued_pods",
                     "ks_last_error", "ks_last_step_stats", "ks_set_profiling", "ks_debug_counters", "ks_selftest",
                     "ks_comm_unique_id", "ks_shard", "ks_shard_host", "ks_group_create", "ks_group_destroy",
                     "ks_group_add", "ks_group_size", "ks_group_step", "ks_pod_status",
@@ -44,7 +45,7 @@ EXPORTED_SYMBOLS = ("ks_create", "ks_destroy", "ks_load_nodes", "ks_submit_pods"
 KS_COMM_ID_BYTES = 128
 # include/ks_kubesim.h (libks_kubesim.so)
 RUN_SYMBOLS = ("ks_run", "ks_trace_submit", "ks_local_exchange_create", "ks_local_exchange_destroy",
-               "ks_local_allgather")
+               "ks_local_allgather", "ks_local_exchange_abort")
 
 
 class KsScorer(C.Structure):
@@ -110,6 +111,8 @@ def load_run():
     L.ks_local_exchange_destroy.restype = None
     L.ks_local_allgather.argtypes = [p, C.c_int32, C.c_int32, p, C.c_int64]
     L.ks_local_allgather.restype = C.c_int
+    L.ks_local_exchange_abort.argtypes = [p]
+    L.ks_local_exchange_abort.restype = None
     _run_lib = L
     return L
 
@@ -148,6 +151,8 @@ def load():
         getattr(L, f).restype = C.c_int
     L.ks_current_tick.argtypes = [p]
     L.ks_current_tick.restype = C.c_int64
+    L.ks_tick_seconds.argtypes = [p]
+    L.ks_tick_seconds.restype = C.c_int32
     L.ks_queued_pods.argtypes = [p]
     L.ks_queued_pods.restype = C.c_int64
     L.ks_last_error.argtypes = [p]

@@ -270,6 +270,12 @@ class LocalExchange:
             raise ValueError("bad world size")
         self.fn = C.cast(self._R.ks_local_allgather, C.c_void_p)
 
+    def abort(self):
+        """End every current and later exchange with KS_EDEVICE (a rank failed before its
+        deposit: the others would wait for it forever; ks_local_exchange_abort)."""
+        if getattr(self, "h", None):
+            self._R.ks_local_exchange_abort(self.h)
+
     def close(self):
         if getattr(self, "h", None):
             self._R.ks_local_exchange_destroy(self.h)

@@ -4,9 +4,11 @@ import runpy
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from devlib import lib_path  # noqa: E402
 sys.path.insert(0, os.path.join(ROOT, "kubernetes-simulator_amd"))
 from kubesim_amd import _lib  # noqa: E402
 
-_lib.LIB_PATH = os.path.join(ROOT, "kubernetes-simulator_amd", "kubesim_amd", os.environ.get("KS_LIB", "libks_engine.so"))
+_lib.LIB_PATH = lib_path(os.environ.get("KS_LIB", "libks_engine.so"))
 sys.argv = [os.path.join(ROOT, "bench.py")] + sys.argv[1:]
 runpy.run_path(sys.argv[0], run_name="__main__")

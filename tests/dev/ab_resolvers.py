@@ -5,10 +5,12 @@ other device time (HIP events), pods per launch, wall pods/s and a CRC of the bi
 import os, sys, time, zlib
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from devlib import lib_path  # noqa: E402
 sys.path.insert(0, os.path.join(ROOT, "kubernetes-simulator_amd"))
 from kubesim_amd import _lib
 if os.environ.get("KS_DIAG_LIB"):
-    _lib.LIB_PATH = os.path.join(ROOT, "kubernetes-simulator_amd", "kubesim_amd", os.environ["KS_DIAG_LIB"])
+    _lib.LIB_PATH = lib_path(os.environ["KS_DIAG_LIB"])
 from kubesim_amd import tracegen, encode
 from kubesim_amd.engine import Engine
 args = [x for x in sys.argv[1:] if not x.startswith("--")]

@@ -5,9 +5,11 @@ state / both cached nodes rebound, 1 candidate buffer overflow, 2 truncated list
 finalize, commit; [21] cids, [22] E nodes, [23] batch pods."""
 import os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from devlib import lib_path  # noqa: E402
 sys.path.insert(0, os.path.join(ROOT, "kubernetes-simulator_amd"))
 from kubesim_amd import _lib
-_lib.LIB_PATH = os.path.join(ROOT, "kubernetes-simulator_amd", "kubesim_amd", os.environ.get("KS_DIAG_LIB", "libks_engine_chunkdiag.so"))
+_lib.LIB_PATH = lib_path(os.environ.get("KS_DIAG_LIB", "libks_engine_chunkdiag.so"))
 from kubesim_amd import tracegen, encode
 from kubesim_amd.engine import Engine
 c5 = "--c5" in sys.argv

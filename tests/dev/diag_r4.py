@@ -7,11 +7,12 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from devlib import lib_path  # noqa: E402
 sys.path.insert(0, os.path.join(ROOT, "kubernetes-simulator_amd"))
 from kubesim_amd import _lib  # noqa: E402
 
-_lib.LIB_PATH = os.path.join(ROOT, "kubernetes-simulator_amd", "kubesim_amd",
-                             sys.argv[1] if len(sys.argv) > 1 else "libks_engine_st.so")
+_lib.LIB_PATH = lib_path(sys.argv[1] if len(sys.argv) > 1 else "libks_engine_st.so")
 from kubesim_amd import encode, tracegen  # noqa: E402
 from kubesim_amd.engine import Engine  # noqa: E402
 

@@ -2,9 +2,11 @@
 import os, sys, time
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from devlib import lib_path  # noqa: E402
 sys.path.insert(0, os.path.join(ROOT, "kubernetes-simulator_amd"))
 from kubesim_amd import _lib
-_lib.LIB_PATH = os.path.join(ROOT, "kubernetes-simulator_amd", "kubesim_amd", os.environ.get("KS_DIAG_LIB", "libks_engine_stamps.so"))
+_lib.LIB_PATH = lib_path(os.environ.get("KS_DIAG_LIB", "libks_engine_stamps.so"))
 from kubesim_amd import tracegen, encode
 from kubesim_amd.engine import Engine
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256

@@ -132,6 +132,34 @@ def test_c2_prefix_native_run_equals_oracle(window):
     print(f"\nnative Run window {window}: {len(b) / sec:.0f} pods/s ({sec / T * 1e6:.1f} us/tick)")
 
 
+@pytest.mark.parametrize("window", [1, 16])
+def test_native_run_submit_error_steps_the_ticks_before_it(window):
+    """a submit that fails at tick t (a request outside the exact domain: KS_EINVAL from
+    ks_submit_pods) stops Run after it has scheduled every tick before t — also with window > 1,
+    where the ticks since the last step are stepped before the error returns."""
+    from kubesim_amd import _lib
+    from kubesim_amd.engine import KsError
+    P, T = 300, 400
+    tr = tracegen.c2_trace(n_pods=P, arrival="stream")
+    enc = encoded(tr)
+    bad = 137
+    enc["pods"]["req"] = np.array(enc["pods"]["req"], copy=True)
+    enc["pods"]["req"].reshape(-1, 3)[bad, 0] = 1 << 60
+    t_bad = int(enc["pods"]["arrival"][bad])
+    mode = "feeds_all_lrba"
+    ora = make_oracle(tr, mode)
+    ora.submit(tr)
+    ob, rc = ora.step(t_bad - 1, cap=T)  # Run's binds before tick t_bad
+    assert rc == 0
+    nr = _native(tr, enc, mode)
+    with pytest.raises(KsError) as ex:
+        nr.run(T, window)
+    assert ex.value.code == _lib.KS_EINVAL
+    assert_same_binds(ex.value.binds, ob)
+    assert nr.eng.tick == t_bad - 1
+    np.testing.assert_array_equal(nr.eng.usage(), ora.usage())
+
+
 def test_tick_path_dense_expiries_mixed_steps_and_probes():
     """Short phases (many expiries due per tick), one pod per tick: ks_step(1) takes the one-launch
     path, its by-value expiry list and the host-staged submits; interleaved with batched steps

@@ -51,3 +51,30 @@ def test_bad_arguments():
     b = np.zeros(4, np.uint64)
     assert R.ks_local_allgather(x.h, 2, 2, b.ctypes.data_as(C.c_void_p), 16) == _lib.KS_EINVAL
     assert R.ks_local_allgather(x.h, 0, 3, b.ctypes.data_as(C.c_void_p), 16) == _lib.KS_EINVAL
+
+
+def test_abort_releases_waiting_ranks():
+    """A rank that failed before its deposit: its driver aborts the exchange and the ranks already
+    waiting in it (and any later call) return KS_EDEVICE instead of hanging."""
+    R = _lib.load_run()
+    x = LocalExchange(3)
+    rcs = {}
+
+    def rank(r):
+        b = np.zeros(3 * 4, np.uint64)
+        rcs[r] = R.ks_local_allgather(x.h, r, 3, b.ctypes.data_as(C.c_void_p), 32)
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in (0, 1)]  # rank 2 never arrives
+    for t in th:
+        t.start()
+    import time
+    time.sleep(0.2)
+    assert all(t.is_alive() for t in th)  # both wait for rank 2
+    x.abort()
+    for t in th:
+        t.join(10)
+    assert not any(t.is_alive() for t in th), "abort did not release the waiting ranks"
+    assert rcs == {0: _lib.KS_EDEVICE, 1: _lib.KS_EDEVICE}
+    b = np.zeros(12, np.uint64)
+    assert R.ks_local_allgather(x.h, 2, 3, b.ctypes.data_as(C.c_void_p), 32) == _lib.KS_EDEVICE
+    x.close()

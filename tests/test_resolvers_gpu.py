@@ -100,17 +100,9 @@ def test_chunk_decimal_memory_class():
 
 
 # ---- the overlap (next batch's scan fused into the chunk kernel, ks_engine.cpp step loop) ------
-def _engine_env(tr, enc, mode, overlap, **kw):
-    import os
-    old = os.environ.get("KS_OVERLAP")
-    os.environ["KS_OVERLAP"] = "1" if overlap else "0"  # read once, at engine creation
-    try:
-        return make_engine(tr, enc, mode, **kw)
-    finally:
-        if old is None:
-            del os.environ["KS_OVERLAP"]
-        else:
-            os.environ["KS_OVERLAP"] = old
+def _engine_env(tr, enc, mode, overlap, engine_flags=0, **kw):
+    flags = engine_flags | (0 if overlap else _lib.KS_ENGINE_NO_OVERLAP)
+    return make_engine(tr, enc, mode, engine_flags=flags, **kw)
 
 
 @pytest.mark.parametrize("case", ["c2", "dense_expiries"])

@@ -34,7 +34,7 @@ def _ranks(tr, enc, world, vshards, mode=MODE, **kw):
     return engs, x
 
 
-def _step_all(engs, k):
+def _step_all(engs, k, x=None):
     out = [None] * len(engs)
 
     def run(r):
@@ -42,6 +42,8 @@ def _step_all(engs, k):
             out[r] = engs[r].step(k)
         except Exception as ex:  # noqa: BLE001 - reported below
             out[r] = ex
+            if x is not None:  # the other ranks would wait for this one's deposit
+                x.abort()
     th = [threading.Thread(target=run, args=(r,)) for r in range(len(engs))]
     for t in th:
         t.start()
@@ -62,7 +64,7 @@ def test_ranks_match_oracle_small(world, vshards):
     ora = make_oracle(tr, MODE)
     ora.submit(tr)
     for k in (1, 700, 1900):
-        bs = _step_all(engs, k)
+        bs = _step_all(engs, k, _x)
         ob, rc = ora.step(k, cap=k)
         for b in bs:
             assert_same_binds(b, ob)
@@ -78,7 +80,7 @@ def test_c2_prefix_two_ranks_match_oracle():
     ora = make_oracle(tr, MODE)
     ora.submit(tr)
     for k in (4096, 3904):
-        bs = _step_all(engs, k)
+        bs = _step_all(engs, k, _x)
         ob, rc = ora.step(k, cap=k)
         assert rc == 0
         for b in bs:
@@ -100,7 +102,7 @@ def test_c5_whole_trace_two_ranks_match_oracle_golden():
     done = 0
     for w, want in enumerate(g["bind_digests"]):
         k = min(g["window"], g["pods"] - done)
-        bs = _step_all(engs, k)
+        bs = _step_all(engs, k, _x)
         for r, b in enumerate(bs):
             assert len(b) == k and int(b["pod"][0]) == done
             assert full_run_digest.bind_digest(b) == want, f"rank {r}: window {w} differs"
