@@ -22,6 +22,7 @@
 #include <climits>
 
 #include "ks_device.h"
+#include "ks_prep.h"
 
 namespace ks {
 namespace sq {
@@ -29,14 +30,11 @@ namespace sq {
 constexpr int kL = kTopL;
 constexpr int kR = kChR;
 constexpr int kPrepThreads = 1024;
-constexpr int kEHashLog2 = 12, kEHash = 1 << kEHashLog2;
-static_assert(2 * kEMax <= kEHash, "E hash load <= 1/2");
 constexpr int kClBuf = 256;
 static_assert(kR <= kWave, "one candidate per lane");
 static_assert(kWinSlots <= kPrepThreads, "one window slot per prep thread");
 
 __device__ __forceinline__ int32_t key_node(uint64_t key) { return (int32_t)(0xFFFFFFFFu - (uint32_t)key); }
-__device__ __forceinline__ uint32_t ehslot(int32_t n) { return ((uint32_t)n * 2654435761u) >> (32 - kEHashLog2); }
 __device__ __forceinline__ int32_t clamp32(int64_t v) { return (int32_t)(v > INT_MAX ? INT_MAX : v); }
 
 template <typename T>
@@ -45,159 +43,16 @@ __device__ __forceinline__ const __attribute__((address_space(1))) T* cg(const T
 }
 
 // ---------------------------------------------------------------------------------------------
-// Window: the expiries attached to pods start+1 .. start+nb-1 (exp_off CSR), one slot each; the
-// batch shrinks to the largest prefix whose window fits kWinSlots.  E = the distinct nodes of the
-// slots whose pod was bound Ok before the batch and has not expired; e_idx marks them.
-// Overlap (`spec`): the batch's block lists come from the speculative scan that ran beside the
-// previous batch's resolve, on the node table as it was then.  They are exact for every node the
-// previous batch did not change; the changed ones (its binds and window expiry nodes, written by
-// its commit as `touched`, and the head expiries applied here) join E with no slots, so the
-// candidate lists evaluate them exactly (an E node enters a list when its exact key reaches the
-// list's threshold — the same rule as for the expiry nodes).  The speculative scan covered the
-// pods after the previous batch; if that batch stopped early (this batch starts elsewhere) or the
-// touched nodes overflow E, `rescan` asks the conditional scan on the engine's stream to redo the
-// lists on the current table.  The speculative counters for the next scan are written last.
+// Window (ks_prep.h prep_body): the expiries attached to pods start+1 .. start+nb-1, the node set E,
+// the head expiries, the overlap's touched nodes and rescan flag.  This kernel runs it for the first
+// batch of each ks_step pass (and for every batch of the plain chain); an overlapped batch's window
+// is computed by the previous chunk kernel's resolver workgroup right after its commit.
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kPrepThreads) void window_prep_kernel(const EngineArgs* __restrict__ A, int head, int spec,
                                                                     int slot) {
     const EngineArgs& a = A[0];
-    WinWS& ws = *a.sw;
-    const int tid = threadIdx.x;
-    __shared__ int32_t hk[kEHash], hv[kEHash];
-    __shared__ int32_t cnt[kWinSlots], fill[kWinSlots];
-    __shared__ int32_t xn[kEMax];  // touched nodes to insert (overlap)
-    __shared__ int32_t s_ne, s_nx;
-    const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
-    // the speculative counters, double-buffered by batch parity: this batch writes `slot` (read by
-    // the next batch's speculative scan, which may still run while the batch after writes the
-    // other), and checks the previous batch's
-    int64_t* const spec_out = a.spec_ctr + kSpecStride * slot;
-    const int64_t* const spec_in = a.spec_ctr + kSpecStride * (slot ^ 1);
-    int nb = (int)min<int64_t>(min<int64_t>(a.B, kWinMaxB), end - start);
-    if (a.ctr[kCtrErr] != 0 || nb <= 0) {
-        if (tid == 0) {
-            ws.nb = 0; ws.e_cnt = 0; ws.n_e = 0; ws.n_es = 0; ws.rescan = 0;
-            spec_out[kCtrStart] = end; spec_out[kCtrEnd] = end; spec_out[kCtrErr] = 0;
-        }
-        return;
-    }
-    const int64_t e0 = a.exp_off[start], e1 = a.exp_off[start + 1];
-    const int64_t e_base = e1;
-    const bool fits_win = tid < nb && a.exp_off[start + tid + 1] - e_base <= kWinSlots;
-    for (int h = tid; h < kEHash; h += kPrepThreads) hk[h] = -1;
-    if (tid == 0) { s_ne = 0; s_nx = 0; }
-    nb = __syncthreads_count(fits_win);  // exp_off is non-decreasing: a prefix of the pods
-    const int e_cnt = (int)(a.exp_off[start + nb] - e_base);
-    // overlap: the lists are usable when the speculative scan covered this batch's pods and the
-    // changed nodes fit E
-    int rescan = 0;
-    if (spec) rescan = start != spec_in[kCtrStart] || (int64_t)e_cnt + (e1 - e0) + ws.n_touched > kEMax;
-    const bool touch = spec && !rescan;
-    if (head) {  // expire_head's work: the expiries due before the batch's first pod
-        for (int64_t e = e0 + tid; e < e1; e += kPrepThreads) {
-            const int32_t q = a.exp_pod[e];
-            if (a.b_status[q] != 0 || a.expired[q]) continue;
-            const int32_t nd = a.b_node[q];
-            const PodRec& p = a.pods[q];
-            atomicAdd((unsigned long long*)&a.s.rc[nd], (unsigned long long)(-p.req[0]));
-            atomicAdd((unsigned long long*)&a.s.rm[nd], (unsigned long long)(-p.req[1]));
-            atomicAdd((unsigned long long*)&a.s.rg[nd], (unsigned long long)(-p.req[2]));
-            atomicAdd((unsigned long long*)&a.s.nr[nd], (unsigned long long)(-1ll));
-            a.expired[q] = 1;
-            if (touch) xn[atomicAdd(&s_nx, 1)] = nd;
-        }
-    }
-    if (touch) {
-        for (int t = tid; t < ws.n_touched; t += kPrepThreads) xn[atomicAdd(&s_nx, 1)] = ws.touched[t];
-    }
-    if (tid < nb) {
-        ws.win_hi[tid] = tid >= 1 ? (int32_t)(a.exp_off[start + tid + 1] - e_base) : 0;
-        const int64_t pos = a.exp_pos[start + tid];
-        ws.own[tid] = (pos >= e_base && pos - e_base < e_cnt) ? (int32_t)(pos - e_base) : -1;
-    }
-    int32_t my_node = -1, my_k = -1;
-    if (tid < e_cnt) {
-        const int32_t q = a.exp_pod[e_base + tid];
-        const PodRec& pq = a.pods[q];
-        ws.ex_q[tid] = q;
-        ws.ex_req[tid][0] = pq.req[0]; ws.ex_req[tid][1] = pq.req[1]; ws.ex_req[tid][2] = pq.req[2];
-        const bool ok = q < start && a.b_status[q] == 0 && !a.expired[q];
-        ws.ex_ok[tid] = ok ? 1 : 0;
-        if (ok) my_node = a.b_node[q];
-    }
-    if (my_node >= 0) {
-        uint32_t h = ehslot(my_node);
-        bool claimed = false;
-        for (;;) {  // <= kEMax distinct nodes < kEHash slots: terminates
-            const int32_t prev = atomicCAS(&hk[h], -1, my_node);
-            if (prev == -1) { claimed = true; break; }
-            if (prev == my_node) break;
-            h = (h + 1) & (kEHash - 1);
-        }
-        my_k = (int32_t)h;  // hash slot; the claiming thread numbers the node
-        if (claimed) hv[h] = atomicAdd(&s_ne, 1);
-    }
-    __syncthreads();
-    const int n_es = s_ne;  // the slot nodes; the touched nodes after them (no slots)
-    __syncthreads();
-    const int n_x = s_nx;
-    for (int t = tid; t < n_x; t += kPrepThreads) {
-        const int32_t nd = xn[t];
-        uint32_t h = ehslot(nd);
-        for (;;) {
-            const int32_t prev = atomicCAS(&hk[h], -1, nd);
-            if (prev == -1) { const int k = atomicAdd(&s_ne, 1); hv[h] = k; ws.e_node[k] = nd; break; }
-            if (prev == nd) break;
-            h = (h + 1) & (kEHash - 1);
-        }
-    }
-    __syncthreads();
-    const int n_e = s_ne;
-    if (tid < n_es) { cnt[tid] = 0; fill[tid] = 0; }
-    __syncthreads();
-    int k_of = -1;
-    if (my_node >= 0) {
-        k_of = hv[my_k];
-        ws.e_node[k_of] = my_node;
-        atomicAdd(&cnt[k_of], 1);
-    }
-    __syncthreads();
-    {  // exclusive prefix of the slot nodes' counts (n_es <= kWinSlots: one per thread)
-        __shared__ int32_t wsum[kPrepThreads / 64];
-        const int lane = tid & 63, wv = tid >> 6;
-        const int v = tid < n_es ? cnt[tid] : 0;
-        int incl = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int u = __shfl_up(incl, o);
-            if (lane >= o) incl += u;
-        }
-        if (lane == 63) wsum[wv] = incl;
-        __syncthreads();
-        int base = 0;
-        for (int g = 0; g < wv; ++g) base += wsum[g];
-        if (tid < n_es) ws.e_off[tid] = base + incl - v;
-        if (tid == n_es - 1) ws.e_off[n_es] = base + incl;
-        if (n_es == 0 && tid == 0) ws.e_off[0] = 0;
-    }
-    __syncthreads();
-    if (my_node >= 0) ws.e_slot[ws.e_off[k_of] + atomicAdd(&fill[k_of], 1)] = tid;  // slot x == tid
-    __syncthreads();
-    if (tid < n_es) {  // each node's few slots ascending
-        const int lo = ws.e_off[tid], hi = ws.e_off[tid + 1];
-        for (int u = lo + 1; u < hi; ++u) {
-            const int32_t x = ws.e_slot[u];
-            int v = u - 1;
-            while (v >= lo && ws.e_slot[v] > x) { ws.e_slot[v + 1] = ws.e_slot[v]; --v; }
-            ws.e_slot[v + 1] = x;
-        }
-    }
-    for (int k = tid; k < n_e; k += kPrepThreads) a.e_idx[ws.e_node[k]] = k;
-    if (tid == 0) {
-        ws.nb = nb; ws.e_cnt = e_cnt; ws.n_e = n_e; ws.n_es = n_es; ws.nslot = 0; ws.rescan = rescan;
-        // the next speculative scan: the pods after this batch, if it commits them all
-        spec_out[kCtrStart] = start + nb; spec_out[kCtrEnd] = end; spec_out[kCtrErr] = 0;
-    }
+    __shared__ prep::PrepLDS L;
+    prep::prep_body<kPrepThreads>(a, a.ctr[kCtrStart], a.ctr[kCtrEnd], a.ctr[kCtrErr], head, spec, slot, L);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -23,6 +23,7 @@
 
 #include "ks_device.h"
 #include "ks_scan.h"
+#include "ks_prep.h"
 
 namespace ks {
 namespace chk {
@@ -152,6 +153,7 @@ struct ChShared {
     int16_t ceix[kCid];           // cid -> the node's index in E, -1 if not an E node
     int16_t e2c[kSlots];          // slot-E index -> cid, -1: the E node is no candidate of this batch
     int32_t nbc, cut, fc[2], fs[2];
+    int64_t t_start, t_end, t_err;  // the counters after this launch (chunk_scan_kernel's window prep)
     uint64_t chg;                 // chunk rows (slots c0 + j) rewritten since the last full sweep
 #ifdef KS_CHUNK_DIAG
     int8_t why[kB];  // stop reason of a code-1 decision
@@ -398,7 +400,9 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid >> 6;
     const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
     int nb = ws.nb;
-    if (a.ctr[kCtrErr] != 0 || nb <= 0) return;
+    const int64_t err0 = a.ctr[kCtrErr];
+    if (tid == 0) { sh.t_start = start; sh.t_end = end; sh.t_err = err0; }
+    if (err0 != 0 || nb <= 0) return;
     const int n_e = ws.n_es, n_eall = ws.n_e, e_cnt = ws.e_cnt;  // (n_e: the slot-E nodes)
 
     // ---- setup: pods, window, candidate ids, records.  The candidate ids are the batch's
@@ -1093,6 +1097,8 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
             a.ctr[kCtrErr] = stop_code == 2 ? kErrNotFound : kErrEinval;
             a.ctr[kCtrErrPod] = start + c;
         }
+        sh.t_start = start + c;
+        sh.t_err = err ? 1 : 0;
         if (c < a.B && !err && start + c < end) a.ctr[kCtrEarly] += 1;
     }
 #ifdef KS_CHUNK_DIAG
@@ -1136,12 +1142,20 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
 // node the batch could bind, was measured worse: those nodes then all join the next batch's E,
 // enough of them reach its lists' thresholds to overflow the candidate slots, and the batches
 // commit ~104 pods instead of ~181.)
+// After its commit the resolver workgroup also computes the next batch's window (ks_prep.h, with the
+// head expiries and the touched nodes; `slot`: that batch's speculative-counter parity) in its LDS:
+// the standalone window-prep launch and its kernel boundary leave the critical path.
 template <int kMode>
 __global__ __launch_bounds__(kThreads) void chunk_scan_kernel(const EngineArgs* __restrict__ A,
-                                                              const EngineArgs* __restrict__ As) {
+                                                              const EngineArgs* __restrict__ As, int slot) {
     __shared__ ChShared sh;
     if (blockIdx.x == 0) {
         chunk_body<kMode>(A, sh);
+        __syncthreads();
+        const int64_t st = sh.t_start, en = sh.t_end, er = sh.t_err;
+        __syncthreads();  // (the window's scratch overlays the resolver's LDS)
+        static_assert(sizeof(prep::PrepLDS) <= sizeof(ChShared), "window scratch");
+        prep::prep_body<kThreads>(A[0], st, en, er, 1, 1, slot, *reinterpret_cast<prep::PrepLDS*>(&sh));
         return;
     }
     static_assert(kThreads == 2 * scn::kNodes, "two scan groups per workgroup");
@@ -1171,13 +1185,15 @@ static_assert(sizeof(ChShared) >= 2 * kMaxPGScan * scn::kNodes * sizeof(uint16_t
 
 // the chunk resolver proper (its window and candidate lists: launch_window_prep(head) and
 // launch_merge_cl, ks_cand.hip)
-hipError_t launch_chunk_scan(const EngineArgs* d, const EngineArgs* ds, int workers, int mode, hipStream_t st) {
+hipError_t launch_chunk_scan(const EngineArgs* d, const EngineArgs* ds, int workers, int next_slot, int mode,
+                             hipStream_t st) {
     const dim3 g(1 + workers);
+    const int sl = next_slot & 1;
     switch (mode) {
-        case kEvalMicro: hipLaunchKernelGGL(chk::chunk_scan_kernel<kEvalMicro>, g, dim3(chk::kThreads), 0, st, d, ds); break;
-        case kEvalTiny: hipLaunchKernelGGL(chk::chunk_scan_kernel<kEvalTiny>, g, dim3(chk::kThreads), 0, st, d, ds); break;
-        case kEvalNarrow: hipLaunchKernelGGL(chk::chunk_scan_kernel<kEvalNarrow>, g, dim3(chk::kThreads), 0, st, d, ds); break;
-        default: hipLaunchKernelGGL(chk::chunk_scan_kernel<kEvalWide>, g, dim3(chk::kThreads), 0, st, d, ds); break;
+        case kEvalMicro: hipLaunchKernelGGL(chk::chunk_scan_kernel<kEvalMicro>, g, dim3(chk::kThreads), 0, st, d, ds, sl); break;
+        case kEvalTiny: hipLaunchKernelGGL(chk::chunk_scan_kernel<kEvalTiny>, g, dim3(chk::kThreads), 0, st, d, ds, sl); break;
+        case kEvalNarrow: hipLaunchKernelGGL(chk::chunk_scan_kernel<kEvalNarrow>, g, dim3(chk::kThreads), 0, st, d, ds, sl); break;
+        default: hipLaunchKernelGGL(chk::chunk_scan_kernel<kEvalWide>, g, dim3(chk::kThreads), 0, st, d, ds, sl); break;
     }
     return hipGetLastError();
 }

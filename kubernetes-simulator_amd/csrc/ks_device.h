@@ -650,8 +650,10 @@ int small_resolver_max_nodes();
 // on a second stream beside the chunk kernel (its commit writes the touched nodes)
 hipError_t launch_chunk_only(const EngineArgs* d, int mode, hipStream_t st);
 // the same with the next batch's speculative scan fused in (ds: its arguments; `workers` scan
-// workgroups beside the resolver's; 16-bit key tables, so key16 engines only)
-hipError_t launch_chunk_scan(const EngineArgs* d, const EngineArgs* ds, int workers, int mode, hipStream_t st);
+// workgroups beside the resolver's; 16-bit key tables, so key16 engines only); after its commit the
+// resolver workgroup runs the next batch's window prep (head, spec; next_slot: that batch's parity)
+hipError_t launch_chunk_scan(const EngineArgs* d, const EngineArgs* ds, int workers, int next_slot, int mode,
+                             hipStream_t st);
 // the batch window (expiries of the batch's pods, the node set E): the resolvers' first kernel;
 // head: also apply the expiries due before the batch's first pod (expire_head's work); spec: the
 // batch's lists come from the speculative scan (the touched nodes join E, or a rescan is flagged)

@@ -1203,7 +1203,8 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
             // rescan when they do not fit, ks_cand.hip window_prep_kernel)
             const bool spec = overlap && b > 0;
             if (ev[0]) HIPCHK(e, hipEventRecord(ev[0], st));
-            HIPCHK(e, fused ? ks::launch_window_prep(d, true, spec, (int)(b & 1), st) : ks::launch_expire_head(d, 1, st));
+            // (an overlapped batch's window was computed by the previous chunk kernel after its commit)
+            if (!spec) HIPCHK(e, fused ? ks::launch_window_prep(d, true, false, (int)(b & 1), st) : ks::launch_expire_head(d, 1, st));
             if (ev[1]) HIPCHK(e, hipEventRecord(ev[1], st));
             HIPCHK(e, ks::launch_scan(d, 1, e->blk_n, e->B, e->PG, e->mode, key16(e), st, spec));
             if (ev[2]) HIPCHK(e, hipEventRecord(ev[2], st));
@@ -1238,7 +1239,7 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
             }
             if (ev[3]) HIPCHK(e, hipEventRecord(ev[3], st));
             if (overlap && b + 1 < nbat)  // the resolver with the next batch's scan beside it
-                HIPCHK(e, ks::launch_chunk_scan(d, e->d_args_spec + (b & 1), e->scan_workers, e->mode, st));
+                HIPCHK(e, ks::launch_chunk_scan(d, e->d_args_spec + (b & 1), e->scan_workers, (int)((b + 1) & 1), e->mode, st));
             else
                 HIPCHK(e, fused ? ks::launch_chunk_only(d, e->mode, st) : launch_resolver(d, 1, e->mode, which, st));
             if (ev[4]) HIPCHK(e, hipEventRecord(ev[4], st));

@@ -1,0 +1,176 @@
+// ks_prep.h — a batch's expiry window (gfx950): the body of ks_cand.hip's window_prep_kernel, shared
+// with the chunk kernel, whose resolver workgroup runs it for the next batch right after its commit
+// (ks_chunk.hip chunk_scan_kernel: one launch and one kernel boundary fewer per overlapped batch).
+//
+// The reference binds one pod per tick in FIFO order (kubesim/kubesim.go:105-121); before pod j is
+// scheduled, every pod whose run ended by its tick stops counting toward its node's totals
+// (kubesim/node/node.go:97-118 over kubesim/pod/pod.go:67-69).  Per batch this computes:
+//   * head: the expiries due before the batch's first pod, applied to the node state;
+//   * the window: the expiries attached to pods start+1 .. start+nb-1 (exp_off CSR), one slot each;
+//     the batch shrinks to the largest prefix whose window fits kWinSlots;
+//   * E: the distinct nodes of the window's slots whose pod was bound Ok before the batch and has
+//     not expired (e_idx marks them), and — `spec`, the overlap — the nodes the previous batch
+//     changed (its commit's `touched`) and the head expiries' nodes, with no slots: the batch's
+//     block lists come from the speculative scan that ran beside the previous batch's resolve, on
+//     the node table as it was then — exact for every other node.  The speculative scan covered the
+//     pods after the previous batch; if that batch stopped early (this batch starts elsewhere) or the
+//     changed nodes overflow E, `rescan` asks the conditional scan to redo the lists;
+//   * the speculative counters for the next scan (the pods after this batch), double-buffered by
+//     batch parity `slot`.
+#pragma once
+#include "ks_device.h"
+
+namespace ks {
+namespace prep {
+
+constexpr int kEHashLog2 = 12, kEHash = 1 << kEHashLog2;
+static_assert(2 * kEMax <= kEHash, "E hash load <= 1/2");
+
+__device__ __forceinline__ uint32_t ehslot(int32_t n) { return ((uint32_t)n * 2654435761u) >> (32 - kEHashLog2); }
+
+// LDS scratch of one window prep (~44 KB)
+struct PrepLDS {
+    int32_t hk[kEHash], hv[kEHash];
+    int32_t cnt[kWinSlots], fill[kWinSlots];
+    int32_t xn[kEMax];  // touched nodes to insert (overlap)
+    int32_t wsum[16];
+    int32_t s_ne, s_nx;
+};
+
+// One workgroup of NT threads (tid = threadIdx.x).  start / end / err: the batch's counters (the
+// caller read them; the chunk kernel passes its commit's values through LDS).
+template <int NT>
+__device__ __forceinline__ void prep_body(const EngineArgs& a, int64_t start, int64_t end, int64_t err, int head,
+                                          int spec, int slot, PrepLDS& L) {
+    static_assert(kWinSlots <= NT && kWinMaxB <= NT, "one window slot and one pod per thread");
+    static_assert(NT / 64 <= 16, "wave sums");
+    WinWS& ws = *a.sw;
+    const int tid = threadIdx.x;
+    int64_t* const spec_out = a.spec_ctr + kSpecStride * slot;
+    const int64_t* const spec_in = a.spec_ctr + kSpecStride * (slot ^ 1);
+    int nb = (int)min<int64_t>(min<int64_t>(a.B, kWinMaxB), end - start);
+    if (err != 0 || nb <= 0) {
+        if (tid == 0) {
+            ws.nb = 0; ws.e_cnt = 0; ws.n_e = 0; ws.n_es = 0; ws.rescan = 0;
+            spec_out[kCtrStart] = end; spec_out[kCtrEnd] = end; spec_out[kCtrErr] = 0;
+        }
+        return;
+    }
+    const int64_t e0 = a.exp_off[start], e1 = a.exp_off[start + 1];
+    const int64_t e_base = e1;
+    const bool fits_win = tid < nb && a.exp_off[start + tid + 1] - e_base <= kWinSlots;
+    for (int h = tid; h < kEHash; h += NT) L.hk[h] = -1;
+    if (tid == 0) { L.s_ne = 0; L.s_nx = 0; }
+    nb = __syncthreads_count(fits_win);  // exp_off is non-decreasing: a prefix of the pods
+    const int e_cnt = (int)(a.exp_off[start + nb] - e_base);
+    int rescan = 0;
+    if (spec) rescan = start != spec_in[kCtrStart] || (int64_t)e_cnt + (e1 - e0) + ws.n_touched > kEMax;
+    const bool touch = spec && !rescan;
+    if (head) {  // expire_head's work: the expiries due before the batch's first pod
+        for (int64_t e = e0 + tid; e < e1; e += NT) {
+            const int32_t q = a.exp_pod[e];
+            if (a.b_status[q] != 0 || a.expired[q]) continue;
+            const int32_t nd = a.b_node[q];
+            const PodRec& p = a.pods[q];
+            atomicAdd((unsigned long long*)&a.s.rc[nd], (unsigned long long)(-p.req[0]));
+            atomicAdd((unsigned long long*)&a.s.rm[nd], (unsigned long long)(-p.req[1]));
+            atomicAdd((unsigned long long*)&a.s.rg[nd], (unsigned long long)(-p.req[2]));
+            atomicAdd((unsigned long long*)&a.s.nr[nd], (unsigned long long)(-1ll));
+            a.expired[q] = 1;
+            if (touch) L.xn[atomicAdd(&L.s_nx, 1)] = nd;
+        }
+    }
+    if (touch) {
+        for (int t = tid; t < ws.n_touched; t += NT) L.xn[atomicAdd(&L.s_nx, 1)] = ws.touched[t];
+    }
+    if (tid < nb) {
+        ws.win_hi[tid] = tid >= 1 ? (int32_t)(a.exp_off[start + tid + 1] - e_base) : 0;
+        const int64_t pos = a.exp_pos[start + tid];
+        ws.own[tid] = (pos >= e_base && pos - e_base < e_cnt) ? (int32_t)(pos - e_base) : -1;
+    }
+    int32_t my_node = -1, my_k = -1;
+    if (tid < e_cnt) {
+        const int32_t q = a.exp_pod[e_base + tid];
+        const PodRec& pq = a.pods[q];
+        ws.ex_q[tid] = q;
+        ws.ex_req[tid][0] = pq.req[0]; ws.ex_req[tid][1] = pq.req[1]; ws.ex_req[tid][2] = pq.req[2];
+        const bool ok = q < start && a.b_status[q] == 0 && !a.expired[q];
+        ws.ex_ok[tid] = ok ? 1 : 0;
+        if (ok) my_node = a.b_node[q];
+    }
+    if (my_node >= 0) {
+        uint32_t h = ehslot(my_node);
+        bool claimed = false;
+        for (;;) {  // <= kEMax distinct nodes < kEHash slots: terminates
+            const int32_t prev = atomicCAS(&L.hk[h], -1, my_node);
+            if (prev == -1) { claimed = true; break; }
+            if (prev == my_node) break;
+            h = (h + 1) & (kEHash - 1);
+        }
+        my_k = (int32_t)h;  // hash slot; the claiming thread numbers the node
+        if (claimed) L.hv[h] = atomicAdd(&L.s_ne, 1);
+    }
+    __syncthreads();
+    const int n_es = L.s_ne;  // the slot nodes; the touched nodes after them (no slots)
+    __syncthreads();
+    const int n_x = L.s_nx;
+    for (int t = tid; t < n_x; t += NT) {
+        const int32_t nd = L.xn[t];
+        uint32_t h = ehslot(nd);
+        for (;;) {
+            const int32_t prev = atomicCAS(&L.hk[h], -1, nd);
+            if (prev == -1) { const int k = atomicAdd(&L.s_ne, 1); L.hv[h] = k; ws.e_node[k] = nd; break; }
+            if (prev == nd) break;
+            h = (h + 1) & (kEHash - 1);
+        }
+    }
+    __syncthreads();
+    const int n_e = L.s_ne;
+    if (tid < n_es) { L.cnt[tid] = 0; L.fill[tid] = 0; }
+    __syncthreads();
+    int k_of = -1;
+    if (my_node >= 0) {
+        k_of = L.hv[my_k];
+        ws.e_node[k_of] = my_node;
+        atomicAdd(&L.cnt[k_of], 1);
+    }
+    __syncthreads();
+    {  // exclusive prefix of the slot nodes' counts (n_es <= kWinSlots: one per thread)
+        const int lane = tid & 63, wv = tid >> 6;
+        const int v = tid < n_es ? L.cnt[tid] : 0;
+        int incl = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int u = __shfl_up(incl, o);
+            if (lane >= o) incl += u;
+        }
+        if (lane == 63) L.wsum[wv] = incl;
+        __syncthreads();
+        int base = 0;
+        for (int g = 0; g < wv; ++g) base += L.wsum[g];
+        if (tid < n_es) ws.e_off[tid] = base + incl - v;
+        if (tid == n_es - 1) ws.e_off[n_es] = base + incl;
+        if (n_es == 0 && tid == 0) ws.e_off[0] = 0;
+    }
+    __syncthreads();
+    if (my_node >= 0) ws.e_slot[ws.e_off[k_of] + atomicAdd(&L.fill[k_of], 1)] = tid;  // slot x == tid
+    __syncthreads();
+    if (tid < n_es) {  // each node's few slots ascending
+        const int lo = ws.e_off[tid], hi = ws.e_off[tid + 1];
+        for (int u = lo + 1; u < hi; ++u) {
+            const int32_t x = ws.e_slot[u];
+            int v = u - 1;
+            while (v >= lo && ws.e_slot[v] > x) { ws.e_slot[v + 1] = ws.e_slot[v]; --v; }
+            ws.e_slot[v + 1] = x;
+        }
+    }
+    for (int k = tid; k < n_e; k += NT) a.e_idx[ws.e_node[k]] = k;
+    if (tid == 0) {
+        ws.nb = nb; ws.e_cnt = e_cnt; ws.n_e = n_e; ws.n_es = n_es; ws.nslot = 0; ws.rescan = rescan;
+        // the next speculative scan: the pods after this batch, if it commits them all
+        spec_out[kCtrStart] = start + nb; spec_out[kCtrEnd] = end; spec_out[kCtrErr] = 0;
+    }
+}
+
+}  // namespace prep
+}  // namespace ks
