@@ -106,7 +106,12 @@ enum { KS_ENGINE_FORCE_WIDE = 1, KS_ENGINE_NO_TINY = 2, KS_ENGINE_NO_MICRO = 4,
         * NO_OVERLAP: the chunk resolver's batches run the plain chain (each batch's scan before its
         * resolve) instead of fusing the next batch's speculative scan into the resolve launch — the
         * same binds; for A/B timing and to test the two chains against each other. */
-       KS_ENGINE_ONE_POD_RESOLVER = 8, KS_ENGINE_CHUNK_RESOLVER = 64, KS_ENGINE_NO_OVERLAP = 256 };
+       KS_ENGINE_ONE_POD_RESOLVER = 8, KS_ENGINE_CHUNK_RESOLVER = 64, KS_ENGINE_NO_OVERLAP = 256,
+       /* PRUNED_LISTS: the scan writes a block's top-L list only when it can reach the pod's global
+        * top-L (a running per-pod threshold) and the merge reads only those — the default for chunk-
+        * resolver clusters of >= 1,024 scan blocks (262,144 nodes); the flag forces it at every size
+        * (same binds; to test the two list forms against each other). */
+       KS_ENGINE_PRUNED_LISTS = 512 };
 
 typedef struct {
     int64_t pod;    /* FIFO index (submission order) */

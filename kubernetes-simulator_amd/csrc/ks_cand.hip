@@ -23,6 +23,7 @@
 
 #include "ks_device.h"
 #include "ks_prep.h"
+#include "ks_scan.h"
 
 namespace ks {
 namespace sq {
@@ -168,33 +169,48 @@ __device__ __forceinline__ void cand_list(const EngineArgs& a, WinWS& ws, int i,
 
 // merge + candidate list of pod b in one workgroup (the merge kernel's exact top-L over nl sorted
 // lists lists[b * pod_stride + k * list_stride], ks_kernels.hip, then cand_list) — one launch
-// fewer per batch.  src == nullptr: the engine's own block lists.
+// fewer per batch.  src == nullptr: the engine's own block lists (pruned: only the blocks its
+// bitmap flags, ks_scan.h).  Every launch clears the pods' bitmaps and thresholds for the next scan.
 constexpr int kMergeMaxWaves = 16;
 template <int kMode>
 __global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs* __restrict__ A, const uint64_t* src,
                                                          int64_t pod_stride, int32_t nl, int64_t list_stride) {
     const EngineArgs& a = A[0];
     WinWS& ws = *a.sw;
-    if (src == nullptr) {
+    const bool own = src == nullptr;
+    if (own) {
         src = a.lists;
         pod_stride = (int64_t)a.nblk * kL;
         nl = a.nblk;
         list_stride = kL;
     }
     const int b = blockIdx.x;
-    if (b >= ws.nb) return;  // (the window prep cut the batch; errors left nb = 0)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nthr = blockDim.x, nwav = nthr / kWave;
+    const bool prn = a.lbit != nullptr;
+    const int lset = prn ? ws.lset : 1;
+    const bool pruned = own && prn;
+    // pruned: the flagged blocks of the batch's set (one round trip for the bitmap words); then both
+    // sets' bitmaps and thresholds of pod b are cleared for the next scans (every pod slot: b >= nb too)
+    __shared__ scn::FlagLDS F;
+    int nfl = nl;
+    if (b < ws.nb && pruned) nfl = scn::flagged_index(lbit_of(a, lset, b), 0, nl, F);
+    if (prn) {
+        for (int w = tid; w < 2 * a.nwl; w += nthr) lbit_of(a, w / a.nwl, b)[w % a.nwl] = 0;
+        if (tid < 2 * kThrCopies) *lthr_of(a, tid / kThrCopies, tid % kThrCopies, b) = 0;
+    }
+    if (b >= ws.nb) return;  // (the window prep cut the batch; errors left nb = 0)
     uint64_t top[kL];
 #pragma unroll
     for (int k = 0; k < kL; ++k) top[k] = 0;
     const uint64_t* lists = src + (int64_t)b * pod_stride;
-    const int nthr = blockDim.x, nwav = nthr / kWave;
     // independent reads first: this thread's first block list, then the E nodes' keys (dependent
     // chains: node, slots, expiring requests) while it is in flight
     uint64_t lv0[kL];
-    const bool has0 = tid < nl;
+    const bool has0 = tid < nfl;
     {
-        const ulonglong2* lp = reinterpret_cast<const ulonglong2*>(lists + (int64_t)(has0 ? tid : 0) * list_stride);
+        const int l0 = has0 ? (pruned ? scn::flagged_block(tid, 0, nl, F) : tid) : 0;
+        const ulonglong2* lp = reinterpret_cast<const ulonglong2*>(lists + (int64_t)l0 * list_stride);
 #pragma unroll
         for (int k = 0; k < kL / 2; ++k) {
             const ulonglong2 w = has0 ? lp[k] : make_ulonglong2(0, 0);
@@ -224,7 +240,8 @@ __global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs* __rest
         }
     }
     if (has0) topl_insert(top, lv0);
-    for (int blk = tid + nthr; blk < nl; blk += nthr) {
+    for (int j = tid + nthr; j < nfl; j += nthr) {
+        const int blk = pruned ? scn::flagged_block(j, 0, nl, F) : j;
         const ulonglong2* lp = reinterpret_cast<const ulonglong2*>(lists + (int64_t)blk * list_stride);
         uint64_t lv[kL];
 #pragma unroll

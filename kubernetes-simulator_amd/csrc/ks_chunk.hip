@@ -1145,7 +1145,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
 // After its commit the resolver workgroup also computes the next batch's window (ks_prep.h, with the
 // head expiries and the touched nodes; `slot`: that batch's speculative-counter parity) in its LDS:
 // the standalone window-prep launch and its kernel boundary leave the critical path.
-template <int kMode>
+template <int kMode, bool kPrune>
 __global__ __launch_bounds__(kThreads) void chunk_scan_kernel(const EngineArgs* __restrict__ A,
                                                               const EngineArgs* __restrict__ As, int slot) {
     __shared__ ChShared sh;
@@ -1176,7 +1176,7 @@ __global__ __launch_bounds__(kThreads) void chunk_scan_kernel(const EngineArgs* 
     for (int64_t r = lo + 2 * (int64_t)j; r < hi; r += 2 * (int64_t)nx) {  // (uniform per workgroup)
         if (r != lo + 2 * (int64_t)j) __syncthreads();  // the previous round's extraction has read kv
         const int64_t it = r + half;
-        scn::scan_item<kMode, uint16_t>(a, kv, start, nb, groups, it, it < hi, lt);
+        scn::scan_item<kMode, uint16_t, kPrune>(a, kv, start, nb, groups, it, it < hi, lt, x);
     }
 }
 static_assert(sizeof(ChShared) >= 2 * kMaxPGScan * scn::kNodes * sizeof(uint16_t), "two 16-bit key tables");
@@ -1185,16 +1185,21 @@ static_assert(sizeof(ChShared) >= 2 * kMaxPGScan * scn::kNodes * sizeof(uint16_t
 
 // the chunk resolver proper (its window and candidate lists: launch_window_prep(head) and
 // launch_merge_cl, ks_cand.hip)
-hipError_t launch_chunk_scan(const EngineArgs* d, const EngineArgs* ds, int workers, int next_slot, int mode,
-                             hipStream_t st) {
-    const dim3 g(1 + workers);
-    const int sl = next_slot & 1;
+template <bool kPrune>
+static void launch_chunk_scan_t(const EngineArgs* d, const EngineArgs* ds, const dim3& g, int sl, int mode, hipStream_t st) {
     switch (mode) {
-        case kEvalMicro: hipLaunchKernelGGL(chk::chunk_scan_kernel<kEvalMicro>, g, dim3(chk::kThreads), 0, st, d, ds, sl); break;
-        case kEvalTiny: hipLaunchKernelGGL(chk::chunk_scan_kernel<kEvalTiny>, g, dim3(chk::kThreads), 0, st, d, ds, sl); break;
-        case kEvalNarrow: hipLaunchKernelGGL(chk::chunk_scan_kernel<kEvalNarrow>, g, dim3(chk::kThreads), 0, st, d, ds, sl); break;
-        default: hipLaunchKernelGGL(chk::chunk_scan_kernel<kEvalWide>, g, dim3(chk::kThreads), 0, st, d, ds, sl); break;
+        case kEvalMicro: hipLaunchKernelGGL((chk::chunk_scan_kernel<kEvalMicro, kPrune>), g, dim3(chk::kThreads), 0, st, d, ds, sl); break;
+        case kEvalTiny: hipLaunchKernelGGL((chk::chunk_scan_kernel<kEvalTiny, kPrune>), g, dim3(chk::kThreads), 0, st, d, ds, sl); break;
+        case kEvalNarrow: hipLaunchKernelGGL((chk::chunk_scan_kernel<kEvalNarrow, kPrune>), g, dim3(chk::kThreads), 0, st, d, ds, sl); break;
+        default: hipLaunchKernelGGL((chk::chunk_scan_kernel<kEvalWide, kPrune>), g, dim3(chk::kThreads), 0, st, d, ds, sl); break;
     }
+}
+
+hipError_t launch_chunk_scan(const EngineArgs* d, const EngineArgs* ds, int workers, int next_slot, int mode,
+                             bool prune, hipStream_t st) {
+    const dim3 g(1 + workers);
+    if (prune) launch_chunk_scan_t<true>(d, ds, g, next_slot & 1, mode, st);
+    else launch_chunk_scan_t<false>(d, ds, g, next_slot & 1, mode, st);
     return hipGetLastError();
 }
 

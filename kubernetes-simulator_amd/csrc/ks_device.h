@@ -589,6 +589,7 @@ struct WinWS {
     // be rescanned (the speculative scan covered other pods, or the touched nodes overflow E)
     int32_t touched[kTouchMax];
     int32_t n_touched, rescan;
+    int32_t lset, pad_;                   // pruned lists: the set holding this batch's lists (EngineArgs)
 };
 
 // Arguments of the batch kernels (expire_head / scan / resolve).
@@ -616,7 +617,27 @@ struct EngineArgs {
     int32_t* n_slot;         // [n_pad] node -> its candidate slot in this batch, -1 otherwise
     int64_t* spec_ctr;       // the speculative scan's counters, two sets of kSpecStride (window prep
                              // writes: the next batch if this one commits all its pods)
+    // pruned block lists (ks_scan.h; nullptr: every block writes its whole list): per pod a bitmap of
+    // the blocks that wrote one and a running threshold key, in two sets — [2][B][nwl] u64 and
+    // [2][B]: set 0 written by the overlap's speculative scan (which may still run while the next
+    // batch's window prep decides on a rescan), set 1 by the engine's own scans (plain chain, a
+    // pass's first batch, the rescan).  merge_cl reads the set window prep names (WinWS::lset) and
+    // clears both for the next batch
+    uint64_t* lbit;
+    uint64_t* lthr;
+    int32_t nwl;             // bitmap words per pod: ceil(nblk / 64)
+    int32_t lset;            // the set this argument record's scans write
 };
+// pruned lists: pod b's bitmap / threshold in set `set`
+__host__ __device__ __forceinline__ uint64_t* lbit_of(const EngineArgs& a, int set, int b) {
+    return a.lbit + ((int64_t)set * a.B + b) * a.nwl;
+}
+// thresholds: [2][kThrCopies][B], one copy per XCD-sized group of workgroups (any copy is a valid
+// threshold; plain loads and stores, no contended atomics)
+constexpr int kThrCopies = 8;
+__host__ __device__ __forceinline__ uint64_t* lthr_of(const EngineArgs& a, int set, int copy, int b) {
+    return a.lthr + ((int64_t)set * kThrCopies + copy) * a.B + b;
+}
 
 // Launchers and limits (defined in ks_kernels.hip).  The batch launchers take a device array of
 // S engines' arguments (S = 1 for ks_step, the group's scenarios for ks_group_step).
@@ -628,14 +649,18 @@ hipError_t launch_expire_head(const EngineArgs* d, int S, hipStream_t st);
 // scan of each scenario's blocks [blk_lo, blk_lo + blk_n); grid x = the largest blk_n
 // key16: every total + 1 < 2^16 (scan_kernel's 16-bit key table)
 // cond: only when the window workspace's rescan flag is set (the overlap's fallback)
+// prune: the pruned-list form (the engine's lbit / lthr set, ks_scan.h)
 hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int mode, bool key16, hipStream_t st,
-                       bool cond = false);
+                       bool cond = false, bool prune = false);
 // per scenario and pod b < batch size: exact top-L over nl sorted lists
 // lists[b*pod_stride + k*list_stride] into out (lists == nullptr: the scenario's own block lists
 // into its candidate lists)
 // nl_max: the largest nl of the launch (<= 64 / L candidates per pod: one wave per pod)
+// bits (pruned lists, ks_scan.h; nullptr: read every list): the pods' bitmaps ([B][nwl]); list k of
+// the range is block blk0 + k
 hipError_t launch_merge(const EngineArgs* d, int S, int B, const uint64_t* lists, int64_t pod_stride, int32_t nl,
-                        int64_t list_stride, uint64_t* out, int nl_max, hipStream_t st);
+                        int64_t list_stride, uint64_t* out, int nl_max, hipStream_t st, const uint64_t* bits = nullptr,
+                        int32_t nwl = 0, int32_t blk0 = 0);
 // the role-split resolver (ks_kernels.hip): batches of up to max_batch_pods() pods, any cluster
 hipError_t launch_resolve(const EngineArgs* d, int S, int mode, hipStream_t st);
 // the register-table resolver (ks_resolve.hip): batches of <= small_resolver_max_batch() pods of
@@ -653,7 +678,7 @@ hipError_t launch_chunk_only(const EngineArgs* d, int mode, hipStream_t st);
 // workgroups beside the resolver's; 16-bit key tables, so key16 engines only); after its commit the
 // resolver workgroup runs the next batch's window prep (head, spec; next_slot: that batch's parity)
 hipError_t launch_chunk_scan(const EngineArgs* d, const EngineArgs* ds, int workers, int next_slot, int mode,
-                             hipStream_t st);
+                             bool prune, hipStream_t st);
 // the batch window (expiries of the batch's pods, the node set E): the resolvers' first kernel;
 // head: also apply the expiries due before the batch's first pod (expire_head's work); spec: the
 // batch's lists come from the speculative scan (the touched nodes join E, or a rescan is flagged)

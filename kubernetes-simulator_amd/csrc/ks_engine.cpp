@@ -203,6 +203,11 @@ struct ks_engine {
     std::vector<int> part_lo;  // [world * vsh + 1] block boundaries of the parts
     int blk_lo = 0, blk_n = 0;  // this rank's scan range
     uint64_t* cand_all = nullptr;  // [world * vsh][B][L]
+    // pruned block lists (ks_scan.h): per-pod bitmaps of the blocks that wrote a list and thresholds
+    bool prune = false;
+    uint64_t* lbit = nullptr;  // [B][nwl]
+    uint64_t* lthr = nullptr;  // [2][kThrCopies][B]
+    int nwl = 0;
     int64_t* d_ctr = nullptr;
     int64_t* h_ctr = nullptr;  // pinned
     ks::EngineArgs* d_args = nullptr;  // the kernels' argument record (device)
@@ -285,6 +290,10 @@ ks::EngineArgs make_args(ks_engine* e) {
     a.e_idx = e->d_eidx;
     a.n_slot = e->d_nslot;
     a.spec_ctr = e->d_spec;
+    a.lbit = e->prune ? e->lbit : nullptr;
+    a.lthr = e->prune ? e->lthr : nullptr;
+    a.nwl = e->nwl;
+    a.lset = 1;  // the engine's own scans (the speculative scan's record: set 0, step_body)
     return a;
 }
 
@@ -445,7 +454,7 @@ ks_status engine_init(const ks_config* cfg, ks_engine** out) {
     if (cfg->batch_pods < 0 || cfg->batch_pods > kMaxBatch) return KS_EINVAL;
     if (cfg->engine_flags &
         ~(uint32_t)(KS_ENGINE_FORCE_WIDE | KS_ENGINE_NO_TINY | KS_ENGINE_NO_MICRO | KS_ENGINE_ONE_POD_RESOLVER |
-                    KS_ENGINE_CHUNK_RESOLVER | KS_ENGINE_NO_OVERLAP))
+                    KS_ENGINE_CHUNK_RESOLVER | KS_ENGINE_NO_OVERLAP | KS_ENGINE_PRUNED_LISTS))
         return KS_EINVAL;
     int64_t const_total = 0, w_lr = 0, w_ba = 0;
     for (int i = 0; i < cfg->n_scorers; i++) {
@@ -521,6 +530,8 @@ void engine_free(ks_engine* e) {
     if (e->lists) (void)hipFree(e->lists);
     if (e->cand) (void)hipFree(e->cand);
     if (e->cand_all) (void)hipFree(e->cand_all);
+    if (e->lbit) (void)hipFree(e->lbit);
+    if (e->lthr) (void)hipFree(e->lthr);
     if (e->comm) (void)ncclCommDestroy(e->comm);
     if (e->h_xbuf) (void)hipHostFree(e->h_xbuf);
     if (!e->group) {
@@ -1122,8 +1133,22 @@ static bool tick_step(ks_engine* e, int64_t t_end, ks_bind* out, int64_t cap, in
 
 // The batch window workspace (~0.8 MB) and the node -> E index, allocated on the first step that
 // runs a resolver using them (what-if group members never do).
+// pruned block lists for chunk-resolver engines of >= this many scan blocks (or KS_ENGINE_PRUNED_LISTS)
+#ifndef KS_PRUNE_MIN_BLOCKS
+#define KS_PRUNE_MIN_BLOCKS 1024  // (A/B: make variant NAME=noprune DEFS=-DKS_PRUNE_MIN_BLOCKS=1000000)
+#endif
+constexpr int kPruneMinBlocks = KS_PRUNE_MIN_BLOCKS;
+
 static ks_status ensure_window_ws(ks_engine* e) {
     const int r = resolver_of(e);
+    e->prune = r == kResolveChunk && !e->group && (e->nblk >= kPruneMinBlocks || (e->flags & KS_ENGINE_PRUNED_LISTS));
+    if (e->prune && !e->lbit) {
+        e->nwl = (e->nblk + 63) / 64;
+        HIPCHK(e, hipMalloc(&e->lbit, sizeof(uint64_t) * 2 * (size_t)e->B * e->nwl));  // two sets (EngineArgs)
+        HIPCHK(e, hipMemsetAsync(e->lbit, 0, sizeof(uint64_t) * 2 * (size_t)e->B * e->nwl, e->st));
+        HIPCHK(e, hipMalloc(&e->lthr, sizeof(uint64_t) * 2 * ks::kThrCopies * (size_t)e->B));
+        HIPCHK(e, hipMemsetAsync(e->lthr, 0, sizeof(uint64_t) * 2 * ks::kThrCopies * (size_t)e->B, e->st));
+    }
     if (e->d_sweep || r != kResolveChunk) return KS_OK;
     HIPCHK(e, hipMalloc(&e->d_sweep, sizeof(ks::WinWS)));
     HIPCHK(e, hipMalloc(&e->d_eidx, sizeof(int32_t) * e->n_pad));
@@ -1165,16 +1190,20 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
     const bool fused = which == kResolveChunk;
     HIPCHK(e, hipMemcpyAsync(e->d_ctr, e->h_ctr, 5 * sizeof(int64_t), hipMemcpyHostToDevice, st));
     HIPCHK(e, hipMemcpyAsync(e->d_args, e->h_args, sizeof(ks::EngineArgs), hipMemcpyHostToDevice, st));
-    // the overlap (chunk class, one shard, 16-bit keys, not profiling): batch b + 1's scan fused
-    // into batch b's chunk kernel, over the pods after batch b (the speculative counters window
-    // prep writes).  Large clusters keep the plain chain: their scan is longer than the resolve it
-    // would hide behind (C5: 0.33 vs 0.09 ms), and in the fused kernel it runs one workgroup per CU
-    const bool overlap = fused && e->overlap && e->world * e->vsh == 1 && !e->profiling && e->d_args_spec &&
-                         key16(e) && e->nblk <= 1024;
+    // the overlap (chunk class, 16-bit keys, not profiling): batch b + 1's scan fused into batch b's
+    // chunk kernel, over the pods after batch b (the speculative counters window prep writes) and
+    // this rank's scan blocks.  Sharded engines too: every rank's lists are speculative alike and its
+    // touched nodes (the same on every rank: the resolvers are identical) join E; the exchange runs
+    // every batch whether or not window prep flagged a rescan, so every rank issues the same
+    // collectives.  Ranks scanning many blocks keep the plain chain: their scan is longer than the
+    // resolve it would hide behind (C5 unsharded: 4,096 blocks, 0.33 vs 0.08 ms), and in the fused
+    // kernel it runs one workgroup per CU
+    const bool overlap = fused && e->overlap && !e->profiling && e->d_args_spec && key16(e) && e->blk_n <= 1024;
     if (overlap) {
         for (int k = 0; k < 2; k++) {
             e->h_args_spec[k] = *e->h_args;
             e->h_args_spec[k].ctr = e->d_spec + ks::kSpecStride * k;
+            e->h_args_spec[k].lset = 0;  // pruned lists: the speculative set
         }
         HIPCHK(e, hipMemcpyAsync(e->d_args_spec, e->h_args_spec, 2 * sizeof(ks::EngineArgs), hipMemcpyHostToDevice, st));
     }
@@ -1206,7 +1235,7 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
             // (an overlapped batch's window was computed by the previous chunk kernel after its commit)
             if (!spec) HIPCHK(e, fused ? ks::launch_window_prep(d, true, false, (int)(b & 1), st) : ks::launch_expire_head(d, 1, st));
             if (ev[1]) HIPCHK(e, hipEventRecord(ev[1], st));
-            HIPCHK(e, ks::launch_scan(d, 1, e->blk_n, e->B, e->PG, e->mode, key16(e), st, spec));
+            HIPCHK(e, ks::launch_scan(d, 1, e->blk_n, e->B, e->PG, e->mode, key16(e), st, spec, e->prune));
             if (ev[2]) HIPCHK(e, hipEventRecord(ev[2], st));
             const int G = e->world * e->vsh;
             const int64_t L = ks::kTopL, BL = (int64_t)e->B * L;
@@ -1218,7 +1247,8 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
                     const int p = e->rank * e->vsh + v;
                     const int nlp = e->part_lo[p + 1] - e->part_lo[p];
                     HIPCHK(e, ks::launch_merge(d, 1, e->B, e->lists + (int64_t)e->part_lo[p] * L, (int64_t)e->nblk * L,
-                                               nlp, L, e->cand_all + p * BL, nlp, st));
+                                               nlp, L, e->cand_all + p * BL, nlp, st, e->prune ? e->lbit : nullptr,
+                                               e->nwl, e->part_lo[p]));
                 }
                 if (e->comm) {
                     const ncclResult_t nr = ncclAllGather(e->cand_all + (int64_t)e->rank * e->vsh * BL, e->cand_all,
@@ -1239,7 +1269,8 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
             }
             if (ev[3]) HIPCHK(e, hipEventRecord(ev[3], st));
             if (overlap && b + 1 < nbat)  // the resolver with the next batch's scan beside it
-                HIPCHK(e, ks::launch_chunk_scan(d, e->d_args_spec + (b & 1), e->scan_workers, (int)((b + 1) & 1), e->mode, st));
+                HIPCHK(e, ks::launch_chunk_scan(d, e->d_args_spec + (b & 1), e->scan_workers, (int)((b + 1) & 1), e->mode,
+                                                e->prune, st));
             else
                 HIPCHK(e, fused ? ks::launch_chunk_only(d, e->mode, st) : launch_resolver(d, 1, e->mode, which, st));
             if (ev[4]) HIPCHK(e, hipEventRecord(ev[4], st));

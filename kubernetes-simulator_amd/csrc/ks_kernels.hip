@@ -117,11 +117,11 @@ __global__ __launch_bounds__(256) void expire_head_kernel(const EngineArgs* __re
 // ------------------------------------------------------------------------------------------
 // KT: the key table's word, uint16_t when every total + 1 < 2^16 (the host's check on the scorer
 // weights) — half the LDS per workgroup, so more workgroups fit a CU.
-template <int kMode, typename KT>
+template <int kMode, typename KT, bool kPrune>
 __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict__ A, int xcd, int cond) {
     extern __shared__ uint32_t kv_raw[];
     KT* const kv = reinterpret_cast<KT*>(kv_raw);  // [PG][kBlockNodes]: total+1 per (pod, node of the block)
-    const EngineArgs a = A[blockIdx.z];
+    const EngineArgs& a = A[blockIdx.z];
     // cond: the overlap's fallback scan, needed only when window prep flagged a rescan
     if (cond && *(volatile const int32_t*)&a.sw->rescan == 0) return;
     const int64_t start = sload(a.ctr + kCtrStart), end = sload(a.ctr + kCtrEnd);
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict_
         if ((int)blockIdx.x >= a.blk_n || (int)blockIdx.y >= groups) return;  // scenarios may differ in size
         it_lo = (int64_t)blockIdx.x * groups + blockIdx.y;
     }
-    scn::scan_item<kMode, KT>(a, kv, start, nb, groups, it_lo, true, threadIdx.x);
+    scn::scan_item<kMode, KT, kPrune>(a, kv, start, nb, groups, it_lo, true, threadIdx.x, (int)(blockIdx.x % kThrCopies));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -155,9 +155,11 @@ __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict_
 // all-gathered lists).  src == nullptr: the scenario's own block lists into its candidate lists.
 // ------------------------------------------------------------------------------------------
 constexpr int kMergeMaxWaves = 16;
+// bits != nullptr (a pruned engine's per-part merge, ks_scan.h): only the blocks pod b's bitmap
+// bits[b * nwl ...] flags among blocks [blk0, blk0 + nl) (list k = block blk0 + k) are read
 __global__ __launch_bounds__(1024) void merge_kernel(const EngineArgs* __restrict__ A, const uint64_t* src,
                                                       int64_t pod_stride, int32_t nl, int64_t list_stride,
-                                                      uint64_t* out) {
+                                                      uint64_t* out, const uint64_t* bits, int32_t nwl, int32_t blk0) {
     const EngineArgs a = A[blockIdx.y];
     if (src == nullptr) {
         src = a.lists;
@@ -177,7 +179,13 @@ __global__ __launch_bounds__(1024) void merge_kernel(const EngineArgs* __restric
     for (int k = 0; k < kL; ++k) top[k] = 0;
     const uint64_t* lists = src + (int64_t)b * pod_stride;
     const int nthr = blockDim.x, nwav = nthr / kWave;
-    for (int blk = tid; blk < nl; blk += nthr) {
+    __shared__ scn::FlagLDS F;
+    // (a sharded chunk engine's per-part merge: bits = the two sets, [2][B][nwl]; the batch's set is
+    // the one its window prep named)
+    const int lset = bits && a.sw ? a.sw->lset : 1;
+    const int nfl = bits ? scn::flagged_index(bits + ((int64_t)lset * a.B + b) * nwl, blk0, nl, F) : nl;
+    for (int j = tid; j < nfl; j += nthr) {
+        const int blk = bits ? scn::flagged_block(j, blk0, nl, F) : j;
         // the whole list in one round trip (four 16-byte loads), then the insertions
         const ulonglong2* lp = reinterpret_cast<const ulonglong2*>(lists + (int64_t)blk * list_stride);
         uint64_t lv[kL];
@@ -1105,40 +1113,45 @@ hipError_t launch_expire_head(const EngineArgs* d, int S, hipStream_t st) {
     return hipGetLastError();
 }
 
-template <typename KT>
+template <typename KT, bool kPrune>
 static void launch_scan_t(const EngineArgs* d, const dim3& g, size_t lds, int mode, int xcd, int cond, hipStream_t st) {
     switch (mode) {
-        case kEvalMicro: hipLaunchKernelGGL((scan_kernel<kEvalMicro, KT>), g, dim3(kBlockNodes), lds, st, d, xcd, cond); break;
-        case kEvalTiny: hipLaunchKernelGGL((scan_kernel<kEvalTiny, KT>), g, dim3(kBlockNodes), lds, st, d, xcd, cond); break;
-        case kEvalNarrow: hipLaunchKernelGGL((scan_kernel<kEvalNarrow, KT>), g, dim3(kBlockNodes), lds, st, d, xcd, cond); break;
-        default: hipLaunchKernelGGL((scan_kernel<kEvalWide, KT>), g, dim3(kBlockNodes), lds, st, d, xcd, cond); break;
+        case kEvalMicro: hipLaunchKernelGGL((scan_kernel<kEvalMicro, KT, kPrune>), g, dim3(kBlockNodes), lds, st, d, xcd, cond); break;
+        case kEvalTiny: hipLaunchKernelGGL((scan_kernel<kEvalTiny, KT, kPrune>), g, dim3(kBlockNodes), lds, st, d, xcd, cond); break;
+        case kEvalNarrow: hipLaunchKernelGGL((scan_kernel<kEvalNarrow, KT, kPrune>), g, dim3(kBlockNodes), lds, st, d, xcd, cond); break;
+        default: hipLaunchKernelGGL((scan_kernel<kEvalWide, KT, kPrune>), g, dim3(kBlockNodes), lds, st, d, xcd, cond); break;
     }
 }
 
 hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int mode, bool key16, hipStream_t st,
-                       bool cond) {
+                       bool cond, bool prune) {
     if (blk_n > 0 && S > 0) {
         // one (block, pod group) item per workgroup; one engine: the XCD-aware 1-D deal
         const int groups = (B + PG - 1) / PG;
         const size_t lds = (key16 ? sizeof(uint16_t) : sizeof(uint32_t)) * kBlockNodes * PG;
         const bool xcd = S == 1;
         const dim3 g = xcd ? dim3((unsigned)(((int64_t)blk_n * groups + 7) / 8 * 8), 1, 1) : dim3(blk_n, groups, S);
-        if (key16)
-            launch_scan_t<uint16_t>(d, g, lds, mode, xcd ? 1 : 0, cond ? 1 : 0, st);
-        else
-            launch_scan_t<uint32_t>(d, g, lds, mode, xcd ? 1 : 0, cond ? 1 : 0, st);
+        const int x = xcd ? 1 : 0, c = cond ? 1 : 0;
+        if (key16) {
+            if (prune) launch_scan_t<uint16_t, true>(d, g, lds, mode, x, c, st);
+            else launch_scan_t<uint16_t, false>(d, g, lds, mode, x, c, st);
+        } else {
+            if (prune) launch_scan_t<uint32_t, true>(d, g, lds, mode, x, c, st);
+            else launch_scan_t<uint32_t, false>(d, g, lds, mode, x, c, st);
+        }
     }
     return hipGetLastError();
 }
 
 hipError_t launch_merge(const EngineArgs* d, int S, int B, const uint64_t* lists, int64_t pod_stride, int32_t nl,
-                        int64_t list_stride, uint64_t* out, int nl_max, hipStream_t st) {
-    if ((int64_t)nl_max * kL <= kWave)
+                        int64_t list_stride, uint64_t* out, int nl_max, hipStream_t st, const uint64_t* bits,
+                        int32_t nwl, int32_t blk0) {
+    if ((int64_t)nl_max * kL <= kWave && !bits)
         hipLaunchKernelGGL(merge_small_kernel, dim3((B + 3) / 4, S), dim3(256), 0, st, d, lists, pod_stride, nl,
                            list_stride, out);
     else
         hipLaunchKernelGGL(merge_kernel, dim3(B, S), dim3(nl_max > 1024 ? 1024 : 256), 0, st, d, lists, pod_stride, nl,
-                           list_stride, out);
+                           list_stride, out, bits, nwl, blk0);
     return hipGetLastError();
 }
 

@@ -51,7 +51,7 @@ __device__ __forceinline__ void prep_body(const EngineArgs& a, int64_t start, in
     int nb = (int)min<int64_t>(min<int64_t>(a.B, kWinMaxB), end - start);
     if (err != 0 || nb <= 0) {
         if (tid == 0) {
-            ws.nb = 0; ws.e_cnt = 0; ws.n_e = 0; ws.n_es = 0; ws.rescan = 0;
+            ws.nb = 0; ws.e_cnt = 0; ws.n_e = 0; ws.n_es = 0; ws.rescan = 0; ws.lset = 1;
             spec_out[kCtrStart] = end; spec_out[kCtrEnd] = end; spec_out[kCtrErr] = 0;
         }
         return;
@@ -167,6 +167,7 @@ __device__ __forceinline__ void prep_body(const EngineArgs& a, int64_t start, in
     for (int k = tid; k < n_e; k += NT) a.e_idx[ws.e_node[k]] = k;
     if (tid == 0) {
         ws.nb = nb; ws.e_cnt = e_cnt; ws.n_e = n_e; ws.n_es = n_es; ws.nslot = 0; ws.rescan = rescan;
+        ws.lset = touch ? 0 : 1;  // pruned lists: the speculative scan's set, or the engine's own scan's
         // the next speculative scan: the pods after this batch, if it commits them all
         spec_out[kCtrStart] = start + nb; spec_out[kCtrEnd] = end; spec_out[kCtrErr] = 0;
     }

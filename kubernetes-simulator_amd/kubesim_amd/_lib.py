@@ -25,6 +25,7 @@ KS_ENGINE_NO_MICRO = 4
 KS_ENGINE_ONE_POD_RESOLVER = 8
 KS_ENGINE_CHUNK_RESOLVER = 64
 KS_ENGINE_NO_OVERLAP = 256
+KS_ENGINE_PRUNED_LISTS = 512
 KS_SELFTEST_LR_MICRO = 0
 
 STATUS_NAMES = {KS_OK: "OK", KS_EINVAL: "InvalidArgument", KS_ENOTFOUND: "NotFound",

@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol():
 def test_retired_resolver_flags_rejected_without_device():
     """Bits 16, 32 and 128 were the pair, sweep and sequential resolvers (removed in round 4)."""
     L = _lib.load()
-    for bit in (16, 32, 128, 512):
+    for bit in (16, 32, 128, 1024):
         cfg = _lib.KsConfig()
         cfg.abi_version = _lib.KS_ABI_VERSION
         cfg.tick_seconds = 10

@@ -28,7 +28,7 @@ import pytest
 
 import full_run_digest
 from harness import assert_same_binds, encoded, make_engine, make_oracle
-from kubesim_amd import tracegen
+from kubesim_amd import _lib, tracegen
 
 pytestmark = pytest.mark.gpu
 MODE = "feeds_all_lrba"
@@ -105,7 +105,7 @@ def test_c3_40k_pods_bit_exact_with_usage_samples(c3):
     assert_same_binds(eb, ob)
 
 
-@pytest.mark.parametrize("flags", [0], ids=["default"])
+@pytest.mark.parametrize("flags", [0, _lib.KS_ENGINE_PRUNED_LISTS], ids=["default", "pruned_lists"])
 def test_c3_whole_trace_matches_oracle_golden(c3, flags):
     """Every pod of the 1M-pod trace — the whole range bench.py times — bind-for-bind against the
     oracle's committed digests (tests/golden/full_run.json, tests/golden/make_full_run.py), at

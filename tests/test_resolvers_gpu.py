@@ -14,7 +14,10 @@ from harness import MODES, assert_same_binds, encoded, engine_run, make_engine, 
 from kubesim_amd import _lib, tracegen
 
 pytestmark = pytest.mark.gpu
-RESOLVERS = {"one_pod": _lib.KS_ENGINE_ONE_POD_RESOLVER, "chunk": _lib.KS_ENGINE_CHUNK_RESOLVER}
+RESOLVERS = {"one_pod": _lib.KS_ENGINE_ONE_POD_RESOLVER, "chunk": _lib.KS_ENGINE_CHUNK_RESOLVER,
+             # the chunk resolver on pruned block lists (ks_scan.h: a block writes only keys that can
+             # reach the pod's global top-L; the merge reads the flagged blocks)
+             "chunk_pruned": _lib.KS_ENGINE_CHUNK_RESOLVER | _lib.KS_ENGINE_PRUNED_LISTS}
 
 
 def _run(tr, mode, ticks, batch, flags, chunks):
@@ -105,8 +108,9 @@ def _engine_env(tr, enc, mode, overlap, engine_flags=0, **kw):
     return make_engine(tr, enc, mode, engine_flags=flags, **kw)
 
 
+@pytest.mark.parametrize("pruned", [False, True], ids=["full_lists", "pruned_lists"])
 @pytest.mark.parametrize("case", ["c2", "dense_expiries"])
-def test_overlap_on_and_off_bind_identically_and_match_oracle(case):
+def test_overlap_on_and_off_bind_identically_and_match_oracle(case, pruned):
     """The speculative lists (stale for the nodes the previous batch touched, which join E) and
     the conditional rescan after early stops: the overlapped chain gives the plain chain's binds,
     statuses and usage, and the oracle's."""
@@ -123,7 +127,8 @@ def test_overlap_on_and_off_bind_identically_and_match_oracle(case):
     ob, orc = oracle_run(ora, ticks)
     assert orc == 0
     for overlap in (False, True):  # (the chunk resolver forced: these clusters are the small class)
-        eng = _engine_env(tr, enc, mode, overlap, batch_pods=192, engine_flags=RESOLVERS["chunk"])
+        eng = _engine_env(tr, enc, mode, overlap, batch_pods=192,
+                          engine_flags=RESOLVERS["chunk_pruned" if pruned else "chunk"])
         eng.submit(enc["pods"])
         got = []
         for c in chunks:

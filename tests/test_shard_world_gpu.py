@@ -12,7 +12,7 @@ import pytest
 
 import full_run_digest
 from harness import assert_same_binds, encoded, make_engine, make_oracle, small_trace
-from kubesim_amd import tracegen
+from kubesim_amd import _lib, tracegen
 from kubesim_amd.engine import LocalExchange
 
 pytestmark = pytest.mark.gpu
@@ -73,10 +73,15 @@ def test_ranks_match_oracle_small(world, vshards):
         np.testing.assert_array_equal(e.usage(), ora.usage())
 
 
-def test_c2_prefix_two_ranks_match_oracle():
+@pytest.mark.parametrize("flags", [0, _lib.KS_ENGINE_PRUNED_LISTS, _lib.KS_ENGINE_NO_OVERLAP],
+                         ids=["overlap", "overlap_pruned", "plain_chain"])
+def test_c2_prefix_two_ranks_match_oracle(flags):
+    """C2 on the chunk resolver: by default with the overlap (each rank's speculative scan of its
+    own blocks fused into its chunk kernel, the exchange every batch), also with pruned lists (the
+    per-part merges read only flagged blocks) and on the plain chain."""
     tr = tracegen.c2_trace(n_pods=8000)
     enc = encoded(tr)
-    engs, _x = _ranks(tr, enc, 2, 2)
+    engs, _x = _ranks(tr, enc, 2, 2, engine_flags=flags)
     ora = make_oracle(tr, MODE)
     ora.submit(tr)
     for k in (4096, 3904):
@@ -99,6 +104,27 @@ def test_c5_whole_trace_two_ranks_match_oracle_golden():
     enc = encoded(tr)
     assert g["nodes"] == tr["nodes"]["n"]
     engs, _x = _ranks(tr, enc, 2, 4)
+    done = 0
+    for w, want in enumerate(g["bind_digests"]):
+        k = min(g["window"], g["pods"] - done)
+        bs = _step_all(engs, k, _x)
+        for r, b in enumerate(bs):
+            assert len(b) == k and int(b["pod"][0]) == done
+            assert full_run_digest.bind_digest(b) == want, f"rank {r}: window {w} differs"
+        done += k
+
+
+def test_c5_whole_trace_four_ranks_overlapped_match_oracle_golden():
+    """BASELINE configs[4] as 4 ranks x 2 parts: 1,024 scan blocks per rank, so every rank runs the
+    overlap (its speculative scan fused into its chunk kernel) on pruned lists (1M nodes), with the
+    exchange every batch — every pod of the C5 leg against tests/golden/full_run.json on every
+    rank."""
+    g = full_run_digest.load("c5")
+    if g is None:
+        pytest.skip("no c5 golden")
+    tr = tracegen.c5_trace(n_pods=g["pods"])
+    enc = encoded(tr)
+    engs, _x = _ranks(tr, enc, 4, 2)
     done = 0
     for w, want in enumerate(g["bind_digests"]):
         k = min(g["window"], g["pods"] - done)
