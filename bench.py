@@ -127,19 +127,25 @@ def stream_copy_gbs(device: int, mib: int = 2048, reps: int = 10):
         return None
 
 
-# the kernels of one batch round.  The chunk resolver's chain (ks_step): window prep with the
-# head's expiries -> scan -> merge with the candidate lists -> the chunk kernel; the small-cluster
-# chain: expire_head -> scan -> merge -> resolve_kernel
-BATCH_KERNELS = {"ks::expire_head_kernel": "expire_head", "ks::sq::window_prep_kernel": "expire_head",
-                 "ks::scan_kernel": "scan", "ks::merge_kernel": "merge", "ks::sq::merge_cl_kernel": "merge",
+# the kernels of one batch round (rocprofv3 names -> roles of ks_kernel_stats).  The chunk
+# resolver's chain (ks_step): window prep (a pass's first batch; an overlapped batch's window is
+# computed inside the previous chunk kernel) -> scan (the overlap's conditional rescan, mostly an
+# empty launch) -> merge with the candidate lists -> the chunk kernel, fused with the next batch's
+# speculative scan and window prep ("fused") or alone ("resolve"); the small-cluster chain:
+# expire_head -> scan -> merge -> resolve_kernel
+BATCH_KERNELS = {"ks::expire_head_kernel": "prep", "ks::sq::window_prep_kernel": "prep",
+                 "ks::scan_kernel": "scan", "ks::merge_kernel": "merge", "ks::merge_small_kernel": "merge",
+                 "ks::sq::merge_cl_kernel": "merge",
                  "ks::resolve_kernel": "resolve", "ks::chk::resolve_chunk_kernel": "resolve",
-                 "ks::chk::chunk_scan_kernel": "resolve"}  # (the resolver with the next batch's scan fused in)
+                 "ks::chk::chunk_scan_kernel": "fused"}
+VALU_ISSUE_PER_S = 256 * 4 * 0.5 * 2.4e9  # wave-instructions/s: 256 CUs x 4 SIMDs x 1/2 per cycle x 2.4 GHz
 
 
-def load_traffic(config: str = "c3"):
-    """Measured HBM bytes per launch of each batch kernel (2 x FETCH_SIZE + WRITE_SIZE, the gfx950
-    correction of MI355X_MICROARCH.md §HBM) from the committed PMC summary of this workload
-    (profiles/pmc_<config>.json, made by profiles/collect.sh + profiles/db_summary.py)."""
+def load_pmc(config: str = "c3"):
+    """Per-launch PMC averages of each batch kernel role from the committed summary of this workload
+    (profiles/pmc_<config>.json, made by profiles/collect.sh + profiles/db_summary.py): HBM bytes =
+    2 x FETCH_SIZE + WRITE_SIZE (the gfx950 correction of MI355X_MICROARCH.md §HBM), SQ_INSTS_VALU
+    (wave-instructions, summed over the chip)."""
     p = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
     if not os.path.exists(p):
         return None
@@ -148,56 +154,87 @@ def load_traffic(config: str = "c3"):
     per = {}
     for k, v in d.get("per_kernel", {}).items():
         role = BATCH_KERNELS.get(k)
-        if role and "FETCH_SIZE_KB_avg" in v and "WRITE_SIZE_KB_avg" in v:
-            per[role] = per.get(role, 0) + int((2 * v["FETCH_SIZE_KB_avg"] + v["WRITE_SIZE_KB_avg"]) * 1024)
-    if "scan" not in per:
-        return None
-    return {"per_kernel": per, "per_batch": sum(per.values()), "source": d.get("source", p),
-            "file": os.path.relpath(p, ROOT)}
+        if not role:
+            continue
+        r = per.setdefault(role, {"bytes": 0, "valu": 0.0, "launches": 0})
+        if "FETCH_SIZE_KB_avg" in v and "WRITE_SIZE_KB_avg" in v:
+            r["bytes"] += int((2 * v["FETCH_SIZE_KB_avg"] + v["WRITE_SIZE_KB_avg"]) * 1024)
+        r["valu"] += v.get("SQ_INSTS_VALU_avg", 0.0)
+        r["launches"] += v.get("launches", 0)
+    return {"per_role": per, "source": d.get("source", p), "file": os.path.relpath(p, ROOT)}
 
 
-def roofline_block(value, st, nodes, config, stream_gbs=None):
-    """The roofline object: the path is bound by the resolver's latency (one
-    workgroup walks each batch in FIFO order), so "achieved" is the MEASURED HBM bandwidth of the
-    whole batch chain — PMC bytes per batch round over its device time (HIP events on the
-    engine's stream) — against the 8 TB/s peak; the 80-B-per-evaluation model of SURVEY.md §8(d)
-    is reported beside it as model_gbs / model_frac."""
-    launches = max(st["launches"], 1)
-    pods_per_launch = st["pods"] / launches
-    dev_ms = (st["scan_ms"] + st["resolve_ms"] + st["other_ms"]) / launches
-    scan_ms, res_ms = st["scan_ms"] / launches, st["resolve_ms"] / launches
-    tr = load_traffic(config)
-    model_gbs = value * BYTES_PER_EVAL / 1e9
-    achieved = tr["per_batch"] / (dev_ms * 1e-3) / 1e9 if tr and dev_ms > 0 else None
-    res_ns_pod = st["resolve_ms"] * 1e6 / max(st["pods"], 1)
-    per = tr["per_kernel"] if tr else {}
+def roofline_block(value, st, ks, nodes, config, stream_gbs=None):
+    """The roofline object: one formula, one configuration.
+
+    Every time is a HIP-event average of the profiled step, which runs the same chain as the timed
+    steps (the overlap on); every byte count is the committed PMC summary's per-launch average of
+    the same kernel.  The dominant kernel is the batch kernel with the largest share of device time
+    (C3: the resolve launch — the chunk kernel, fused with the next batch's scan and window prep on
+    most batches, alone on a pass's last; C5 unsharded: the scan).  For it:
+        traffic  = call-share-weighted PMC bytes per launch (2 x FETCH_SIZE + WRITE_SIZE)
+        achieved = traffic / (its summed event ms / its launches)
+        frac     = achieved / 8,000 GB/s
+    beside it the algorithmic model (80 B per (pod, node) evaluation the launch performs, SURVEY.md
+    §8(d): node records are reused across a scan workgroup's pods, so this exceeds the traffic),
+    the scan's VALU-issue fraction (SQ_INSTS_VALU per launch / (1,024 SIMDs x 1/2 x 2.4 GHz x its
+    time)) and the batch round (every kernel's time and bytes per batch)."""
+    batches = max(st["launches"], 1)
+    pods_per_batch = st["pods"] / batches
+    pmc = load_pmc(config)
+    per = pmc["per_role"] if pmc else {}
+    roles = {"prep": (ks["prep_ms"], ks["prep_n"]), "scan": (ks["scan_ms"], ks["scan_n"]),
+             "merge": (ks["merge_ms"], ks["merge_n"]),
+             "resolve": (ks["resolve_ms"] + ks["fused_ms"], ks["resolve_n"] + ks["fused_n"])}
+    dom = max(roles, key=lambda r: roles[r][0])
+    ms_tot, n_dom = roles[dom]
+    t_dom = ms_tot / max(n_dom, 1)
+    if dom == "resolve":
+        n_f, n_r = ks["fused_n"], ks["resolve_n"]
+        b_f, b_r = (per.get("fused") or {}).get("bytes"), (per.get("resolve") or {}).get("bytes")
+        traffic = (n_f * (b_f or 0) + n_r * (b_r or 0)) / max(n_f + n_r, 1) if (b_f or not n_f) and (b_r or not n_r) else None
+        evals = pods_per_batch * nodes * n_f / max(n_f + n_r, 1)   # the fused scans' evaluations
+        name = "resolve launch (chunk kernel; fused with the next batch's speculative scan + window prep)"
+    else:
+        b = (per.get(dom) or {}).get("bytes")
+        traffic = b
+        evals = pods_per_batch * nodes if dom == "scan" else 0
+        name = dom
+    achieved = traffic / (t_dom * 1e-3) / 1e9 if traffic and t_dom > 0 else None
+    alg_gbs = BYTES_PER_EVAL * evals / (t_dom * 1e-3) / 1e9 if t_dom > 0 else None
+    # the scan's VALU issue (standalone scan launches; at C3 with the overlap most are empty rescans,
+    # the fused kernel's SQ_INSTS_VALU is reported with the resolve launch)
+    t_scan = ks["scan_ms"] / max(ks["scan_n"], 1)
+    v_scan = (per.get("scan") or {}).get("valu")
+    v_fused = (per.get("fused") or {}).get("valu")
+    t_fused = ks["fused_ms"] / max(ks["fused_n"], 1)
+    round_ms = sum(v[0] for v in roles.values()) / batches
+    round_bytes = sum((per.get(r) or {}).get("bytes", 0) * roles[r][1] for r in ("prep", "scan", "merge")) / batches
+    round_bytes += ((per.get("fused") or {}).get("bytes", 0) * ks["fused_n"] +
+                    (per.get("resolve") or {}).get("bytes", 0) * ks["resolve_n"]) / batches
     return {
-        "bound": "latency (resolver: one workgroup per batch reaches the FIFO-sequential binds by chunked "
-                 "Jacobi sweeps, barrier-separated rounds)",
+        "bound": "latency" if dom == "resolve" else "VALU issue",
+        "kernel": name,
         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": achieved / HBM_PEAK_GBS if achieved is not None else None,
-        "traffic": tr["per_batch"] if tr else None,
-        "traffic_note": "HBM bytes per batch round (expire_head + scan + merge + resolve), PMC "
-                        "2 x FETCH_SIZE + WRITE_SIZE" + (f" from {tr['file']}" if tr else " (no PMC summary)"),
-        "batch_device_ms": dev_ms, "pods_per_batch": pods_per_launch,
-        "model_gbs": model_gbs, "model_frac": model_gbs / HBM_PEAK_GBS,
-        "model": "80 B per (pod, node) evaluation (SURVEY.md 8(d)) x evals/s; node records are reused "
-                 "across a scan workgroup's pods, so the model exceeds the measured traffic",
+        "traffic": traffic,
+        "formula": "frac = traffic / (event ms per launch) / 8000 GB/s; traffic = call-share-weighted PMC "
+                   "(2 x FETCH_SIZE + WRITE_SIZE) per launch" + (f" from {pmc['file']}" if pmc else " (no PMC summary)"),
+        "launch_ms": t_dom, "launches_per_batch": n_dom / batches,
+        "algorithmic_bytes": BYTES_PER_EVAL * evals, "algorithmic_gbs": alg_gbs,
+        "algorithmic_frac": alg_gbs / HBM_PEAK_GBS if alg_gbs is not None else None,
+        "model": "80 B per (pod, node) evaluation the launch performs (SURVEY.md 8(d)); node records are "
+                 "reused across a scan workgroup's pods (L2 / Infinity Cache), so it exceeds the traffic",
         "stream_copy_gbs": stream_gbs,
-        "model_frac_of_stream_copy": model_gbs / stream_gbs if stream_gbs else None,
-        "kernels": {
-            "scan": {"ms": scan_ms, "hbm_bytes": per.get("scan"),
-                     "gbs": per["scan"] / (scan_ms * 1e-3) / 1e9 if per.get("scan") and scan_ms > 0 else None,
-                     "model_bytes": BYTES_PER_EVAL * pods_per_launch * nodes,
-                     "bound": "VALU issue: fused Filter+Score evaluations + top-L extraction per 256-node "
-                              "block (SQ counters in profiles/)"},
-            "resolve": {"ms": res_ms, "hbm_bytes": per.get("resolve"), "ns_per_pod": res_ns_pod,
-                        "cycles_per_pod_at_2_4ghz": res_ns_pod * 2.4,
-                        "share_of_device_time": res_ms / dev_ms if dev_ms > 0 else None,
-                        "bound": "latency: barrier-separated sweep rounds in one workgroup (window prep + "
-                                 "candidate lists + chunk kernel)"},
-            "merge_and_expire_head": {"ms": st["other_ms"] / launches,
-                                      "hbm_bytes": (per.get("merge") or 0) + (per.get("expire_head") or 0) or None},
+        "scan_valu_frac": v_scan / (VALU_ISSUE_PER_S * t_scan * 1e-3) if v_scan and t_scan > 0 else None,
+        "fused_valu_frac": v_fused / (VALU_ISSUE_PER_S * t_fused * 1e-3) if v_fused and ks["fused_n"] else None,
+        "batch_round": {
+            "ms": round_ms, "pods": pods_per_batch, "hbm_bytes": round_bytes or None,
+            "gbs": round_bytes / (round_ms * 1e-3) / 1e9 if round_bytes and round_ms > 0 else None,
+            "kernels": {r: {"ms_per_launch": v[0] / max(v[1], 1), "launches_per_batch": v[1] / batches,
+                            "hbm_bytes_per_launch": (per.get(r) or {}).get("bytes")}
+                        for r, v in {**roles, "resolve": (ks["resolve_ms"], ks["resolve_n"]),
+                                     "fused": (ks["fused_ms"], ks["fused_n"])}.items()},
         },
     }
 
@@ -300,6 +337,7 @@ def main():
     eng.set_profiling(True)
     eng.step(S)
     st = eng.last_step_stats()
+    kst = eng.last_step_kernels()
     eng.set_profiling(False)
     # per-tick node usage: ks_usage_at = zero + usage kernel over the pod
     # blocks that may run at t (run-interval index) + the [N][3] copy; the digest covers every
@@ -358,11 +396,11 @@ def main():
                        "parallelism": "replicas" if world > 1 else "single-gpu",
                        "batch_pods": args.batch or 192},
             "pods_per_s": pods_per_s,
-            "roofline": roofline_block(value, st, nodes, "c3", stream_copy_gbs(local)),
+            "roofline": roofline_block(value, st, kst, nodes, "c3", stream_copy_gbs(local)),
             "kernels": {"launches_per_step": launches, "pods_per_launch": pods_per_launch,
                         "scan_avg_ms": scan_avg_ms, "resolve_avg_ms": res_avg_ms,
                         "other_avg_ms": other_avg_ms,
-                        "profiled_step_ms": st["step_ms"]},
+                        "profiled_step_ms": st["step_ms"], "per_kernel": kst},
             "usage_query": {"ms_per_call": usage_ms, "nodes": nodes, "tick": t_now,
                             "digest_ms": digest_ms, "digest_ticks": S,
                             "note": "ks_usage_at wall time at ticks near the end of the run, incl. the "
@@ -661,6 +699,7 @@ def _c5_leg_body(args, rank, world, local, dist, steps=None, warmup=1):
     eng.set_profiling(True)
     eng.step(S)
     st = eng.last_step_stats()
+    kst = eng.last_step_kernels()
     eng.set_profiling(False)
     eng.close()
     if rank != 0:
@@ -680,8 +719,9 @@ def _c5_leg_body(args, rank, world, local, dist, steps=None, warmup=1):
                    "batch_pods": args.batch or 192},
         "kernels": {"launches_per_step": launches, "pods_per_launch": st["pods"] / launches,
                     "scan_avg_ms": st["scan_ms"] / launches, "resolve_avg_ms": st["resolve_ms"] / launches,
-                    "other_avg_ms": st["other_ms"] / launches, "profiled_step_ms": st["step_ms"]},
-        "roofline": roofline_block(binds * nodes / t_el, st, nodes, "c5"),
+                    "other_avg_ms": st["other_ms"] / launches, "profiled_step_ms": st["step_ms"],
+                    "per_kernel": kst},
+        "roofline": roofline_block(binds * nodes / t_el, st, kst, nodes, "c5"),
     }
 
 

@@ -275,6 +275,17 @@ typedef struct {
     double other_ms;
 } ks_step_stats;
 ks_status ks_last_step_stats(const ks_engine* eng, ks_step_stats* out);
+/* The same per kernel of the batch chain (profiling on): summed HIP-event ms and launch counts of
+ * the window prep (launched for a pass's first batch and on the plain chain; an overlapped batch's
+ * window is computed inside the previous chunk kernel), the scan (the overlap's conditional rescan
+ * included, mostly an empty launch), the list merge (with the candidate lists, a sharded engine's
+ * per-part merges and exchange), and the resolve launch — the chunk kernel alone, or fused with the
+ * next batch's speculative scan and window prep. */
+typedef struct {
+    double prep_ms, scan_ms, merge_ms, resolve_ms, fused_ms;
+    int64_t prep_n, scan_n, merge_n, resolve_n, fused_n;
+} ks_kernel_stats;
+ks_status ks_last_step_kernels(const ks_engine* eng, ks_kernel_stats* out);
 ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, int64_t* n_out,
                         int32_t* status_out, ks_step_stats* stats);
 /* Device counters (diagnostics): [0] next pod, [1] step end, [2] error, [3] error pod,

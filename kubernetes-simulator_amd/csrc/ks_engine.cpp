@@ -224,6 +224,7 @@ struct ks_engine {
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     std::vector<hipEvent_t> prof_ev;
     ks_step_stats stats{};
+    ks_kernel_stats kstats{};
 
     // scratch for queries
     uint8_t* d_mask = nullptr;
@@ -963,6 +964,7 @@ bool step_prepare(ks_engine* e, int64_t ticks, int64_t* p_hi_out) {
                          e->h_bind_tick.begin();
     *p_hi_out = p_hi;
     e->stats = ks_step_stats{};
+    e->kstats = ks_kernel_stats{};
     e->h_ctr[0] = e->done;
     e->h_ctr[1] = std::max(p_hi, e->done);
     e->h_ctr[2] = 0;
@@ -1198,7 +1200,8 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
     // collectives.  Ranks scanning many blocks keep the plain chain: their scan is longer than the
     // resolve it would hide behind (C5 unsharded: 4,096 blocks, 0.33 vs 0.08 ms), and in the fused
     // kernel it runs one workgroup per CU
-    const bool overlap = fused && e->overlap && !e->profiling && e->d_args_spec && key16(e) && e->blk_n <= 1024;
+    // (profiling keeps it: the per-kernel events bracket the same launches)
+    const bool overlap = fused && e->overlap && e->d_args_spec && key16(e) && e->blk_n <= 1024;
     if (overlap) {
         for (int k = 0; k < 2; k++) {
             e->h_args_spec[k] = *e->h_args;
@@ -1212,6 +1215,8 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
     int64_t start = e->done;
     int64_t launches = 0;
     double scan_ms = 0, res_ms = 0;
+    ks_kernel_stats ks{};
+    std::vector<uint8_t> kind;  // per launch: 1 window prep launched, 2 fused resolve
     while (true) {
         const int64_t nbat = (p_hi - start + e->B - 1) / e->B;
         for (int64_t b = 0; b < nbat; b++) {
@@ -1274,6 +1279,7 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
             else
                 HIPCHK(e, fused ? ks::launch_chunk_only(d, e->mode, st) : launch_resolver(d, 1, e->mode, which, st));
             if (ev[4]) HIPCHK(e, hipEventRecord(ev[4], st));
+            if (e->profiling) kind.push_back((uint8_t)((!spec ? 1 : 0) | (overlap && b + 1 < nbat ? 2 : 0)));
             launches++;
         }
         HIPCHK(e, hipMemcpyAsync(e->h_ctr, e->d_ctr, 5 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
@@ -1304,8 +1310,14 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
             other_ms += t[0] + t[2];
             scan_ms += t[1];
             res_ms += t[3];
+            ks.prep_ms += t[0]; ks.prep_n += kind[l] & 1;
+            ks.scan_ms += t[1]; ks.scan_n += 1;
+            ks.merge_ms += t[2]; ks.merge_n += 1;
+            if (kind[l] & 2) { ks.fused_ms += t[3]; ks.fused_n += 1; }
+            else { ks.resolve_ms += t[3]; ks.resolve_n += 1; }
         }
     }
+    e->kstats = ks;
     e->stats.step_ms = ms;
     e->stats.scan_ms = scan_ms;
     e->stats.resolve_ms = res_ms;
@@ -1842,6 +1854,12 @@ const char* ks_last_error(const ks_engine* e) { return e ? e->errmsg.c_str() : "
 ks_status ks_last_step_stats(const ks_engine* e, ks_step_stats* out) {
     if (!e || !out) return KS_EINVAL;
     *out = e->stats;
+    return KS_OK;
+}
+
+ks_status ks_last_step_kernels(const ks_engine* e, ks_kernel_stats* out) {
+    if (!e || !out) return KS_EINVAL;
+    *out = e->kstats;
     return KS_OK;
 }
 

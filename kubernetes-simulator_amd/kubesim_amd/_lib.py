@@ -34,7 +34,7 @@ STATUS_NAMES = {KS_OK: "OK", KS_EINVAL: "InvalidArgument", KS_ENOTFOUND: "NotFou
 # every symbol include/*.h declares
 EXPORTED_SYMBOLS = ("ks_create", "ks_destroy", "ks_load_nodes", "ks_submit_pods", "ks_step",
                     "ks_filter", "ks_score", "ks_usage", "ks_current_tick", "ks_tick_seconds", "ks_queued_pods",
-                    "ks_last_error", "ks_last_step_stats", "ks_set_profiling", "ks_debug_counters", "ks_selftest",
+                    "ks_last_error", "ks_last_step_stats", "ks_last_step_kernels", "ks_set_profiling", "ks_debug_counters", "ks_selftest",
                     "ks_comm_unique_id", "ks_shard", "ks_shard_host", "ks_group_create", "ks_group_destroy",
                     "ks_group_add", "ks_group_size", "ks_group_step", "ks_pod_status",
                     "ks_usage_at", "ks_usage_digest", "ks_node_mix", "ks_pod_lookup", "ks_node_pods",
@@ -75,6 +75,12 @@ KS_PHASE_PENDING, KS_PHASE_RUNNING, KS_PHASE_SUCCEEDED, KS_PHASE_FAILED = 0, 1, 
 class KsStepStats(C.Structure):
     _fields_ = [("step_ms", C.c_double), ("scan_ms", C.c_double), ("resolve_ms", C.c_double),
                 ("launches", C.c_int64), ("pods", C.c_int64), ("other_ms", C.c_double)]
+
+
+class KsKernelStats(C.Structure):
+    _fields_ = [("prep_ms", C.c_double), ("scan_ms", C.c_double), ("merge_ms", C.c_double),
+                ("resolve_ms", C.c_double), ("fused_ms", C.c_double), ("prep_n", C.c_int64),
+                ("scan_n", C.c_int64), ("merge_n", C.c_int64), ("resolve_n", C.c_int64), ("fused_n", C.c_int64)]
 
 
 class KsPods(C.Structure):
@@ -160,6 +166,8 @@ def load():
     L.ks_last_error.restype = C.c_char_p
     L.ks_last_step_stats.argtypes = [p, C.POINTER(KsStepStats)]
     L.ks_last_step_stats.restype = C.c_int
+    L.ks_last_step_kernels.argtypes = [p, C.POINTER(KsKernelStats)]
+    L.ks_last_step_kernels.restype = C.c_int
     L.ks_debug_counters.argtypes = [p, p]
     L.ks_debug_counters.restype = C.c_int
     L.ks_set_profiling.argtypes = [p, C.c_int]

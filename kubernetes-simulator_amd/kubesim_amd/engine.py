@@ -233,6 +233,12 @@ class Engine:
         return dict(step_ms=s.step_ms, scan_ms=s.scan_ms, resolve_ms=s.resolve_ms, launches=s.launches,
                     pods=s.pods, other_ms=s.other_ms)
 
+    def last_step_kernels(self):
+        """Per-kernel event times of the last profiled step (include/ks_engine.h ks_kernel_stats)."""
+        s = _lib.KsKernelStats()
+        self._check(self._L.ks_last_step_kernels(self.h, C.byref(s)))
+        return {f: getattr(s, f) for f, _ in s._fields_}
+
     def debug_counters(self):
         out = np.zeros(32, np.int64)
         self._check(self._L.ks_debug_counters(self.h, _p(out)))
