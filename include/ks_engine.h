@@ -280,10 +280,12 @@ ks_status ks_last_step_stats(const ks_engine* eng, ks_step_stats* out);
  * window is computed inside the previous chunk kernel), the scan (the overlap's conditional rescan
  * included, mostly an empty launch), the list merge (with the candidate lists, a sharded engine's
  * per-part merges and exchange), and the resolve launch — the chunk kernel alone, or fused with the
- * next batch's speculative scan and window prep. */
+ * next batch's speculative scan and window prep.  Sharded engines: part_ms = the per-part merges
+ * and xchg_ms = the exchange (RCCL all-gather, or the host exchange's copies, callback and wait),
+ * both inside merge_ms, xchg_n batches. */
 typedef struct {
-    double prep_ms, scan_ms, merge_ms, resolve_ms, fused_ms;
-    int64_t prep_n, scan_n, merge_n, resolve_n, fused_n;
+    double prep_ms, scan_ms, merge_ms, resolve_ms, fused_ms, part_ms, xchg_ms;
+    int64_t prep_n, scan_n, merge_n, resolve_n, fused_n, xchg_n;
 } ks_kernel_stats;
 ks_status ks_last_step_kernels(const ks_engine* eng, ks_kernel_stats* out);
 ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, int64_t* n_out,

@@ -56,7 +56,7 @@ constexpr int64_t kStageMaxPods = 4096;  // submits of up to this many pods are 
 #ifndef KS_PG_MIN_WG
 #define KS_PG_MIN_WG 2048  // scan workgroups to keep when raising the pods per workgroup
 #endif
-constexpr int kProfEv = 5;  // per launch: expire_head | scan | merge (+exchange) | resolve
+constexpr int kProfEv = 7;  // per launch: prep | scan | part merges | exchange | merge | resolve
 constexpr int64_t kNever = std::numeric_limits<int64_t>::max();
 constexpr int64_t kUBlk = 256;   // usage index: pods per block (= the usage kernels' workgroup)
 constexpr int64_t kUSup = 64;    // blocks per super block
@@ -1243,6 +1243,7 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
             HIPCHK(e, ks::launch_scan(d, 1, e->blk_n, e->B, e->PG, e->mode, key16(e), st, spec, e->prune));
             if (ev[2]) HIPCHK(e, hipEventRecord(ev[2], st));
             const int G = e->world * e->vsh;
+            hipEvent_t evx[2] = {ev[5], ev[6]};  // part merges | exchange | merge (sharded engines)
             const int64_t L = ks::kTopL, BL = (int64_t)e->B * L;
             if (G == 1) {
                 HIPCHK(e, fused ? ks::launch_merge_cl(d, e->mode, e->B, nullptr, 0, 0, 0, e->nblk, st)
@@ -1255,6 +1256,7 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
                                                nlp, L, e->cand_all + p * BL, nlp, st, e->prune ? e->lbit : nullptr,
                                                e->nwl, e->part_lo[p]));
                 }
+                if (evx[0]) HIPCHK(e, hipEventRecord(evx[0], st));
                 if (e->comm) {
                     const ncclResult_t nr = ncclAllGather(e->cand_all + (int64_t)e->rank * e->vsh * BL, e->cand_all,
                                                           (size_t)e->vsh * BL, ncclUint64, e->comm, st);
@@ -1269,6 +1271,7 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
                     HIPCHK(e, hipMemcpyAsync(e->cand_all, e->h_xbuf, sizeof(uint64_t) * slice * e->world,
                                              hipMemcpyHostToDevice, st));
                 }
+                if (evx[1]) HIPCHK(e, hipEventRecord(evx[1], st));
                 HIPCHK(e, fused ? ks::launch_merge_cl(d, e->mode, e->B, e->cand_all, L, G, BL, G, st)
                                 : ks::launch_merge(d, 1, e->B, e->cand_all, L, G, BL, e->cand, G, st));
             }
@@ -1279,7 +1282,7 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
             else
                 HIPCHK(e, fused ? ks::launch_chunk_only(d, e->mode, st) : launch_resolver(d, 1, e->mode, which, st));
             if (ev[4]) HIPCHK(e, hipEventRecord(ev[4], st));
-            if (e->profiling) kind.push_back((uint8_t)((!spec ? 1 : 0) | (overlap && b + 1 < nbat ? 2 : 0)));
+            if (e->profiling) kind.push_back((uint8_t)((!spec ? 1 : 0) | (overlap && b + 1 < nbat ? 2 : 0) | (G > 1 ? 4 : 0)));
             launches++;
         }
         HIPCHK(e, hipMemcpyAsync(e->h_ctr, e->d_ctr, 5 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
@@ -1304,9 +1307,16 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
     double other_ms = 0;
     if (e->profiling) {
         for (int64_t l = 0; l < launches; l++) {
-            float t[kProfEv - 1] = {};
-            for (int k = 0; k + 1 < kProfEv; k++)
-                (void)hipEventElapsedTime(&t[k], e->prof_ev[kProfEv * l + k], e->prof_ev[kProfEv * l + k + 1]);
+            float t[4] = {};
+            hipEvent_t* E = &e->prof_ev[kProfEv * l];
+            for (int k = 0; k < 4; k++) (void)hipEventElapsedTime(&t[k], E[k], E[k + 1]);
+            if (kind[l] & 4) {  // sharded: [2, 5) part merges, [5, 6) exchange, [6, 3) merge
+                float pm = 0, xc = 0;
+                (void)hipEventElapsedTime(&pm, E[2], E[5]);
+                (void)hipEventElapsedTime(&xc, E[5], E[6]);
+                ks.part_ms += pm; ks.xchg_ms += xc;
+                ks.xchg_n += 1;
+            }
             other_ms += t[0] + t[2];
             scan_ms += t[1];
             res_ms += t[3];
