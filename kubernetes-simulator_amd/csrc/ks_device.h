@@ -406,6 +406,88 @@ __host__ __device__ __forceinline__ uint32_t eval_total1_micro(const Cfg& c, con
     return ok ? total1 : 0u;
 }
 
+// ---------------------------------------------------------------------------------------------
+// The scan's form of the micro evaluator.  A scan workgroup evaluates every pod of its group on
+// its node, so whatever depends on the pod only is computed once per pod on the host instead of
+// in every wave: the requests clamped to the micro range, the Filter's per-key tests folded into
+// biased requests, the tolerations complemented, the disabled filters neutralised.  The scalar
+// work per (pod, wave) drops from ~38 to a handful of instructions (the scan issues on one scalar
+// unit per CU beside four SIMDs: C5 scan 0.31 -> 0.26 ms for the clamp and key tests alone), and
+// the filters combine as integers in VALU instead of as lane masks.  Results are those of
+// eval_total1_micro bit for bit (tests/test_evaluator_host.py):
+//   fit (node.go:44-47): every requested key k satisfies f_k = (A_k - r_k) - q_k >= 0 and
+//     nr < ap  <=>  min(f_c', f_m', f_g', npen) >= 0 with f_k' = (A_k - r_k) - qf_k, qf_k = q_k
+//     for a requested key and -2^30 otherwise (f_k' > 0: A_k - r_k >= -1 - 2^16), npen = -1 when
+//     nr >= ap (or no scorer, or every node fails), else 0; fit filter off: qf_k = -2^30, npen 0;
+//   taint / selector: (taint & ~tol) | (sel & ~label) == 0, ntol = ~tol (0: taint filter off),
+//     sel (0: selector filter off).
+struct alignas(8) ScanRec {
+    int32_t qc, qm;          // clamp_micro(req) (0 for an absent key, as PodRec)
+    int32_t qfc, qfm, qfg;   // the fit test's requests (above)
+    int32_t pad_;
+    uint64_t ntol, sel;
+};
+static_assert(sizeof(ScanRec) == 40, "ScanRec layout");
+constexpr int32_t kFitPass = -(1 << 30);
+
+__host__ __device__ __forceinline__ ScanRec scan_rec_micro(const Cfg& c, const PodRec& p) {
+    const bool fit_on = c.filter_feeds && (c.filters & kFilterFit);
+    const bool taint_on = c.filter_feeds && (c.filters & kFilterTaint);
+    const bool sel_on = c.filter_feeds && (c.filters & kFilterSelector);
+    ScanRec r{};
+    r.qc = clamp_micro(p.req[0]);
+    r.qm = clamp_micro(p.req[1]);
+    const int32_t qg = clamp_micro(p.req[2]);
+    r.qfc = fit_on && (p.keymask & 1) ? r.qc : kFitPass;
+    r.qfm = fit_on && (p.keymask & 2) ? r.qm : kFitPass;
+    r.qfg = fit_on && (p.keymask & 4) ? qg : kFitPass;
+    r.ntol = taint_on ? ~p.tol : 0ull;
+    r.sel = sel_on ? p.sel : 0ull;
+    return r;
+}
+
+// npen: -1 when no pod can make the node a candidate (no scorer, or the fit filter on and nr >= ap)
+template <class NS>
+__host__ __device__ __forceinline__ int32_t scan_npen(const Cfg& c, const NS& n) {
+    const bool fit_on = c.filter_feeds && (c.filters & kFilterFit);
+    return (!c.has_scorers || (fit_on && !(n.nr < n.ap))) ? -1 : 0;
+}
+
+template <class NS>
+__host__ __device__ __forceinline__ uint32_t eval_scan_micro(const Cfg& c, const ScanRec& p, const NS& n, int32_t npen) {
+    const int32_t ac = (int32_t)n.ac, am = (int32_t)n.am, ag = (int32_t)n.ag;
+    const int32_t bc = ac - (int32_t)n.rc, bm = am - (int32_t)n.rm, bg = ag - (int32_t)n.rg;  // per node
+    const int32_t fc = bc - p.qc, fm = bm - p.qm;
+    const int32_t f1 = bc - p.qfc, f2 = bm - p.qfm, f3 = bg - p.qfg;
+    int32_t fmin = f1 < f2 ? f1 : f2;
+    fmin = fmin < f3 ? fmin : f3;
+    fmin = fmin < npen ? fmin : npen;
+    const uint32_t nt_lo = (uint32_t)n.taint, nt_hi = (uint32_t)(n.taint >> 32);
+    const uint32_t nl_lo = ~(uint32_t)n.label, nl_hi = ~(uint32_t)(n.label >> 32);
+    uint32_t bad = (nt_lo & (uint32_t)p.ntol) | (nt_hi & (uint32_t)(p.ntol >> 32));
+    bad |= (nl_lo & (uint32_t)p.sel) | (nl_hi & (uint32_t)(p.sel >> 32));
+    bad |= (uint32_t)(fmin >> 31);
+    const int32_t acs = ac > 0 ? ac : 1, ams = am > 0 ? am : 1;
+    const float iac = micro_ic(n, acs), iam = micro_im(n, ams);  // node-invariant: hoisted
+    const float rc10 = 10.f * iac, rm10 = 10.f * iam;
+    const float fcf = (float)fc, fmf = (float)fm;  // exact: |f| < 2^24
+    const int32_t lc0 = (int32_t)fmaf(fcf, rc10, kMicroBias), lm0 = (int32_t)fmaf(fmf, rm10, kMicroBias);
+    const uint32_t lrs = (uint32_t)((lc0 > 0 ? lc0 : 0) + (lm0 > 0 ? lm0 : 0)) >> 1;
+    const bool ba_on = (fc < fm ? fc : fm) > 0;
+    const uint32_t D = (uint32_t)micro_d(n, acs, ams);
+    const uint32_t a = umad24((uint32_t)fm, (uint32_t)acs, 0u), b = umad24((uint32_t)fc, (uint32_t)ams, 0u);
+    const uint32_t X = usad(a, b);
+    const uint32_t N = umad24(D - X, 10u, 0u);
+    int32_t q = (int32_t)(10.f - fabsf(fmaf(fmf, rm10, -fcf * rc10)));
+    q = q < 0 ? 0 : (q > 10 ? 10 : q);
+    const uint32_t t = umad24((uint32_t)q, D, 0u);
+    q += (N >= t + D) ? 1 : 0;
+    q -= (N < t) ? 1 : 0;
+    const uint32_t base = umad24((uint32_t)c.w_lr, lrs, (uint32_t)c.const_total + 1u);
+    const uint32_t total1 = umad24((uint32_t)c.w_ba, ba_on ? (uint32_t)q : 0u, base);
+    return bad == 0 ? total1 : 0u;
+}
+
 // Evaluator variants: 0 wide (64/128-bit), 1 narrow (capacities < 2^29), 2 tiny, 3 micro (above).
 // A larger value is a narrower domain; each evaluator is exact on every narrower domain.
 enum : int { kEvalWide = 0, kEvalNarrow = 1, kEvalTiny = 2, kEvalMicro = 3 };
@@ -627,6 +709,7 @@ struct EngineArgs {
     uint64_t* lthr;
     int32_t nwl;             // bitmap words per pod: ceil(nblk / 64)
     int32_t lset;            // the set this argument record's scans write
+    const ScanRec* srec;     // [P] the pods' scan records (the micro evaluator's scan form)
 };
 // pruned lists: pod b's bitmap / threshold in set `set`
 __host__ __device__ __forceinline__ uint64_t* lbit_of(const EngineArgs& a, int set, int b) {

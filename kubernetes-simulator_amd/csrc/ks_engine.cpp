@@ -137,6 +137,7 @@ struct ks_engine {
     DVec<int32_t> dur, b_node, b_status, phase_off, cum_sec, exp_pod;
     DVec<int64_t> exp_off, t0, fin, use, exp_pos;
     DVec<uint8_t> expired;
+    DVec<ks::ScanRec> srec;  // the pods' scan records (ks_device.h scan_rec_micro), rebuilt on a rescale
     // pods (host mirror of placement-independent facts)
     std::vector<int64_t> h_bind_tick, h_fin;
     std::vector<int64_t> h_exp_off{0};
@@ -295,6 +296,7 @@ ks::EngineArgs make_args(ks_engine* e) {
     a.lthr = e->prune ? e->lthr : nullptr;
     a.nwl = e->nwl;
     a.lset = 1;  // the engine's own scans (the speculative scan's record: set 0, step_body)
+    a.srec = e->srec.p;
     return a;
 }
 
@@ -526,7 +528,7 @@ void engine_free(ks_engine* e) {
     e->pods.release(); e->dur.release(); e->b_node.release(); e->b_status.release();
     e->phase_off.release(); e->cum_sec.release(); e->exp_pod.release(); e->exp_off.release();
     e->t0.release(); e->fin.release(); e->use.release(); e->expired.release(); e->exp_pos.release();
-    e->preg.release(); e->d_blk.release(); e->d_digest.release();
+    e->preg.release(); e->d_blk.release(); e->d_digest.release(); e->srec.release();
     if (e->node_mem) (void)hipFree(e->node_mem);
     if (e->lists) (void)hipFree(e->lists);
     if (e->cand) (void)hipFree(e->cand);
@@ -810,9 +812,15 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
             for (ks::PodRec& r : e->h_pods)
                 for (int k = 0; k < 3; k++) r.req[k] *= f[k];
             update_mode(e);
+            if (e->P) {  // the scan records of the rescaled requests
+                std::vector<ks::ScanRec> sr(e->P);
+                for (int64_t q = 0; q < e->P; q++) sr[q] = ks::scan_rec_micro(e->dc, e->h_pods[q]);
+                HIPCHK(e, hipMemcpy(e->srec.p, sr.data(), sizeof(ks::ScanRec) * e->P, hipMemcpyHostToDevice));
+            }
         }
     }
     std::vector<ks::PodRec> recs(m);
+    std::vector<ks::ScanRec> srecs(m);
     std::vector<int32_t> dur(m), poff(m), cum(nf);
     std::vector<int64_t> t0(m), fin(m), eoff(m);
     std::vector<int32_t> tsec(m);
@@ -833,6 +841,7 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
         r.sel = sel[i];
         r.keymask = km;
         r.flags = flags ? flags[i] : 0;
+        srecs[i] = ks::scan_rec_micro(e->dc, r);
         const int64_t arr = std::max<int64_t>(arrival[i], e->tick + 1);
         const int64_t bt = std::max<int64_t>(prev_bind + 1, arr);
         prev_bind = bt;
@@ -877,6 +886,7 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
     const int64_t z0 = 0;
     if (!e->group && m <= kStageMaxPods) {
         HIPCHK(e, stage_append(e, e->pods, recs.data(), m));
+        HIPCHK(e, stage_append(e, e->srec, srecs.data(), m));
         HIPCHK(e, stage_append(e, e->dur, dur.data(), m));
         HIPCHK(e, stage_append(e, e->t0, t0.data(), m));
         HIPCHK(e, stage_append(e, e->fin, fin.data(), m));
@@ -901,6 +911,7 @@ ks_status ks_submit_pods(ks_engine* e, int64_t m, const int64_t* arrival, const 
     } else {
         HIPCHK(e, stage_flush(e));
         HIPCHK(e, e->pods.append(recs.data(), m, st));
+        HIPCHK(e, e->srec.append(srecs.data(), m, st));
         HIPCHK(e, e->dur.append(dur.data(), m, st));
         HIPCHK(e, e->t0.append(t0.data(), m, st));
         HIPCHK(e, e->fin.append(fin.data(), m, st));

@@ -63,24 +63,44 @@ __device__ __forceinline__ void scan_item(const EngineArgs& a, KT* kv, int64_t s
         NodeV n{};
         if (node < (int64_t)a.c.nwb * kWave) n = load_node(a.s, node);
         if (excl && valid && excl[node] >= 0) valid = false;
-        const PodRec* pp = a.pods + start + pg0;
         int b = 0;
-        // kUnroll pods at a time: their scalar loads share one wait and the independent
-        // evaluations interleave (instruction-level parallelism within the wave)
-        for (; b + kUnroll <= np; b += kUnroll) {
-            PodRec p[kUnroll];
+        if constexpr (kMode == kEvalMicro) {  // the scan records (ks_device.h eval_scan_micro)
+            const ScanRec* sp = a.srec + start + pg0;
+            const int32_t npen = scan_npen(a.c, n);
+            for (; b + kUnroll <= np; b += kUnroll) {
+                ScanRec p[kUnroll];
 #pragma unroll
-            for (int u = 0; u < kUnroll; ++u) p[u] = sload(pp + b + u);  // uniform: SGPRs, scalar cache
+                for (int u = 0; u < kUnroll; ++u) p[u] = sload(sp + b + u);
 #pragma unroll
-            for (int u = 0; u < kUnroll; ++u) {
-                const uint32_t t = eval_t<kMode>(a.c, p[u], n);  // branch-free; padding lanes discarded
-                kv[(b + u) * kNodes + lt] = (KT)(valid ? t : 0u);
+                for (int u = 0; u < kUnroll; ++u) {
+                    const uint32_t t = eval_scan_micro(a.c, p[u], n, npen);
+                    kv[(b + u) * kNodes + lt] = (KT)(valid ? t : 0u);
+                }
             }
-        }
-        for (; b < np; ++b) {
-            const PodRec p = sload(pp + b);
-            const uint32_t t = eval_t<kMode>(a.c, p, n);
-            kv[b * kNodes + lt] = (KT)(valid ? t : 0u);
+            for (; b < np; ++b) {
+                const ScanRec p = sload(sp + b);
+                const uint32_t t = eval_scan_micro(a.c, p, n, npen);
+                kv[b * kNodes + lt] = (KT)(valid ? t : 0u);
+            }
+        } else {
+            const PodRec* pp = a.pods + start + pg0;
+            // kUnroll pods at a time: their scalar loads share one wait and the independent
+            // evaluations interleave (instruction-level parallelism within the wave)
+            for (; b + kUnroll <= np; b += kUnroll) {
+                PodRec p[kUnroll];
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) p[u] = sload(pp + b + u);  // uniform: SGPRs, scalar cache
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) {
+                    const uint32_t t = eval_t<kMode>(a.c, p[u], n);  // branch-free; padding lanes discarded
+                    kv[(b + u) * kNodes + lt] = (KT)(valid ? t : 0u);
+                }
+            }
+            for (; b < np; ++b) {
+                const PodRec p = sload(pp + b);
+                const uint32_t t = eval_t<kMode>(a.c, p, n);
+                kv[b * kNodes + lt] = (KT)(valid ? t : 0u);
+            }
         }
     }
     __syncthreads();

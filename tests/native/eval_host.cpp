@@ -69,3 +69,19 @@ extern "C" void ks_host_micro_batch(const ks::Cfg* c, int64_t n, const int64_t* 
         total1_m[i] = ks::eval_total1_micro(*c, p, v);
     }
 }
+// the same with the scan's form of the micro evaluator (per-pod ScanRec, per-node npen)
+extern "C" void ks_host_scan_micro_batch(const ks::Cfg* c, int64_t n, const int64_t* alloc, const int64_t* run,
+                                         const int64_t* req, const uint32_t* keymask, const uint64_t* masks,
+                                         uint32_t* total1_s) {
+    for (int64_t i = 0; i < n; i++) {
+        ks::NodeV v{};
+        v.ac = alloc[i * 4 + 0]; v.am = alloc[i * 4 + 1]; v.ag = alloc[i * 4 + 2]; v.ap = alloc[i * 4 + 3];
+        v.rc = run[i * 4 + 0]; v.rm = run[i * 4 + 1]; v.rg = run[i * 4 + 2]; v.nr = run[i * 4 + 3];
+        v.taint = masks[i * 4 + 0]; v.label = masks[i * 4 + 1];
+        ks::PodRec p{};
+        p.req[0] = req[i * 3 + 0]; p.req[1] = req[i * 3 + 1]; p.req[2] = req[i * 3 + 2];
+        p.keymask = keymask[i];
+        p.tol = masks[i * 4 + 2]; p.sel = masks[i * 4 + 3];
+        total1_s[i] = ks::eval_scan_micro(*c, ks::scan_rec_micro(*c, p), v, ks::scan_npen(*c, v));
+    }
+}

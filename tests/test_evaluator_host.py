@@ -214,3 +214,11 @@ def test_micro_eval_exact(lib, feeds, filters, const, w_lr, w_ba, cap_bits):
     lib.ks_host_micro_batch(C.byref(c), n, _p(alloc), _p(run), _p(req), _p(keymask), _p(masks), _p(t1), _p(t1m))
     assert (t1 > 0).sum() > n // 10
     np.testing.assert_array_equal(t1m, t1)
+    # the scan's form (per-pod ScanRec: clamped / fit-biased requests, complemented tolerations)
+    t1s = np.zeros(n, np.uint32)
+    lib.ks_host_scan_micro_batch.argtypes = [C.POINTER(Cfg), C.c_int64] + [C.c_void_p] * 6
+    lib.ks_host_scan_micro_batch(C.byref(c), n, _p(alloc), _p(run), _p(req), _p(keymask), _p(masks), _p(t1s))
+    np.testing.assert_array_equal(t1s, t1)
+    c.has_scorers = 0  # no scorer: no candidate
+    lib.ks_host_scan_micro_batch(C.byref(c), n, _p(alloc), _p(run), _p(req), _p(keymask), _p(masks), _p(t1s))
+    assert (t1s == 0).all()
