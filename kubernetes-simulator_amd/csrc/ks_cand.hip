@@ -28,7 +28,6 @@
 namespace ks {
 namespace sq {
 
-constexpr int kL = kTopL;
 constexpr int kR = kChR;
 constexpr int kPrepThreads = 1024;
 constexpr int kClBuf = 256;
@@ -81,33 +80,52 @@ __device__ __forceinline__ void put_rec(uint32_t* o, const NodeV& v) {
 // E-node keys per merge_cl thread (E node tid + q * threads)
 constexpr int kEPer = kEMax / 256;
 
-// Pod i's static candidates from its merged top-L `cand` (LDS or global), by one workgroup: the
-// kept entries (sorted, <= kR) with their slots.  ek: this thread's E-node keys (computed before
-// the merge, so their dependent reads overlap the block lists'), 0 = none.
-template <int kMode>
+// Pod i's static candidates from its merged top-L `cand` (LDS or global, kLL entries), by one
+// workgroup: the kept entries (sorted, <= kR) with their slots.  ek: this thread's E-node keys
+// (computed before the merge, so their dependent reads overlap the block lists'), 0 = none.
+// The list's entries on no E node (their snapshot key is exact) are kept up to kTopL of them; the
+// threshold thr is the last kept one when kTopL are kept, else the list's last key (1 when the list
+// is not full: no other node is a candidate at all); an E node is kept when its exact key reaches
+// thr.  Any other node scores below thr: an untouched node outside the kept entries is below them
+// in the snapshot order, and the list's own order bounds every node outside it.  (kLL = kTopL: the
+// list's entries outside E and thr = its last key; the overlap's longer lists keep kTopL exact
+// entries even when the previous batch bound some of the top ones.)
+template <int kMode, int kLL>
 __device__ __forceinline__ void cand_list(const EngineArgs& a, WinWS& ws, int i, const uint64_t* cand,
                                           const uint64_t (&ek)[kEPer]) {
+    static_assert(kLL >= kTopL && kLL <= kWave, "one list entry per lane");
     const int tid = threadIdx.x;
     __shared__ uint64_t buf[kClBuf];
     __shared__ int cnt;
+    __shared__ uint64_t s_thr;
+    __shared__ int s_full;
     if (tid == 0) cnt = 0;
     __syncthreads();
-    const uint64_t last = cand[kL - 1];
-    const bool full = last != 0;
-    const uint64_t thr = full ? last : 1ull;
+    if (tid < kWave) {  // wave 0, lane k: list entry k
+        const int lane = tid;
+        const uint64_t x = lane < kLL ? cand[lane] : 0ull;
+        const bool un = x != 0 && a.e_idx[key_node(x)] < 0;
+        const uint64_t um = __ballot(un);
+        const int rank = __popcll(um & ((1ull << lane) - 1ull));
+        if (un && rank < kTopL) {
+            const int pos = atomicAdd(&cnt, 1);
+            if (pos < kClBuf) buf[pos] = x;
+        }
+        const uint64_t last = cand[kLL - 1];
+        const bool enough = __popcll(um) >= kTopL;
+        if (enough && un && rank == kTopL - 1) s_thr = x;
+        if (!enough && lane == 0) s_thr = last != 0 ? last : 1ull;
+        if (lane == 0) s_full = enough || last != 0;
+    }
+    __syncthreads();
+    const uint64_t thr = s_thr;
+    const bool full = s_full != 0;
 #pragma unroll
     for (int q = 0; q < kEPer; ++q)
         if (ek[q] != 0 && ek[q] >= thr) {
             const int pos = atomicAdd(&cnt, 1);
             if (pos < kClBuf) buf[pos] = ek[q];
         }
-    if (tid < kL) {
-        const uint64_t x = cand[tid];
-        if (x != 0 && a.e_idx[key_node(x)] < 0) {
-            const int pos = atomicAdd(&cnt, 1);
-            if (pos < kClBuf) buf[pos] = x;
-        }
-    }
     __syncthreads();
     const int c = cnt, n = c < kClBuf ? c : kClBuf;
     __shared__ uint64_t kept[kR];
@@ -168,11 +186,11 @@ __device__ __forceinline__ void cand_list(const EngineArgs& a, WinWS& ws, int i,
 }
 
 // merge + candidate list of pod b in one workgroup (the merge kernel's exact top-L over nl sorted
-// lists lists[b * pod_stride + k * list_stride], ks_kernels.hip, then cand_list) — one launch
-// fewer per batch.  src == nullptr: the engine's own block lists (pruned: only the blocks its
+// lists lists[b * pod_stride + k * list_stride] of kLL keys, ks_kernels.hip, then cand_list) — one
+// launch fewer per batch.  src == nullptr: the engine's own block lists (pruned: only the blocks its
 // bitmap flags, ks_scan.h).  Every launch clears the pods' bitmaps and thresholds for the next scan.
 constexpr int kMergeMaxWaves = 16;
-template <int kMode>
+template <int kMode, int kLL>
 __global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs* __restrict__ A, const uint64_t* src,
                                                          int64_t pod_stride, int32_t nl, int64_t list_stride) {
     const EngineArgs& a = A[0];
@@ -180,9 +198,9 @@ __global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs* __rest
     const bool own = src == nullptr;
     if (own) {
         src = a.lists;
-        pod_stride = (int64_t)a.nblk * kL;
+        pod_stride = (int64_t)a.nblk * kLL;
         nl = a.nblk;
-        list_stride = kL;
+        list_stride = kLL;
     }
     const int b = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -200,19 +218,19 @@ __global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs* __rest
         if (tid < 2 * kThrCopies) *lthr_of(a, tid / kThrCopies, tid % kThrCopies, b) = 0;
     }
     if (b >= ws.nb) return;  // (the window prep cut the batch; errors left nb = 0)
-    uint64_t top[kL];
+    uint64_t top[kLL];
 #pragma unroll
-    for (int k = 0; k < kL; ++k) top[k] = 0;
+    for (int k = 0; k < kLL; ++k) top[k] = 0;
     const uint64_t* lists = src + (int64_t)b * pod_stride;
     // independent reads first: this thread's first block list, then the E nodes' keys (dependent
     // chains: node, slots, expiring requests) while it is in flight
-    uint64_t lv0[kL];
+    uint64_t lv0[kLL];
     const bool has0 = tid < nfl;
     {
         const int l0 = has0 ? (pruned ? scn::flagged_block(tid, 0, nl, F) : tid) : 0;
         const ulonglong2* lp = reinterpret_cast<const ulonglong2*>(lists + (int64_t)l0 * list_stride);
 #pragma unroll
-        for (int k = 0; k < kL / 2; ++k) {
+        for (int k = 0; k < kLL / 2; ++k) {
             const ulonglong2 w = has0 ? lp[k] : make_ulonglong2(0, 0);
             lv0[2 * k] = w.x;
             lv0[2 * k + 1] = w.y;
@@ -239,48 +257,72 @@ __global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs* __rest
             ek[q] = make_key(eval_t<kMode>(a.c, p, v), (uint32_t)n);
         }
     }
-    if (has0) topl_insert(top, lv0);
+    if (has0) {  // (the first list is the thread's top as it is: sorted)
+#pragma unroll
+        for (int k = 0; k < kLL; ++k) top[k] = lv0[k];
+    }
     for (int j = tid + nthr; j < nfl; j += nthr) {
         const int blk = pruned ? scn::flagged_block(j, 0, nl, F) : j;
         const ulonglong2* lp = reinterpret_cast<const ulonglong2*>(lists + (int64_t)blk * list_stride);
-        uint64_t lv[kL];
+        uint64_t lv[kLL];
 #pragma unroll
-        for (int k = 0; k < kL / 2; ++k) {
+        for (int k = 0; k < kLL / 2; ++k) {
             const ulonglong2 w = lp[k];
             lv[2 * k] = w.x;
             lv[2 * k + 1] = w.y;
         }
-        topl_insert(top, lv);
+        topl_insert<kLL>(top, lv);
     }
-    __shared__ uint64_t wl[kMergeMaxWaves][kL];
-    __shared__ uint64_t pc[kL];
+    __shared__ uint64_t wl[kMergeMaxWaves][kLL];
+    __shared__ uint64_t pc[kLL];
     int head = 0;
-    for (int r = 0; r < kL; ++r) {
+    for (int r = 0; r < kLL; ++r) {
         uint64_t h = 0;
 #pragma unroll
-        for (int k = 0; k < kL; ++k) h = (k == head) ? top[k] : h;
+        for (int k = 0; k < kLL; ++k) h = (k == head) ? top[k] : h;
         const uint64_t m = wave_max_u64(h);
         const uint64_t hit = __ballot(h == m && m != 0);
         if (lane == 0) wl[wave][r] = m;
         if (hit && lane == __ffsll((unsigned long long)hit) - 1) head++;
     }
     __syncthreads();
-    if (wave == 0) {
-        const int nc = nwav * kL;
-        uint64_t v0 = lane < nc ? wl[lane / kL][lane % kL] : 0ull;
-        uint64_t v1 = lane + kWave < nc ? wl[(lane + kWave) / kL][(lane + kWave) % kL] : 0ull;
-#pragma unroll
-        for (int r = 0; r < kL; ++r) {
-            const uint64_t m = wave_max_u64(v0 > v1 ? v0 : v1);
+    if (wave == 0 && nthr <= 256) {  // the wave lists' top kLL: one candidate per lane (4 waves)
+        static_assert(4 * kLL <= kWave, "one candidate per lane");
+        uint64_t v = lane < nwav * kLL ? wl[lane / kLL][lane % kLL] : 0ull;
+        for (int r = 0; r < kLL; ++r) {
+            const uint64_t m = wave_max_u64(v);
             if (lane == 0) pc[r] = m;
             if (m == 0) continue;
-            const uint64_t h0 = __ballot(v0 == m), h1 = __ballot(v1 == m);
-            if (h0 && lane == __ffsll((unsigned long long)h0) - 1) v0 = 0;
-            if (!h0 && h1 && lane == __ffsll((unsigned long long)h1) - 1) v1 = 0;
+            const uint64_t h = __ballot(v == m);  // keys are distinct: one holder
+            if (lane == __ffsll((unsigned long long)h) - 1) v = 0;
+        }
+    } else if (wave == 0) {  // up to kPer candidates per lane
+        constexpr int kPer = (kMergeMaxWaves * kLL + kWave - 1) / kWave;
+        const int nc = nwav * kLL;
+        uint64_t v[kPer];
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            const int c = lane + q * kWave;
+            v[q] = c < nc ? wl[c / kLL][c % kLL] : 0ull;
+        }
+        for (int r = 0; r < kLL; ++r) {
+            uint64_t lm = v[0];
+#pragma unroll
+            for (int q = 1; q < kPer; ++q) lm = lm > v[q] ? lm : v[q];
+            const uint64_t m = wave_max_u64(lm);
+            if (lane == 0) pc[r] = m;
+            if (m == 0) continue;
+            bool done = false;  // keys are distinct: exactly one holder
+#pragma unroll
+            for (int q = 0; q < kPer; ++q) {
+                const uint64_t h = __ballot(!done && v[q] == m);
+                if (h && lane == __ffsll((unsigned long long)h) - 1) v[q] = 0;
+                done = done || h != 0;
+            }
         }
     }
     __syncthreads();
-    cand_list<kMode>(a, ws, b, pc, ek);
+    cand_list<kMode, kLL>(a, ws, b, pc, ek);
 }
 
 }  // namespace sq
@@ -292,15 +334,20 @@ hipError_t launch_window_prep(const EngineArgs* d, bool head, bool spec, int slo
 }
 
 hipError_t launch_merge_cl(const EngineArgs* d, int mode, int B, const uint64_t* lists, int64_t pod_stride,
-                           int32_t nl, int64_t list_stride, int nl_max, hipStream_t st) {
+                           int32_t nl, int64_t list_stride, int nl_max, hipStream_t st, int L) {
     static_assert(sq::kEPer * 256 >= kEMax, "E keys per thread at 256 threads");
     const dim3 g(B), t(nl_max > 1024 ? 1024 : 256);
-    switch (mode) {
-        case kEvalMicro: hipLaunchKernelGGL(sq::merge_cl_kernel<kEvalMicro>, g, t, 0, st, d, lists, pod_stride, nl, list_stride); break;
-        case kEvalTiny: hipLaunchKernelGGL(sq::merge_cl_kernel<kEvalTiny>, g, t, 0, st, d, lists, pod_stride, nl, list_stride); break;
-        case kEvalNarrow: hipLaunchKernelGGL(sq::merge_cl_kernel<kEvalNarrow>, g, t, 0, st, d, lists, pod_stride, nl, list_stride); break;
-        default: hipLaunchKernelGGL(sq::merge_cl_kernel<kEvalWide>, g, t, 0, st, d, lists, pod_stride, nl, list_stride); break;
+#define KS_MCL(LL)                                                                                                   \
+    switch (mode) {                                                                                                  \
+        case kEvalMicro: hipLaunchKernelGGL((sq::merge_cl_kernel<kEvalMicro, LL>), g, t, 0, st, d, lists, pod_stride, nl, list_stride); break; \
+        case kEvalTiny: hipLaunchKernelGGL((sq::merge_cl_kernel<kEvalTiny, LL>), g, t, 0, st, d, lists, pod_stride, nl, list_stride); break;   \
+        case kEvalNarrow: hipLaunchKernelGGL((sq::merge_cl_kernel<kEvalNarrow, LL>), g, t, 0, st, d, lists, pod_stride, nl, list_stride); break; \
+        default: hipLaunchKernelGGL((sq::merge_cl_kernel<kEvalWide, LL>), g, t, 0, st, d, lists, pod_stride, nl, list_stride); break;          \
     }
+    if (L == kTopL) { KS_MCL(kTopL) }
+    else if (L == kTopLOverlap) { KS_MCL(kTopLOverlap) }
+    else return hipErrorInvalidValue;
+#undef KS_MCL
     return hipGetLastError();
 }
 

@@ -854,6 +854,7 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
                 uint64_t dkA = 0, dkB = 0;
                 int dcA = -1, dcB = -1;
                 bool badA = false, badB = false;
+                DG(int dwhy = 0;)  // (diagnostic, pod A bits 0-2 / pod B bits 3-5: row state unknown, cached state unknown, both cached rebound)
                 if (actA || actB) {
                     const PodRec pA = sh.pod[actA ? iA : iB], pB = sh.pod[actB ? iB : iA];
                     SRow r[4];
@@ -875,6 +876,7 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
                         const int i = isA[q] ? iA : iB;
                         if (r[q].m(kMOvf) <= i) {
                             if (isA[q]) badA = true; else badB = true;
+                            DG(dwhy |= isA[q] ? 1 : 8;)
                             continue;
                         }
                         if (KS_CHUNK_ABL & 1) continue;
@@ -900,13 +902,14 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
                     bool& bad = half ? badB : badA;
                     if (sh.cdbad[pi]) {
                         bad = true;
+                        DG(dwhy |= half ? 16 : 2;)
                     } else {
                         uint64_t ck = sh.cd1[pi];
                         int cc = sh.cd1c[pi];
                         if (ck != 0 && (sh.cmask[cc] & below)) {
                             ck = sh.cd2[pi];
                             cc = sh.cd2c[pi];
-                            if (ck != 0 && (sh.cmask[cc] & below)) bad = true;
+                            if (ck != 0 && (sh.cmask[cc] & below)) { bad = true; DG(dwhy |= half ? 32 : 4;) }
                         }
                         if (ck > dk) { dk = ck; dc = cc; }
                     }
@@ -934,7 +937,12 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
                         code = 0;
                         if (bad || (fl & kFlOvf)) {
                             code = 1;
-                            DG(sh.why[i] = bad ? 0 : 1;)
+                            DG({
+                                int wa = 0;  // the group's reasons for this half's pod
+                                for (int o = 0; o < G; ++o) wa |= __shfl(dwhy, (lane & ~(G - 1)) + o);
+                                const int mine = half ? (wa >> 3) & 7 : wa & 7;
+                                sh.why[i] = !bad ? 1 : (mine & 4) ? 6 : (mine & 2) ? 5 : 0;
+                            })
                         } else if (rfree < kR) {
                             const uint64_t sk = cl_key(sh, efree);
                             if (sk > dk) { win = sk; wc = (int)(efree >> 16); }
@@ -1025,7 +1033,7 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
             if (tid == 0) {
                 unsigned long long* d = (unsigned long long*)a.ctr;
                 const int r = cut ? 4 : (stop_code == 1 ? sh.why[cend] : 4);  // (4: adm unknown or NotFound/bad)
-                atomicAdd(&d[9 + r], 1ull);
+                atomicAdd(&d[r == 5 ? 14 : r == 6 ? 22 : 9 + r], 1ull);
             }
 #endif
             break;
@@ -1115,8 +1123,7 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
         atomicAdd(&d[19], acc_fin);
         atomicAdd(&d[20], dstamp() - t3);
         atomicAdd(&d[21], (unsigned long long)ncid);
-        atomicAdd(&d[22], acc_cdp);
-        atomicAdd(&d[14], acc_rb);
+        (void)acc_cdp; (void)acc_rb;  // (d[14], d[22]: stop reasons 5, 6)
         atomicAdd(&d[23], (unsigned long long)nb);
         for (int q = 0; q < 4; ++q) atomicAdd(&d[24 + q], acc_ph[q]);
         atomicAdd(&d[28], (unsigned long long)n_sonly);
@@ -1145,7 +1152,7 @@ __global__ __launch_bounds__(kThreads) void resolve_chunk_kernel(const EngineArg
 // After its commit the resolver workgroup also computes the next batch's window (ks_prep.h, with the
 // head expiries and the touched nodes; `slot`: that batch's speculative-counter parity) in its LDS:
 // the standalone window-prep launch and its kernel boundary leave the critical path.
-template <int kMode, bool kPrune>
+template <int kMode, bool kPrune, int kLL>
 __global__ __launch_bounds__(kThreads) void chunk_scan_kernel(const EngineArgs* __restrict__ A,
                                                               const EngineArgs* __restrict__ As, int slot) {
     __shared__ ChShared sh;
@@ -1176,7 +1183,7 @@ __global__ __launch_bounds__(kThreads) void chunk_scan_kernel(const EngineArgs* 
     for (int64_t r = lo + 2 * (int64_t)j; r < hi; r += 2 * (int64_t)nx) {  // (uniform per workgroup)
         if (r != lo + 2 * (int64_t)j) __syncthreads();  // the previous round's extraction has read kv
         const int64_t it = r + half;
-        scn::scan_item<kMode, uint16_t, kPrune>(a, kv, start, nb, groups, it, it < hi, lt, x);
+        scn::scan_item<kMode, uint16_t, kPrune, kLL>(a, kv, start, nb, groups, it, it < hi, lt, x);
     }
 }
 static_assert(sizeof(ChShared) >= 2 * kMaxPGScan * scn::kNodes * sizeof(uint16_t), "two 16-bit key tables");
@@ -1185,21 +1192,27 @@ static_assert(sizeof(ChShared) >= 2 * kMaxPGScan * scn::kNodes * sizeof(uint16_t
 
 // the chunk resolver proper (its window and candidate lists: launch_window_prep(head) and
 // launch_merge_cl, ks_cand.hip)
-template <bool kPrune>
+template <bool kPrune, int kLL>
 static void launch_chunk_scan_t(const EngineArgs* d, const EngineArgs* ds, const dim3& g, int sl, int mode, hipStream_t st) {
     switch (mode) {
-        case kEvalMicro: hipLaunchKernelGGL((chk::chunk_scan_kernel<kEvalMicro, kPrune>), g, dim3(chk::kThreads), 0, st, d, ds, sl); break;
-        case kEvalTiny: hipLaunchKernelGGL((chk::chunk_scan_kernel<kEvalTiny, kPrune>), g, dim3(chk::kThreads), 0, st, d, ds, sl); break;
-        case kEvalNarrow: hipLaunchKernelGGL((chk::chunk_scan_kernel<kEvalNarrow, kPrune>), g, dim3(chk::kThreads), 0, st, d, ds, sl); break;
-        default: hipLaunchKernelGGL((chk::chunk_scan_kernel<kEvalWide, kPrune>), g, dim3(chk::kThreads), 0, st, d, ds, sl); break;
+        case kEvalMicro: hipLaunchKernelGGL((chk::chunk_scan_kernel<kEvalMicro, kPrune, kLL>), g, dim3(chk::kThreads), 0, st, d, ds, sl); break;
+        case kEvalTiny: hipLaunchKernelGGL((chk::chunk_scan_kernel<kEvalTiny, kPrune, kLL>), g, dim3(chk::kThreads), 0, st, d, ds, sl); break;
+        case kEvalNarrow: hipLaunchKernelGGL((chk::chunk_scan_kernel<kEvalNarrow, kPrune, kLL>), g, dim3(chk::kThreads), 0, st, d, ds, sl); break;
+        default: hipLaunchKernelGGL((chk::chunk_scan_kernel<kEvalWide, kPrune, kLL>), g, dim3(chk::kThreads), 0, st, d, ds, sl); break;
     }
 }
 
 hipError_t launch_chunk_scan(const EngineArgs* d, const EngineArgs* ds, int workers, int next_slot, int mode,
-                             bool prune, hipStream_t st) {
+                             bool prune, int L, hipStream_t st) {
     const dim3 g(1 + workers);
-    if (prune) launch_chunk_scan_t<true>(d, ds, g, next_slot & 1, mode, st);
-    else launch_chunk_scan_t<false>(d, ds, g, next_slot & 1, mode, st);
+    if (L != kTopL) {
+        if (prune || L != kTopLOverlap) return hipErrorInvalidValue;
+        launch_chunk_scan_t<false, kTopLOverlap>(d, ds, g, next_slot & 1, mode, st);
+    } else if (prune) {
+        launch_chunk_scan_t<true, kTopL>(d, ds, g, next_slot & 1, mode, st);
+    } else {
+        launch_chunk_scan_t<false, kTopL>(d, ds, g, next_slot & 1, mode, st);
+    }
     return hipGetLastError();
 }
 

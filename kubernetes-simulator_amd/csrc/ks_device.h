@@ -18,6 +18,16 @@ namespace ks {
 
 constexpr int kWave = 64;
 constexpr int kTopL = 8;  // exact top-L snapshot candidates kept per pod
+// the overlap's single-shard engines scan longer lists: their candidate lists keep the first kTopL
+// entries no node of the previous batch touched (ks_cand.hip cand_list), so a list whose top
+// entries the previous batch bound (stale) still holds kTopL exact ones (fewer exhausted-list stops).
+// 12 measured best on C3 (EXPERIMENTS.md: 8 -> 12 cuts exhausted stops 21 -> 3 per step for ~1.5 us
+// more merge per batch; 16 costs more merge than it saves)
+#ifndef KS_OVERLAP_LIST
+#define KS_OVERLAP_LIST 12
+#endif
+constexpr int kTopLOverlap = KS_OVERLAP_LIST;
+static_assert(kTopLOverlap >= kTopL && kTopLOverlap <= 16 && kTopLOverlap % 2 == 0, "overlap list length");
 
 enum : uint32_t { kFilterFit = 1, kFilterTaint = 2, kFilterSelector = 4 };
 
@@ -585,13 +595,14 @@ __host__ __device__ __forceinline__ uint64_t make_key(uint32_t total1, uint32_t 
 // Insert one sorted (descending, 0-padded) list of L keys into a sorted top-L: the per-thread step
 // of the merge kernel, also the host's ks_merge_candidates.  Keys are distinct (node in the low
 // bits), so the result is the exact top-L of the union.
-__host__ __device__ __forceinline__ void topl_insert(uint64_t (&top)[kTopL], const uint64_t (&lv)[kTopL]) {
+template <int L = kTopL>
+__host__ __device__ __forceinline__ void topl_insert(uint64_t (&top)[L], const uint64_t (&lv)[L]) {
 #pragma unroll
-    for (int k = 0; k < kTopL; ++k) {
+    for (int k = 0; k < L; ++k) {
         uint64_t v = lv[k];
-        if (v <= top[kTopL - 1]) break;  // lists are sorted: nothing further can enter
+        if (v <= top[L - 1]) break;  // lists are sorted: nothing further can enter
 #pragma unroll
-        for (int s = 0; s < kTopL; ++s) {
+        for (int s = 0; s < L; ++s) {
             const uint64_t t = top[s];
             const bool gt = v > t;
             top[s] = gt ? v : t;
@@ -733,8 +744,10 @@ hipError_t launch_expire_head(const EngineArgs* d, int S, hipStream_t st);
 // key16: every total + 1 < 2^16 (scan_kernel's 16-bit key table)
 // cond: only when the window workspace's rescan flag is set (the overlap's fallback)
 // prune: the pruned-list form (the engine's lbit / lthr set, ks_scan.h)
+// L: the block lists' length (kTopL; kTopLOverlap for the overlap's single-shard engines: key16, not
+// pruned)
 hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int mode, bool key16, hipStream_t st,
-                       bool cond = false, bool prune = false);
+                       bool cond = false, bool prune = false, int L = kTopL);
 // per scenario and pod b < batch size: exact top-L over nl sorted lists
 // lists[b*pod_stride + k*list_stride] into out (lists == nullptr: the scenario's own block lists
 // into its candidate lists)
@@ -761,7 +774,7 @@ hipError_t launch_chunk_only(const EngineArgs* d, int mode, hipStream_t st);
 // workgroups beside the resolver's; 16-bit key tables, so key16 engines only); after its commit the
 // resolver workgroup runs the next batch's window prep (head, spec; next_slot: that batch's parity)
 hipError_t launch_chunk_scan(const EngineArgs* d, const EngineArgs* ds, int workers, int next_slot, int mode,
-                             bool prune, hipStream_t st);
+                             bool prune, int L, hipStream_t st);
 // the batch window (expiries of the batch's pods, the node set E): the resolvers' first kernel;
 // head: also apply the expiries due before the batch's first pod (expire_head's work); spec: the
 // batch's lists come from the speculative scan (the touched nodes join E, or a rescan is flagged)
@@ -770,8 +783,9 @@ hipError_t launch_chunk_scan(const EngineArgs* d, const EngineArgs* ds, int work
 hipError_t launch_window_prep(const EngineArgs* d, bool head, bool spec, int slot, hipStream_t st);
 // merge + candidate lists (ks_cand.hip): per pod the merge kernel's exact top-L over its lists, then
 // its static candidates and their slots
+// L: the lists' length (the engine's block lists, or kTopL for the sharded second merge)
 hipError_t launch_merge_cl(const EngineArgs* d, int mode, int B, const uint64_t* lists, int64_t pod_stride,
-                           int32_t nl, int64_t list_stride, int nl_max, hipStream_t st);
+                           int32_t nl, int64_t list_stride, int nl_max, hipStream_t st, int L = kTopL);
 struct BindSeg {
     const int32_t* node;
     const int32_t* status;

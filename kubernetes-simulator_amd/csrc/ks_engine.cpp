@@ -61,6 +61,11 @@ constexpr int64_t kNever = std::numeric_limits<int64_t>::max();
 constexpr int64_t kUBlk = 256;   // usage index: pods per block (= the usage kernels' workgroup)
 constexpr int64_t kUSup = 64;    // blocks per super block
 constexpr int64_t kMaxDigestTicks = 1 << 20;
+// the overlap's limit on a rank's scan blocks (step_body)
+#ifndef KS_OVERLAP_MAX_BLOCKS
+#define KS_OVERLAP_MAX_BLOCKS 256
+#endif
+constexpr int kOverlapMaxBlocks = KS_OVERLAP_MAX_BLOCKS;
 
 // Growable device array (stream-ordered copies on growth).
 template <typename T>
@@ -206,6 +211,7 @@ struct ks_engine {
     uint64_t* cand_all = nullptr;  // [world * vsh][B][L]
     // pruned block lists (ks_scan.h): per-pod bitmaps of the blocks that wrote a list and thresholds
     bool prune = false;
+    int L = ks::kTopL;  // the block lists' length (kTopLOverlap: the overlap's single-shard engines)
     uint64_t* lbit = nullptr;  // [B][nwl]
     uint64_t* lthr = nullptr;  // [2][kThrCopies][B]
     int nwl = 0;
@@ -716,7 +722,9 @@ ks_status ks_load_nodes(ks_engine* e, int64_t n, const int64_t* alloc, const uin
            (int64_t)e->blk_n * ((e->B + pg * 2 - 1) / (pg * 2)) >= KS_PG_MIN_WG)
         pg *= 2;
     e->PG = pg;
-    HIPCHK(e, hipMalloc(&e->lists, sizeof(uint64_t) * (size_t)e->B * e->nblk * ks::kTopL));
+    // (the overlap's single-shard engines may scan lists of kTopLOverlap keys: step_body)
+    const int lmax = G == 1 && e->blk_n <= kOverlapMaxBlocks ? ks::kTopLOverlap : ks::kTopL;
+    HIPCHK(e, hipMalloc(&e->lists, sizeof(uint64_t) * (size_t)e->B * e->nblk * lmax));
     HIPCHK(e, hipMalloc(&e->cand, sizeof(uint64_t) * (size_t)e->B * ks::kTopL));
     if (G > 1) HIPCHK(e, hipMalloc(&e->cand_all, sizeof(uint64_t) * (size_t)G * e->B * ks::kTopL));
     if (G > 1 && e->xfn) HIPCHK(e, hipHostMalloc(&e->h_xbuf, sizeof(uint64_t) * (size_t)G * e->B * ks::kTopL, hipHostMallocDefault));
@@ -1152,6 +1160,7 @@ static bool tick_step(ks_engine* e, int64_t t_end, ks_bind* out, int64_t cap, in
 #endif
 constexpr int kPruneMinBlocks = KS_PRUNE_MIN_BLOCKS;
 
+
 static ks_status ensure_window_ws(ks_engine* e) {
     const int r = resolver_of(e);
     e->prune = r == kResolveChunk && !e->group && (e->nblk >= kPruneMinBlocks || (e->flags & KS_ENGINE_PRUNED_LISTS));
@@ -1208,11 +1217,14 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
     // this rank's scan blocks.  Sharded engines too: every rank's lists are speculative alike and its
     // touched nodes (the same on every rank: the resolvers are identical) join E; the exchange runs
     // every batch whether or not window prep flagged a rescan, so every rank issues the same
-    // collectives.  Ranks scanning many blocks keep the plain chain: their scan is longer than the
-    // resolve it would hide behind (C5 unsharded: 4,096 blocks, 0.33 vs 0.08 ms), and in the fused
-    // kernel it runs one workgroup per CU
+    // collectives.  In the fused kernel the scan runs one workgroup per CU (the resolver's LDS fixes
+    // the kernel's), ~3 blocks per us: ranks scanning more than kOverlapMaxBlocks blocks keep the
+    // plain chain, whose scan runs at full occupancy (C5 on 8 ranks, 512 blocks each: fused kernel
+    // 129 us against a 78 us resolve + a 37 us scan; C3: 196 blocks hide under the resolve)
     // (profiling keeps it: the per-kernel events bracket the same launches)
-    const bool overlap = fused && e->overlap && e->d_args_spec && key16(e) && e->blk_n <= 1024;
+    const bool overlap = fused && e->overlap && e->d_args_spec && key16(e) && e->blk_n <= kOverlapMaxBlocks;
+    // the overlap's single-shard lists are longer (ks_device.h kTopLOverlap, ks_cand.hip cand_list)
+    e->L = overlap && e->world * e->vsh == 1 && !e->prune ? ks::kTopLOverlap : ks::kTopL;
     if (overlap) {
         for (int k = 0; k < 2; k++) {
             e->h_args_spec[k] = *e->h_args;
@@ -1251,13 +1263,13 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
             // (an overlapped batch's window was computed by the previous chunk kernel after its commit)
             if (!spec) HIPCHK(e, fused ? ks::launch_window_prep(d, true, false, (int)(b & 1), st) : ks::launch_expire_head(d, 1, st));
             if (ev[1]) HIPCHK(e, hipEventRecord(ev[1], st));
-            HIPCHK(e, ks::launch_scan(d, 1, e->blk_n, e->B, e->PG, e->mode, key16(e), st, spec, e->prune));
+            HIPCHK(e, ks::launch_scan(d, 1, e->blk_n, e->B, e->PG, e->mode, key16(e), st, spec, e->prune, e->L));
             if (ev[2]) HIPCHK(e, hipEventRecord(ev[2], st));
             const int G = e->world * e->vsh;
             hipEvent_t evx[2] = {ev[5], ev[6]};  // part merges | exchange | merge (sharded engines)
             const int64_t L = ks::kTopL, BL = (int64_t)e->B * L;
             if (G == 1) {
-                HIPCHK(e, fused ? ks::launch_merge_cl(d, e->mode, e->B, nullptr, 0, 0, 0, e->nblk, st)
+                HIPCHK(e, fused ? ks::launch_merge_cl(d, e->mode, e->B, nullptr, 0, 0, 0, e->nblk, st, e->L)
                                 : ks::launch_merge(d, 1, e->B, nullptr, 0, 0, 0, nullptr, e->nblk, st));
             } else {
                 for (int v = 0; v < e->vsh; v++) {
@@ -1289,7 +1301,7 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
             if (ev[3]) HIPCHK(e, hipEventRecord(ev[3], st));
             if (overlap && b + 1 < nbat)  // the resolver with the next batch's scan beside it
                 HIPCHK(e, ks::launch_chunk_scan(d, e->d_args_spec + (b & 1), e->scan_workers, (int)((b + 1) & 1), e->mode,
-                                                e->prune, st));
+                                                e->prune, e->L, st));
             else
                 HIPCHK(e, fused ? ks::launch_chunk_only(d, e->mode, st) : launch_resolver(d, 1, e->mode, which, st));
             if (ev[4]) HIPCHK(e, hipEventRecord(ev[4], st));

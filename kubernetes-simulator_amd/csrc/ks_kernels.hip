@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256) void expire_head_kernel(const EngineArgs* __re
 // ------------------------------------------------------------------------------------------
 // KT: the key table's word, uint16_t when every total + 1 < 2^16 (the host's check on the scorer
 // weights) — half the LDS per workgroup, so more workgroups fit a CU.
-template <int kMode, typename KT, bool kPrune>
+template <int kMode, typename KT, bool kPrune, int kLL>
 __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict__ A, int xcd, int cond) {
     extern __shared__ uint32_t kv_raw[];
     KT* const kv = reinterpret_cast<KT*>(kv_raw);  // [PG][kBlockNodes]: total+1 per (pod, node of the block)
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict_
         if ((int)blockIdx.x >= a.blk_n || (int)blockIdx.y >= groups) return;  // scenarios may differ in size
         it_lo = (int64_t)blockIdx.x * groups + blockIdx.y;
     }
-    scn::scan_item<kMode, KT, kPrune>(a, kv, start, nb, groups, it_lo, true, threadIdx.x, (int)(blockIdx.x % kThrCopies));
+    scn::scan_item<kMode, KT, kPrune, kLL>(a, kv, start, nb, groups, it_lo, true, threadIdx.x, (int)(blockIdx.x % kThrCopies));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1113,18 +1113,18 @@ hipError_t launch_expire_head(const EngineArgs* d, int S, hipStream_t st) {
     return hipGetLastError();
 }
 
-template <typename KT, bool kPrune>
+template <typename KT, bool kPrune, int kLL>
 static void launch_scan_t(const EngineArgs* d, const dim3& g, size_t lds, int mode, int xcd, int cond, hipStream_t st) {
     switch (mode) {
-        case kEvalMicro: hipLaunchKernelGGL((scan_kernel<kEvalMicro, KT, kPrune>), g, dim3(kBlockNodes), lds, st, d, xcd, cond); break;
-        case kEvalTiny: hipLaunchKernelGGL((scan_kernel<kEvalTiny, KT, kPrune>), g, dim3(kBlockNodes), lds, st, d, xcd, cond); break;
-        case kEvalNarrow: hipLaunchKernelGGL((scan_kernel<kEvalNarrow, KT, kPrune>), g, dim3(kBlockNodes), lds, st, d, xcd, cond); break;
-        default: hipLaunchKernelGGL((scan_kernel<kEvalWide, KT, kPrune>), g, dim3(kBlockNodes), lds, st, d, xcd, cond); break;
+        case kEvalMicro: hipLaunchKernelGGL((scan_kernel<kEvalMicro, KT, kPrune, kLL>), g, dim3(kBlockNodes), lds, st, d, xcd, cond); break;
+        case kEvalTiny: hipLaunchKernelGGL((scan_kernel<kEvalTiny, KT, kPrune, kLL>), g, dim3(kBlockNodes), lds, st, d, xcd, cond); break;
+        case kEvalNarrow: hipLaunchKernelGGL((scan_kernel<kEvalNarrow, KT, kPrune, kLL>), g, dim3(kBlockNodes), lds, st, d, xcd, cond); break;
+        default: hipLaunchKernelGGL((scan_kernel<kEvalWide, KT, kPrune, kLL>), g, dim3(kBlockNodes), lds, st, d, xcd, cond); break;
     }
 }
 
 hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int mode, bool key16, hipStream_t st,
-                       bool cond, bool prune) {
+                       bool cond, bool prune, int L) {
     if (blk_n > 0 && S > 0) {
         // one (block, pod group) item per workgroup; one engine: the XCD-aware 1-D deal
         const int groups = (B + PG - 1) / PG;
@@ -1132,12 +1132,15 @@ hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int
         const bool xcd = S == 1;
         const dim3 g = xcd ? dim3((unsigned)(((int64_t)blk_n * groups + 7) / 8 * 8), 1, 1) : dim3(blk_n, groups, S);
         const int x = xcd ? 1 : 0, c = cond ? 1 : 0;
-        if (key16) {
-            if (prune) launch_scan_t<uint16_t, true>(d, g, lds, mode, x, c, st);
-            else launch_scan_t<uint16_t, false>(d, g, lds, mode, x, c, st);
+        if (L != kTopL) {  // the overlap's single-shard lists: 16-bit keys, not pruned (ks_engine.cpp)
+            if (!key16 || prune || L != kTopLOverlap) return hipErrorInvalidValue;
+            launch_scan_t<uint16_t, false, kTopLOverlap>(d, g, lds, mode, x, c, st);
+        } else if (key16) {
+            if (prune) launch_scan_t<uint16_t, true, kTopL>(d, g, lds, mode, x, c, st);
+            else launch_scan_t<uint16_t, false, kTopL>(d, g, lds, mode, x, c, st);
         } else {
-            if (prune) launch_scan_t<uint32_t, true>(d, g, lds, mode, x, c, st);
-            else launch_scan_t<uint32_t, false>(d, g, lds, mode, x, c, st);
+            if (prune) launch_scan_t<uint32_t, true, kTopL>(d, g, lds, mode, x, c, st);
+            else launch_scan_t<uint32_t, false, kTopL>(d, g, lds, mode, x, c, st);
         }
     }
     return hipGetLastError();

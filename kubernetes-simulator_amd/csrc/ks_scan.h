@@ -38,8 +38,9 @@ __device__ __forceinline__ int popc_below(uint64_t mask, int lane) { return __po
 // scan 0.33 -> 0.46 ms with one atomicMax word per pod), updated by a plain store when a block's
 // 8th key beats the value it read.  Most blocks of a large cluster then write nothing: the ties of
 // the top class go to the lowest node indices, which the first blocks of each XCD's range hold.
-// kPrune: the pruned form (the engine's a.lbit is set); the plain form is compiled without it
-template <int kMode, typename KT, bool kPrune>
+// kPrune: the pruned form (the engine's a.lbit is set); the plain form is compiled without it.
+// kLL: the list length (kTopL, or kTopLOverlap for the overlap's single-shard engines)
+template <int kMode, typename KT, bool kPrune, int kLL = kTopL>
 __device__ __forceinline__ void scan_item(const EngineArgs& a, KT* kv, int64_t start, int64_t nb, int groups, int64_t it,
                                           bool has, int lt, int copy, const int32_t* excl = nullptr) {
     const int lane = lt & (kWave - 1), wave = lt >> 6;
@@ -111,7 +112,7 @@ __device__ __forceinline__ void scan_item(const EngineArgs& a, KT* kv, int64_t s
         uint32_t v[kWaves];
 #pragma unroll
         for (int u = 0; u < kWaves; ++u) v[u] = (uint32_t)kv[b * kNodes + u * kWave + lane];  // node u*64 + lane
-        auto out = gptr(a.lists) + ((int64_t)(pg0 + b) * a.nblk + blk) * kL;  // global_: not in lgkmcnt
+        auto out = gptr(a.lists) + ((int64_t)(pg0 + b) * a.nblk + blk) * kLL;  // global_: not in lgkmcnt
         uint64_t thr = 0;
         if constexpr (prune) {
             const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)thr_l, j);
@@ -119,7 +120,7 @@ __device__ __forceinline__ void scan_item(const EngineArgs& a, KT* kv, int64_t s
             thr = ((uint64_t)hi << 32) | lo;
         }
         int cnt = 0, cq = 0;  // ranked entries; of them the ones >= thr (a prefix)
-        for (int r = 0; r < kL && cnt < kL; ++r) {
+        for (int r = 0; r < kLL && cnt < kLL; ++r) {
             uint32_t lm = v[0];
 #pragma unroll
             for (int u = 1; u < kWaves; ++u) lm = lm > v[u] ? lm : v[u];
@@ -136,10 +137,10 @@ __device__ __forceinline__ void scan_item(const EngineArgs& a, KT* kv, int64_t s
                 if (v[u] == m) {
                     const int rank = below + popc_below(mask, lane);
                     const uint64_t key = make_key(m, blk_base + u * kWave + lane);
-                    w = rank < kL && (!prune || key >= thr);
+                    w = rank < kLL && (!prune || key >= thr);
                     if (w) out[rank] = key;
                     // a full list: its 8th key is a threshold for every later block (fire and forget)
-                    if (prune && w && rank == kL - 1 && key > thr) *lthr_of(a, a.lset, copy, pg0 + b) = key;
+                    if (prune && w && rank == kLL - 1 && key > thr) *lthr_of(a, a.lset, copy, pg0 + b) = key;
                     v[u] = 0;
                 }
                 if constexpr (prune) cq += __popcll(__ballot(w));
@@ -148,9 +149,9 @@ __device__ __forceinline__ void scan_item(const EngineArgs& a, KT* kv, int64_t s
             cnt = below;
         }
         if constexpr (!prune) {
-            if (lane >= cnt && lane < kL) out[lane] = 0ull;
+            if (lane >= cnt && lane < kLL) out[lane] = 0ull;
         } else if (cq > 0) {
-            if (lane >= cq && lane < kL) out[lane] = 0ull;
+            if (lane >= cq && lane < kLL) out[lane] = 0ull;
             if (lane == 0)
                 atomicOr((unsigned long long*)(lbit_of(a, a.lset, pg0 + b) + (blk >> 6)), 1ull << (blk & 63));
         }

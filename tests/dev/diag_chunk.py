@@ -28,8 +28,8 @@ d = eng.debug_counters() - c0
 L = max(d[5], 1)
 print(f"launches {L}, pods/launch {d[6] / L:.1f} (batch {d[23] / L:.1f}), sweeps/launch {d[7] / L:.1f}, chunks/launch {d[8] / L:.2f}, "
       f"cids {d[21] / L:.0f}; wall {32768 / dt:.0f} pods/s")
-print("early stops by reason (unknown/rebound, buf ovf, trunc, exhausted, adm unknown or notfound/bad):", [int(x) for x in d[9:14]])
-print("cache split per launch: rebase + cached-node replays %.0f, cached pairs %.0f cycles" % (d[14] / L, d[22] / L))
+print("early stops by reason (row state unknown, buf ovf, trunc, exhausted, adm unknown or notfound/bad, "
+      "cached state unknown, both cached rebound):", [int(x) for x in d[9:14]] + [int(d[14]), int(d[22])])
 print("cycles per launch: setup %.0f, cache %.0f, sweeps %.0f (%.0f per sweep), finalize %.0f, commit %.0f" % (
     d[16] / L, d[17] / L, d[18] / L, d[18] / max(d[7], 1), d[19] / L, d[20] / L))
 print("exclusion-only rounds/launch %.1f; phases, cycles per round (both kinds): A marks %.0f, B replay %.0f, C decide %.0f, D converge %.0f" % ((d[28] / L,) + tuple(d[24 + q] / max(d[7] + d[28], 1) for q in range(4))))

@@ -41,8 +41,8 @@ class _X:  # what Engine.shard_host expects of an exchange
     h = None
 
 
-def run(world):
-    eng = Engine(tick_seconds=10, filter_mode=1, filters=7, scorers=((1, 1, 0), (2, 1, 0)))
+def run(world, flags=0):
+    eng = Engine(tick_seconds=10, filter_mode=1, filters=7, scorers=((1, 1, 0), (2, 1, 0)), engine_flags=flags)
     if world > 1:
         eng.shard_host(world, 0, _X(), 1)
     eng.load_nodes(enc["alloc"], enc["taint"], enc["label"])
@@ -54,7 +54,7 @@ def run(world):
     eng.close()
     nb = max(st["launches"], 1)
     us = lambda ms, n: ms / max(n, 1) * 1e3  # noqa: E731
-    print(f"world {world}: {st['step_ms'] / nb * 1e3:.1f} us per batch (profiled), {st['pods'] / nb:.1f} pods/batch")
+    print(f"world {world} flags {flags}: {st['step_ms'] / nb * 1e3:.1f} us per batch (profiled), {st['pods'] / nb:.1f} pods/batch")
     print(f"   prep {us(k['prep_ms'], k['prep_n']):.1f} us x {k['prep_n'] / nb:.2f}, scan {us(k['scan_ms'], k['scan_n']):.1f}, "
           f"merge {us(k['merge_ms'], k['merge_n']):.1f} (part merges {us(k['part_ms'], k['xchg_n']):.1f}, "
           f"host exchange {us(k['xchg_ms'], k['xchg_n']):.1f}), resolve {us(k['resolve_ms'], k['resolve_n']):.1f} x "
@@ -63,3 +63,4 @@ def run(world):
 
 run(1)
 run(WORLD)
+run(WORLD, _lib.KS_ENGINE_NO_OVERLAP)

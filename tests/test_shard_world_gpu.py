@@ -114,17 +114,17 @@ def test_c5_whole_trace_two_ranks_match_oracle_golden():
         done += k
 
 
-def test_c5_whole_trace_four_ranks_overlapped_match_oracle_golden():
-    """BASELINE configs[4] as 4 ranks x 2 parts: 1,024 scan blocks per rank, so every rank runs the
-    overlap (its speculative scan fused into its chunk kernel) on pruned lists (1M nodes), with the
-    exchange every batch — every pod of the C5 leg against tests/golden/full_run.json on every
-    rank."""
+def test_c5_whole_trace_sixteen_ranks_overlapped_match_oracle_golden():
+    """BASELINE configs[4] as 16 ranks: 256 scan blocks per rank, so every rank runs the overlap
+    (its speculative scan fused into its chunk kernel; ks_engine.cpp kOverlapMaxBlocks) on pruned
+    lists (1M nodes), with the exchange every batch — every pod of the C5 leg against
+    tests/golden/full_run.json on every rank."""
     g = full_run_digest.load("c5")
     if g is None:
         pytest.skip("no c5 golden")
     tr = tracegen.c5_trace(n_pods=g["pods"])
     enc = encoded(tr)
-    engs, _x = _ranks(tr, enc, 4, 2)
+    engs, _x = _ranks(tr, enc, 16, 1)
     done = 0
     for w, want in enumerate(g["bind_digests"]):
         k = min(g["window"], g["pods"] - done)
