@@ -63,6 +63,15 @@ __global__ __launch_bounds__(kPrepThreads) void window_prep_kernel(const EngineA
 // capacities are < 2^32 - 1).  The resolver stages all slots in LDS, so a pod's winner is one LDS
 // read away.
 // ---------------------------------------------------------------------------------------------
+#ifdef KS_MCL_DIAG  // (merge_cl sections, thread 0's cycles: ctr[6..12], workgroups ctr[5])
+#define MDG_AT(I, T)                                                                      \
+    do {                                                                                  \
+        const uint64_t t_ = prep::pstamp();                                               \
+        if (threadIdx.x == 0) atomicAdd((unsigned long long*)&a.ctr[(I)], t_ - (T));      \
+        (T) = t_;                                                                         \
+    } while (0)
+using prep::pstamp;
+#endif
 constexpr int kRecWords = 12;
 static_assert(kRecWords <= kRecDw, "record size");
 constexpr int kSlotsAll = kWinMaxB * kChR;  // claims a batch can make (slot_node holds every one)
@@ -95,6 +104,7 @@ __device__ __forceinline__ void cand_list(const EngineArgs& a, WinWS& ws, int i,
                                           const uint64_t (&ek)[kEPer]) {
     static_assert(kLL >= kTopL && kLL <= kWave, "one list entry per lane");
     const int tid = threadIdx.x;
+    PDG(uint64_t pt = pstamp();)
     __shared__ uint64_t buf[kClBuf];
     __shared__ int cnt;
     __shared__ uint64_t s_thr;
@@ -118,6 +128,7 @@ __device__ __forceinline__ void cand_list(const EngineArgs& a, WinWS& ws, int i,
         if (lane == 0) s_full = enough || last != 0;
     }
     __syncthreads();
+    PDG(MDG_AT(9, pt);)
     const uint64_t thr = s_thr;
     const bool full = s_full != 0;
 #pragma unroll
@@ -127,6 +138,7 @@ __device__ __forceinline__ void cand_list(const EngineArgs& a, WinWS& ws, int i,
             if (pos < kClBuf) buf[pos] = ek[q];
         }
     __syncthreads();
+    PDG(MDG_AT(10, pt);)
     const int c = cnt, n = c < kClBuf ? c : kClBuf;
     __shared__ uint64_t kept[kR];
     if (tid < n) {  // rank by counting (keys are distinct: the node is in the low bits)
@@ -136,6 +148,7 @@ __device__ __forceinline__ void cand_list(const EngineArgs& a, WinWS& ws, int i,
         if (r < kR) kept[r] = me;
     }
     __syncthreads();
+    PDG(MDG_AT(11, pt);)
     if (tid < kWave) {  // the kept entries' slots: one wave, one counter update for its claims
         const int lane = tid;
         const bool valid = lane < (n < kR ? n : kR);
@@ -179,6 +192,7 @@ __device__ __forceinline__ void cand_list(const EngineArgs& a, WinWS& ws, int i,
             ws.cl_slot[i][lane] = sl;
         }
     }
+    PDG(__syncthreads(); MDG_AT(12, pt);)
     if (tid == 0) {
         ws.cl_info[i] = (c < kR ? c : kR) | (c > kR ? kClTrunc : 0) | (full ? kClFull : 0) | (c > kClBuf ? kClOvf : 0);
         ws.cl_thr[i] = thr;
@@ -218,6 +232,7 @@ __global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs* __rest
         if (tid < 2 * kThrCopies) *lthr_of(a, tid / kThrCopies, tid % kThrCopies, b) = 0;
     }
     if (b >= ws.nb) return;  // (the window prep cut the batch; errors left nb = 0)
+    PDG(uint64_t pt = pstamp(); if (tid == 0) atomicAdd((unsigned long long*)&a.ctr[5], 1ull);)
     uint64_t top[kLL];
 #pragma unroll
     for (int k = 0; k < kLL; ++k) top[k] = 0;
@@ -275,6 +290,7 @@ __global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs* __rest
     }
     __shared__ uint64_t wl[kMergeMaxWaves][kLL];
     __shared__ uint64_t pc[kLL];
+    PDG(MDG_AT(6, pt);)
     int head = 0;
     for (int r = 0; r < kLL; ++r) {
         uint64_t h = 0;
@@ -286,6 +302,7 @@ __global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs* __rest
         if (hit && lane == __ffsll((unsigned long long)hit) - 1) head++;
     }
     __syncthreads();
+    PDG(MDG_AT(7, pt);)
     if (wave == 0 && nthr <= 256) {  // the wave lists' top kLL: one candidate per lane (4 waves)
         static_assert(4 * kLL <= kWave, "one candidate per lane");
         uint64_t v = lane < nwav * kLL ? wl[lane / kLL][lane % kLL] : 0ull;
@@ -322,6 +339,7 @@ __global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs* __rest
         }
     }
     __syncthreads();
+    PDG(MDG_AT(8, pt);)
     cand_list<kMode, kLL>(a, ws, b, pc, ek);
 }
 

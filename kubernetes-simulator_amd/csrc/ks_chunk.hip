@@ -108,6 +108,15 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// (k1 > k2 > k3 or zero) with their cids: insert key v of cid c (keys are distinct unless zero)
+__device__ __forceinline__ void top3_insert(uint64_t& k1, uint64_t& k2, uint64_t& k3, int& c1, int& c2, int& c3,
+                                            uint64_t v, int c) {
+    const bool g1 = v > k1, g2 = v > k2, g3 = v > k3;
+    k3 = g2 ? k2 : (g3 ? v : k3); c3 = g2 ? c2 : (g3 ? c : c3);
+    k2 = g1 ? k1 : (g2 ? v : k2); c2 = g1 ? c1 : (g2 ? c : c2);
+    k1 = g1 ? v : k1; c1 = g1 ? c : c1;
+}
+
 // ---------------------------------------------------------------------------------------------
 enum : uint8_t { kFlRun = 1, kFlTrunc = 2, kFlFull = 4, kFlOvf = 8 };
 
@@ -141,12 +150,11 @@ struct ChShared {
     // is not a first binder)
     alignas(16) int16_t smeta[kB][8];
     int32_t sst[kB][kSeg][4];     // segment states rc rm rg nr
-    uint64_t cd1[kC], cd2[kC];    // top two keys of pre-chunk nodes per chunk pod
-    int16_t cd1c[kC], cd2c[kC];
+    uint64_t cd1[kC], cd2[kC], cd3[kC];  // top three keys of pre-chunk nodes per chunk pod
+    int16_t cd1c[kC], cd2c[kC], cd3c[kC];
     uint8_t cdbad[kC];
     struct {
-        uint64_t k[kWaves][kC][2];
-        int16_t c[kWaves][kC][2];  // k[.][.][1] == ~0: the lane met an unknown state
+        uint64_t k[kWaves][kC][2];  // scratch: slot requests (setup), avail lists (guess), pair totals (sweeps)
     } x;
     uint32_t brow[kC][4];         // chunk pod c0 + r: request words (saturated), key mask | run << 3 |
                                   // own expiry's pod (kNoOwn: none) << 16
@@ -410,7 +418,7 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
     // node_slot, its record staged): slots < kCidSlots are cids; a pod with an entry on a later slot
     // cuts the batch before it — except pod 0, whose entries there take the private cids
     // kCidSlots + r (its record read here), so every launch binds at least one pod.
-    DG(uint64_t t_setup = dstamp(); uint64_t acc_cd = 0, acc_sw = 0, acc_fin = 0, acc_ph[4] = {0, 0, 0, 0}, acc_cs = 0, acc_rb = 0, acc_cdp = 0; int n_sweeps = 0, n_sonly = 0, n_chunks = 0;)
+    DG(uint64_t t_setup = dstamp(); uint64_t acc_cd = 0, acc_sw = 0, acc_fin = 0, acc_ph[4] = {0, 0, 0, 0}, acc_cs = 0, acc_rb = 0, acc_cdp = 0, acc_rbase = 0, acc_red = 0, acc_crep = 0; int n_sweeps = 0, n_sonly = 0, n_chunks = 0;)
     const int nslot = ws.nslot < kWinMaxB * kR ? ws.nslot : kWinMaxB * kR;
     const int nlo = nslot < kCidSlots ? nslot : kCidSlots;
     // (1) every global read of the setup issued before any is used: one round trip (the lists and
@@ -563,6 +571,7 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
                 }
             }
             __syncthreads();
+            DG(acc_rbase += dstamp() - t0;)
             tb = c0;
             if (sh.cut <= c0) {  // an own expiry could not be tracked: commit the pods before c0
                 committed = c0;
@@ -578,67 +587,72 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
             }
             __syncthreads();
             DG(uint64_t tr1 = dstamp(); acc_rb += tr1 - t0;)
-            {
-                const int i = c0 + lane;
+            {  // eight lanes per chunk pod (pod c0 + tid / 8), lane s8 takes the rows j = s8 + 8 t
+                const int pi = tid >> 3, s8 = tid & 7;
+                const int i = c0 + pi;
                 const bool li = i < c1;
                 const PodRec p = sh.pod[li ? i : c0];
                 // a cached key below thr_i never decides pod i: a winner from the static list is
                 // >= thr_i, and without one D must beat thr_i (or the last kept entry, >= thr_i)
                 const uint64_t lbc = li ? ws.cl_thr[i] : 0ull;
-                uint64_t k1 = 0, k2 = 0;
-                int16_t q1 = -1, q2 = -1;
+                uint64_t k1 = 0, k2 = 0, k3 = 0;
+                int q1 = -1, q2 = -1, q3 = -1;
                 bool bad = false;
-                // four slots per step (j = wave + 8 (4 t + q)), their loads issued together
-                for (int j0 = wave; j0 < c0; j0 += 4 * kWaves) {
+                // four rows per step (j = s8 + 8 (4 t + q)), their loads issued together
+                for (int j0 = s8; j0 < c0; j0 += 4 * kLanesPerPod) {
                     SRow r[4];
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        const int j = j0 + q * kWaves;
+                        const int j = j0 + q * kLanesPerPod;
                         r[q] = srow(sh, j < c0 ? j : 0);
                         if (j >= c0) r[q].clear_cid();
                     }
+                    // the exact keys (keys below lbc dropped); the wide evaluator first tries the
+                    // float bound — for the 32-bit evaluators the prune saved nothing: in SIMT the
+                    // evaluation runs whenever one lane passes, and these nodes, the batch's earlier
+                    // winners, are near the top of most pods' lists.  The 32-bit evaluators run the
+                    // four rows without branches (an empty row evaluates cid 0 and is masked), so
+                    // their four dependent LDS-and-VALU chains interleave.
+                    uint64_t key[4];
+                    int kc[4];
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        const int j = j0 + q * kWaves;
+                        const int j = j0 + q * kLanesPerPod;
                         const int k = r[q].m(kMCid);
-                        if (k < 0 || !li) continue;
-                        if (r[q].m(kMOvf) <= i) { bad = true; continue; }
-                        // the exact key (keys below lbc dropped); the wide evaluator first tries
-                        // the float bound — for the 32-bit evaluators the prune saved nothing: in
-                        // SIMT the evaluation runs whenever one lane passes, and these nodes, the
-                        // batch's earlier winners, are near the top of most pods' lists
-                        uint64_t key;
-                        if constexpr (kMode == kEvalWide) key = key_at_lb<kMode>(a, sh, p, i, k, j, r[q], lbc);
-                        else key = key_at<kMode>(a, sh, p, i, k, j, r[q]);
-                        key = key < lbc ? 0ull : key;
-                        if (key > k1) { k2 = k1; q2 = q1; k1 = key; q1 = (int16_t)k; }
-                        else if (key > k2) { k2 = key; q2 = (int16_t)k; }
+                        const bool on = k >= 0 && li;
+                        const bool ok = on && r[q].m(kMOvf) > i;
+                        bad |= on && !ok;
+                        kc[q] = k;
+                        if constexpr (kMode == kEvalWide) {
+                            key[q] = ok ? key_at_lb<kMode>(a, sh, p, i, k, j, r[q], lbc) : 0ull;
+                        } else {
+                            const uint64_t kq = key_at<kMode>(a, sh, p, i, k >= 0 ? k : 0, j, r[q]);
+                            key[q] = ok ? kq : 0ull;
+                        }
                     }
-                }
-                sh.x.k[wave][lane][0] = k1; sh.x.k[wave][lane][1] = bad ? ~0ull : k2;
-                sh.x.c[wave][lane][0] = q1; sh.x.c[wave][lane][1] = q2;
-            }
-            __syncthreads();
-            DG(acc_cdp += dstamp() - tr1;)
-            if (wave == 0) {
-                uint64_t k1 = 0, k2 = 0;
-                int16_t q1 = -1, q2 = -1;
-                bool bad = false;
-#pragma unroll 4
-                for (int g = 0; g < kWaves; ++g) {
-                    if (sh.x.k[g][lane][1] == ~0ull) { bad = true; continue; }
 #pragma unroll
-                    for (int z = 0; z < 2; ++z) {
-                        const uint64_t key = sh.x.k[g][lane][z];
-                        const int16_t q = sh.x.c[g][lane][z];
-                        if (key > k1) { k2 = k1; q2 = q1; k1 = key; q1 = q; }
-                        else if (key > k2) { k2 = key; q2 = q; }
-                    }
+                    for (int q = 0; q < 4; ++q) top3_insert(k1, k2, k3, q1, q2, q3, key[q] < lbc ? 0ull : key[q], kc[q]);
                 }
-                sh.cd1[lane] = k1; sh.cd2[lane] = k2; sh.cd1c[lane] = q1; sh.cd2c[lane] = q2; sh.cdbad[lane] = bad;
+                // the pod's top three over its eight lanes (distinct keys: one node per row)
+#pragma unroll
+                for (int o = 1; o < kLanesPerPod; o <<= 1) {
+                    const uint64_t o1 = shfl_xor64(k1, o), o2 = shfl_xor64(k2, o), o3 = shfl_xor64(k3, o);
+                    const int c1_ = __shfl_xor(q1, o), c2_ = __shfl_xor(q2, o), c3_ = __shfl_xor(q3, o);
+                    top3_insert(k1, k2, k3, q1, q2, q3, o1, c1_);
+                    top3_insert(k1, k2, k3, q1, q2, q3, o2, c2_);
+                    top3_insert(k1, k2, k3, q1, q2, q3, o3, c3_);
+                }
+                bad = ((__ballot(bad) >> (lane & ~7)) & 0xFFull) != 0;
+                if (s8 == 0) {
+                    sh.cd1[pi] = k1; sh.cd2[pi] = k2; sh.cd3[pi] = k3;
+                    sh.cd1c[pi] = (int16_t)q1; sh.cd2c[pi] = (int16_t)q2; sh.cd3c[pi] = (int16_t)q3;
+                    sh.cdbad[pi] = bad;
+                }
             }
+            DG(__syncthreads(); acc_cdp += dstamp() - tr1;)
         } else if (tid < kC) {
-            sh.cd1[tid] = 0; sh.cd2[tid] = 0; sh.cd1c[tid] = -1; sh.cd2c[tid] = -1; sh.cdbad[tid] = 0;
+            sh.cd1[tid] = 0; sh.cd2[tid] = 0; sh.cd3[tid] = 0;
+            sh.cd1c[tid] = -1; sh.cd2c[tid] = -1; sh.cd3c[tid] = -1; sh.cdbad[tid] = 0;
         }
         __syncthreads();
 
@@ -696,20 +710,20 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
             // chunk, on its replayed state) when it beats the static pick — fewer full sweeps
             // correct it (the guess only seeds the sweeps: any guess gives the sequential result)
             const bool dok = c0 > 0 && i < c1 && !sh.cdbad[lane];
-            const uint64_t d1 = dok ? sh.cd1[lane] : 0ull, d2 = dok ? sh.cd2[lane] : 0ull;
-            const int dc1 = d1 ? sh.cd1c[lane] : 0, dc2 = d2 ? sh.cd2c[lane] : 0;
+            const uint64_t d1 = dok ? sh.cd1[lane] : 0ull, d2 = dok ? sh.cd2[lane] : 0ull, d3 = dok ? sh.cd3[lane] : 0ull;
+            const int dc1 = d1 ? sh.cd1c[lane] : 0, dc2 = d2 ? sh.cd2c[lane] : 0, dc3 = d3 ? sh.cd3c[lane] : 0;
             int cur = -1, lo_l = 0;
             for (;;) {
                 DG(++n_sonly;)
                 const bool act = lane >= lo_l && nc > 0;
                 int nw = act ? -1 : cur;
                 uint32_t nwt = 0;
-                uint64_t m1, m2;
+                uint64_t m1, m2, m3;
                 {  // probe the first eight (every lane, unconditional loads), then the rest if needed
                     uint64_t cm[8];
 #pragma unroll
                     for (int q = 0; q < 8; ++q) cm[q] = sh.cmask[rg[q]];
-                    m1 = sh.cmask[dc1]; m2 = sh.cmask[dc2];
+                    m1 = sh.cmask[dc1]; m2 = sh.cmask[dc2]; m3 = sh.cmask[dc3];
 #pragma unroll
                     for (int q = 7; q >= 0; --q)  // the lowest free entry wins
                         if (act && q < na && (cm[q] & below) == 0) { nw = rg[q]; nwt = rt[q]; }
@@ -726,8 +740,9 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
                     if (act && nw < 0) { nw = nw2; nwt = nwt2; }
                 }
                 if (act && d1) {
-                    const uint64_t dk = !(m1 & below) ? d1 : ((d2 && !(m2 & below)) ? d2 : 0ull);
-                    const int dc = !(m1 & below) ? dc1 : dc2;
+                    const bool f1 = !(m1 & below), f2 = d2 && !(m2 & below), f3 = d3 && !(m3 & below);
+                    const uint64_t dk = f1 ? d1 : (f2 ? d2 : (f3 ? d3 : 0ull));
+                    const int dc = f1 ? dc1 : (f2 ? dc2 : dc3);
                     const uint64_t sk = nw >= 0 ? cl_key(sh, nwt) : 0ull;
                     if (dk > sk) nw = dc;
                 }
@@ -909,7 +924,11 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
                         if (ck != 0 && (sh.cmask[cc] & below)) {
                             ck = sh.cd2[pi];
                             cc = sh.cd2c[pi];
-                            if (ck != 0 && (sh.cmask[cc] & below)) { bad = true; DG(dwhy |= half ? 32 : 4;) }
+                            if (ck != 0 && (sh.cmask[cc] & below)) {
+                                ck = sh.cd3[pi];
+                                cc = sh.cd3c[pi];
+                                if (ck != 0 && (sh.cmask[cc] & below)) { bad = true; DG(dwhy |= half ? 32 : 4;) }
+                            }
                         }
                         if (ck > dk) { dk = ck; dc = cc; }
                     }
@@ -1061,6 +1080,7 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
             a.s.rc[n] = use64(v.rc); a.s.rm[n] = use64(v.rm); a.s.rg[n] = use64(v.rg); a.s.nr[n] = v.nr;
         }
     }
+    DG(__syncthreads(); acc_crep = dstamp() - t3;)
     // slot-E nodes that are no candidate of this batch: their expiries before pod c - 1's bind
     // here (requests from the LDS words: exact, an admitted request is below its capacity < 2^32)
     static_assert(kSlots <= kThreads, "one slot-E node per thread");
@@ -1125,10 +1145,17 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
         atomicAdd(&d[21], (unsigned long long)ncid);
         (void)acc_cdp; (void)acc_rb;  // (d[14], d[22]: stop reasons 5, 6)
         atomicAdd(&d[23], (unsigned long long)nb);
+#if KS_CHUNK_DIAG == 2  // finer split (tests/dev/diag_chunk.py --d2): cache parts, commit replays, setup loads
+        atomicAdd(&d[24], acc_rbase); atomicAdd(&d[25], acc_rb - acc_rbase); atomicAdd(&d[26], acc_cdp);
+        atomicAdd(&d[27], acc_red); atomicAdd(&d[28], acc_crep); atomicAdd(&d[31], ts1 - (ts3 - t_setup));
+        (void)acc_ph; (void)n_sonly; (void)cs_e; (void)cs_r; (void)cs_x;
+#else
+        (void)acc_rbase; (void)acc_red; (void)acc_crep;
         for (int q = 0; q < 4; ++q) atomicAdd(&d[24 + q], acc_ph[q]);
         atomicAdd(&d[28], (unsigned long long)n_sonly);
+        atomicAdd(&d[29], cs_e); atomicAdd(&d[30], cs_r); atomicAdd(&d[31], cs_x);
+#endif
         atomicAdd(&d[15], acc_cs);
-            atomicAdd(&d[29], cs_e); atomicAdd(&d[30], cs_r); atomicAdd(&d[31], cs_x);
     }
 #endif
 }
@@ -1161,8 +1188,15 @@ __global__ __launch_bounds__(kThreads) void chunk_scan_kernel(const EngineArgs* 
         __syncthreads();
         const int64_t st = sh.t_start, en = sh.t_end, er = sh.t_err;
         __syncthreads();  // (the window's scratch overlays the resolver's LDS)
+#if defined(KS_CHUNK_DIAG) && KS_CHUNK_DIAG == 2
+        const uint64_t tp0 = dstamp();
+#endif
         static_assert(sizeof(prep::PrepLDS) <= sizeof(ChShared), "window scratch");
         prep::prep_body<kThreads>(A[0], st, en, er, 1, 1, slot, *reinterpret_cast<prep::PrepLDS*>(&sh));
+#if defined(KS_CHUNK_DIAG) && KS_CHUNK_DIAG == 2
+        __syncthreads();
+        if (threadIdx.x == 0) atomicAdd((unsigned long long*)&A[0].ctr[30], dstamp() - tp0);
+#endif
         return;
     }
     static_assert(kThreads == 2 * scn::kNodes, "two scan groups per workgroup");

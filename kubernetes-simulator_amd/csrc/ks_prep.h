@@ -24,6 +24,28 @@ namespace ks {
 namespace prep {
 
 constexpr int kEHashLog2 = 12, kEHash = 1 << kEHashLog2;
+
+// Diagnostic build only (-DKS_MCL_DIAG, tests/dev/diag_mcl.py): section cycles of thread 0 in
+// ctr[16..22] (the window prep) — the product executes none of it.
+#ifdef KS_MCL_DIAG
+__device__ __forceinline__ uint64_t pstamp() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define PDG(...) __VA_ARGS__
+#define PDG_AT(I, T)                                                                      \
+    do {                                                                                  \
+        const uint64_t t_ = pstamp();                                                     \
+        if (threadIdx.x == 0) atomicAdd((unsigned long long*)&a.ctr[16 + (I)], t_ - (T)); \
+        (T) = t_;                                                                         \
+    } while (0)
+#else
+#define PDG(...)
+#define PDG_AT(I, T)
+#endif
 static_assert(2 * kEMax <= kEHash, "E hash load <= 1/2");
 
 __device__ __forceinline__ uint32_t ehslot(int32_t n) { return ((uint32_t)n * 2654435761u) >> (32 - kEHashLog2); }
@@ -46,6 +68,7 @@ __device__ __forceinline__ void prep_body(const EngineArgs& a, int64_t start, in
     static_assert(NT / 64 <= 16, "wave sums");
     WinWS& ws = *a.sw;
     const int tid = threadIdx.x;
+    PDG(uint64_t pt = pstamp();)
     int64_t* const spec_out = a.spec_ctr + kSpecStride * slot;
     const int64_t* const spec_in = a.spec_ctr + kSpecStride * (slot ^ 1);
     int nb = (int)min<int64_t>(min<int64_t>(a.B, kWinMaxB), end - start);
@@ -62,6 +85,7 @@ __device__ __forceinline__ void prep_body(const EngineArgs& a, int64_t start, in
     for (int h = tid; h < kEHash; h += NT) L.hk[h] = -1;
     if (tid == 0) { L.s_ne = 0; L.s_nx = 0; }
     nb = __syncthreads_count(fits_win);  // exp_off is non-decreasing: a prefix of the pods
+    PDG_AT(0, pt);
     const int e_cnt = (int)(a.exp_off[start + nb] - e_base);
     int rescan = 0;
     if (spec) rescan = start != spec_in[kCtrStart] || (int64_t)e_cnt + (e1 - e0) + ws.n_touched > kEMax;
@@ -111,6 +135,7 @@ __device__ __forceinline__ void prep_body(const EngineArgs& a, int64_t start, in
         if (claimed) L.hv[h] = atomicAdd(&L.s_ne, 1);
     }
     __syncthreads();
+    PDG_AT(1, pt);
     const int n_es = L.s_ne;  // the slot nodes; the touched nodes after them (no slots)
     __syncthreads();
     const int n_x = L.s_nx;
@@ -125,6 +150,7 @@ __device__ __forceinline__ void prep_body(const EngineArgs& a, int64_t start, in
         }
     }
     __syncthreads();
+    PDG_AT(2, pt);
     const int n_e = L.s_ne;
     if (tid < n_es) { L.cnt[tid] = 0; L.fill[tid] = 0; }
     __syncthreads();
@@ -135,6 +161,7 @@ __device__ __forceinline__ void prep_body(const EngineArgs& a, int64_t start, in
         atomicAdd(&L.cnt[k_of], 1);
     }
     __syncthreads();
+    PDG_AT(3, pt);
     {  // exclusive prefix of the slot nodes' counts (n_es <= kWinSlots: one per thread)
         const int lane = tid & 63, wv = tid >> 6;
         const int v = tid < n_es ? L.cnt[tid] : 0;
@@ -153,8 +180,10 @@ __device__ __forceinline__ void prep_body(const EngineArgs& a, int64_t start, in
         if (n_es == 0 && tid == 0) ws.e_off[0] = 0;
     }
     __syncthreads();
+    PDG_AT(4, pt);
     if (my_node >= 0) ws.e_slot[ws.e_off[k_of] + atomicAdd(&L.fill[k_of], 1)] = tid;  // slot x == tid
     __syncthreads();
+    PDG_AT(5, pt);
     if (tid < n_es) {  // each node's few slots ascending
         const int lo = ws.e_off[tid], hi = ws.e_off[tid + 1];
         for (int u = lo + 1; u < hi; ++u) {
@@ -171,6 +200,7 @@ __device__ __forceinline__ void prep_body(const EngineArgs& a, int64_t start, in
         // the next speculative scan: the pods after this batch, if it commits them all
         spec_out[kCtrStart] = start + nb; spec_out[kCtrEnd] = end; spec_out[kCtrErr] = 0;
     }
+    PDG(__syncthreads(); PDG_AT(6, pt); if (tid == 0) atomicAdd((unsigned long long*)&a.ctr[23], 1ull);)
 }
 
 }  // namespace prep

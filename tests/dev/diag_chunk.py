@@ -32,6 +32,12 @@ print("early stops by reason (row state unknown, buf ovf, trunc, exhausted, adm 
       "cached state unknown, both cached rebound):", [int(x) for x in d[9:14]] + [int(d[14]), int(d[22])])
 print("cycles per launch: setup %.0f, cache %.0f, sweeps %.0f (%.0f per sweep), finalize %.0f, commit %.0f" % (
     d[16] / L, d[17] / L, d[18] / L, d[18] / max(d[7], 1), d[19] / L, d[20] / L))
+if "--d2" in sys.argv:  # (make chunkdiag DIAGLVL=2 NAME=2: d[24..31] remapped)
+    print("cache per chunk with c0 > 0 (%.2f per launch): rebase %.0f, slot replays %.0f, top two %.0f, reduce %.0f cycles" % (
+        (d[8] - L) / L, *(d[24 + q] / max(d[8] - L, 1) for q in range(4))))
+    print("commit %.0f = replays %.0f + rest; tail window prep %.0f; setup loads to first barrier %.0f cycles per launch" % (
+        d[20] / L, d[28] / L, d[30] / L, d[31] / L))
+    sys.exit(0)
 print("exclusion-only rounds/launch %.1f; phases, cycles per round (both kinds): A marks %.0f, B replay %.0f, C decide %.0f, D converge %.0f" % ((d[28] / L,) + tuple(d[24 + q] / max(d[7] + d[28], 1) for q in range(4))))
 print("phase C per exclusion-only round %.0f, per full sweep %.0f cycles; B per full sweep %.0f" % (d[15] / max(d[28], 1), d[26] / max(d[7], 1), d[25] / max(d[7], 1)))
 print("phase C split per full sweep (wave 0, C1 and entries / rows / cached D + reduce): %.0f / %.0f / %.0f cycles" % (
