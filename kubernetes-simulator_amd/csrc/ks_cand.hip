@@ -101,7 +101,7 @@ constexpr int kEPer = kEMax / 256;
 // entries even when the previous batch bound some of the top ones.)
 template <int kMode, int kLL>
 __device__ __forceinline__ void cand_list(const EngineArgs& a, WinWS& ws, int i, const uint64_t* cand,
-                                          const uint64_t (&ek)[kEPer]) {
+                                          const uint64_t* ek, int n_e) {
     static_assert(kLL >= kTopL && kLL <= kWave, "one list entry per lane");
     const int tid = threadIdx.x;
     PDG(uint64_t pt = pstamp();)
@@ -131,11 +131,10 @@ __device__ __forceinline__ void cand_list(const EngineArgs& a, WinWS& ws, int i,
     PDG(MDG_AT(9, pt);)
     const uint64_t thr = s_thr;
     const bool full = s_full != 0;
-#pragma unroll
-    for (int q = 0; q < kEPer; ++q)
-        if (ek[q] != 0 && ek[q] >= thr) {
+    for (int k = tid; k < n_e; k += blockDim.x)
+        if (ek[k] != 0 && ek[k] >= thr) {
             const int pos = atomicAdd(&cnt, 1);
-            if (pos < kClBuf) buf[pos] = ek[q];
+            if (pos < kClBuf) buf[pos] = ek[k];
         }
     __syncthreads();
     PDG(MDG_AT(10, pt);)
@@ -251,26 +250,67 @@ __global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs* __rest
             lv0[2 * k + 1] = w.y;
         }
     }
-    uint64_t ek[kEPer];
+    // The E nodes' keys, into LDS, from the records the window prep staged (ws.e_rec: three 16-byte
+    // words per E node).  The first two per thread (E nodes tid, tid + nthr) have their reads issued
+    // with the counts (unconditionally, clamped into the arrays: one dependent round trip fewer);
+    // any further ones (more than 2 nthr E nodes) in a plain loop.
+    __shared__ uint64_t ek[kEMax];
+    const int n_e = ws.n_e;
     {
         const int64_t start = a.ctr[kCtrStart];
-        const PodRec p = a.pods[start + b];
-        const int hi = ws.win_hi[b], n_e = ws.n_e, n_es = ws.n_es;
+        const int hi = ws.win_hi[b], n_es = ws.n_es;
+        uint4 er[2][3];
+        int32_t en[2], eu[2], ue[2];
 #pragma unroll
-        for (int q = 0; q < kEPer; ++q) {
+        for (int q = 0; q < 2; ++q) {
             const int k = tid + q * nthr;
-            ek[q] = 0;
+            const int kc = k < kEMax ? k : kEMax - 1;
+            const int ks = k < kWinSlots ? k : kWinSlots;
+            en[q] = ws.e_node[kc];
+            const uint4* r = reinterpret_cast<const uint4*>(ws.e_rec[kc]);
+            er[q][0] = r[0]; er[q][1] = r[1]; er[q][2] = r[2];
+            eu[q] = ws.e_off[ks];
+            ue[q] = ws.e_off[ks < kWinSlots ? ks + 1 : ks];
+        }
+#if defined(KS_MCL_DIAG) && KS_MCL_DIAG == 2
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        uint64_t t_e0 = pstamp();
+        if (tid == 0) atomicAdd((unsigned long long*)&a.ctr[13], t_e0 - pt);
+#endif
+        const PodRec p = a.pods[start + b];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int k = tid + q * nthr;
             if (k >= n_e) continue;
+            NodeV v = get_rec12(er[q]);
+            if (k < n_es) {
+                for (int u = eu[q]; u < ue[q]; ++u) {
+                    const int x = ws.e_slot[u];
+                    if (x >= hi) break;  // ascending
+                    v.rc -= ws.ex_req[x][0]; v.rm -= ws.ex_req[x][1]; v.rg -= ws.ex_req[x][2]; v.nr -= 1;
+                }
+            }
+            ek[k] = make_key(eval_t<kMode>(a.c, p, v), (uint32_t)en[q]);
+        }
+#pragma unroll 1
+        for (int k = tid + 2 * nthr; k < n_e; k += nthr) {
             const int32_t n = ws.e_node[k];
-            NodeV v = load_node(a.s, n);
-            const int ue = k < n_es ? ws.e_off[k + 1] : 0;
-            for (int u = k < n_es ? ws.e_off[k] : 0; u < ue; ++u) {
+            const uint4* r = reinterpret_cast<const uint4*>(ws.e_rec[k]);
+            const uint4 w3[3] = {r[0], r[1], r[2]};
+            NodeV w = get_rec12(w3);
+            const int ue1 = k < n_es ? ws.e_off[k + 1] : 0;
+            for (int u = k < n_es ? ws.e_off[k] : 0; u < ue1; ++u) {
                 const int x = ws.e_slot[u];
                 if (x >= hi) break;  // ascending
-                v.rc -= ws.ex_req[x][0]; v.rm -= ws.ex_req[x][1]; v.rg -= ws.ex_req[x][2]; v.nr -= 1;
+                w.rc -= ws.ex_req[x][0]; w.rm -= ws.ex_req[x][1]; w.rg -= ws.ex_req[x][2]; w.nr -= 1;
             }
-            ek[q] = make_key(eval_t<kMode>(a.c, p, v), (uint32_t)n);
+            ek[k] = make_key(eval_t<kMode>(a.c, p, w), (uint32_t)n);
         }
+#if defined(KS_MCL_DIAG) && KS_MCL_DIAG == 2
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        if (tid == 0) { atomicAdd((unsigned long long*)&a.ctr[14], pstamp() - t_e0); atomicAdd((unsigned long long*)&a.ctr[24], (unsigned long long)(n_e > tid) + (n_e > tid + nthr)); }
+        if (tid == 0) atomicAdd((unsigned long long*)&a.ctr[25], (unsigned long long)n_e);
+#endif
     }
     if (has0) {  // (the first list is the thread's top as it is: sorted)
 #pragma unroll
@@ -340,7 +380,7 @@ __global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs* __rest
     }
     __syncthreads();
     PDG(MDG_AT(8, pt);)
-    cand_list<kMode, kLL>(a, ws, b, pc, ek);
+    cand_list<kMode, kLL>(a, ws, b, pc, ek, n_e);
 }
 
 }  // namespace sq

@@ -83,6 +83,23 @@ __device__ __forceinline__ NodeV load_node(const NodeSoA& s, int64_t i) {
     return v;
 }
 
+// A node's record in 12 words — the chunk resolver's format (ks_chunk.hip NS32): capacities and usage
+// as uint32 (-1 = an absent capacity; the engine routes an engine there only when its scaled
+// capacities are < 2^32 - 1), ap clamped to INT_MAX, taint, label — three 16-byte words.
+__device__ __forceinline__ void put_rec12(uint32_t* o, const NodeV& v) {
+    uint4* w = reinterpret_cast<uint4*>(o);
+    w[0] = make_uint4((uint32_t)v.ac, (uint32_t)v.am, (uint32_t)v.ag, (uint32_t)(v.ap > 0x7FFFFFFF ? 0x7FFFFFFF : v.ap));
+    w[1] = make_uint4((uint32_t)v.rc, (uint32_t)v.rm, (uint32_t)v.rg, (uint32_t)v.nr);
+    w[2] = make_uint4((uint32_t)v.taint, (uint32_t)(v.taint >> 32), (uint32_t)v.label, (uint32_t)(v.label >> 32));
+}
+__device__ __forceinline__ NodeV get_rec12(const uint4 (&w)[3]) {
+    auto cap = [](uint32_t x) { return x == 0xFFFFFFFFu ? (int64_t)-1 : (int64_t)x; };
+    NodeV v;
+    v.ac = cap(w[0].x); v.am = cap(w[0].y); v.ag = cap(w[0].z); v.ap = (int32_t)w[0].w;
+    v.rc = (int64_t)w[1].x; v.rm = (int64_t)w[1].y; v.rg = (int64_t)w[1].z; v.nr = (int32_t)w[1].w;
+    v.taint = w[2].x | ((uint64_t)w[2].y << 32); v.label = w[2].z | ((uint64_t)w[2].w << 32);
+    return v;
+}
 // Admission / resource-fit (kubesim/node/node.go:44-47).  Keys requested only by running
 // pods cannot fail: they passed admission against the same static capacity and requests are
 // non-negative.  An absent capacity key is -1, so any request of that
@@ -665,6 +682,10 @@ struct WinWS {
     int32_t e_node[kEMax];
     int32_t e_off[kWinSlots + 1];         // E node k < n_es: its slots e_slot[e_off[k] .. e_off[k+1]) ascending
     int32_t e_slot[kWinSlots];
+    // E node k's record after the window's head (put_rec12), staged by the first workgroups of the
+    // scan launch before merge_cl (ks_kernels.hip scan_kernel): each merge_cl workgroup reads three
+    // contiguous 16-byte words per E node instead of gathering ten scattered fields
+    uint32_t e_rec[kEMax][12];
     // pod i's static candidates, sorted descending
     uint64_t cl_key[kWinMaxB][kChR];
     int32_t cl_info[kWinMaxB];            // kept count | kClTrunc | kClFull | kClOvf
@@ -747,7 +768,7 @@ hipError_t launch_expire_head(const EngineArgs* d, int S, hipStream_t st);
 // L: the block lists' length (kTopL; kTopLOverlap for the overlap's single-shard engines: key16, not
 // pruned)
 hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int mode, bool key16, hipStream_t st,
-                       bool cond = false, bool prune = false, int L = kTopL);
+                       bool cond = false, bool prune = false, int L = kTopL, bool stage = false);
 // per scenario and pod b < batch size: exact top-L over nl sorted lists
 // lists[b*pod_stride + k*list_stride] into out (lists == nullptr: the scenario's own block lists
 // into its candidate lists)

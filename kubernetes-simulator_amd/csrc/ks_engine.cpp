@@ -1263,7 +1263,8 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
             // (an overlapped batch's window was computed by the previous chunk kernel after its commit)
             if (!spec) HIPCHK(e, fused ? ks::launch_window_prep(d, true, false, (int)(b & 1), st) : ks::launch_expire_head(d, 1, st));
             if (ev[1]) HIPCHK(e, hipEventRecord(ev[1], st));
-            HIPCHK(e, ks::launch_scan(d, 1, e->blk_n, e->B, e->PG, e->mode, key16(e), st, spec, e->prune, e->L));
+            // (chunk class: the scan launch also stages the batch's E records for merge_cl)
+            HIPCHK(e, ks::launch_scan(d, 1, e->blk_n, e->B, e->PG, e->mode, key16(e), st, spec, e->prune, e->L, fused));
             if (ev[2]) HIPCHK(e, hipEventRecord(ev[2], st));
             const int G = e->world * e->vsh;
             hipEvent_t evx[2] = {ev[5], ev[6]};  // part merges | exchange | merge (sharded engines)

@@ -55,6 +55,7 @@ struct PrepLDS {
     int32_t hk[kEHash], hv[kEHash];
     int32_t cnt[kWinSlots], fill[kWinSlots];
     int32_t xn[kEMax];  // touched nodes to insert (overlap)
+    int64_t off[kWinMaxB];  // exp_off[start + 1 + i]
     int32_t wsum[16];
     int32_t s_ne, s_nx;
 };
@@ -79,19 +80,58 @@ __device__ __forceinline__ void prep_body(const EngineArgs& a, int64_t start, in
         }
         return;
     }
+    // Three dependent global round trips: (1) the CSR offsets and positions of the batch's pods, the
+    // speculative counters and the touched nodes (read speculatively, bounded by their arrays);
+    // (2) the expiring pods of the head and of the window; (3) their records and bind state.  (Every
+    // read is issued before the head's atomics and stores: the compiler cannot move a read across
+    // them.)  A head pod and a window pod are never the same pod (one expiry per pod).
     const int64_t e0 = a.exp_off[start], e1 = a.exp_off[start + 1];
     const int64_t e_base = e1;
-    const bool fits_win = tid < nb && a.exp_off[start + tid + 1] - e_base <= kWinSlots;
+    const int64_t myoff = tid < nb ? a.exp_off[start + tid + 1] : 0;
+    const int64_t mypos = tid < nb ? a.exp_pos[start + tid] : 0;
+    const int64_t sp_start = spec ? spec_in[kCtrStart] : 0;
+    const int n_touched = spec ? ws.n_touched : 0;
+    constexpr int kTPer = (kTouchMax + NT - 1) / NT;
+    int32_t tch[kTPer];
+#pragma unroll
+    for (int q = 0; q < kTPer; ++q) {
+        const int t = tid + q * NT;
+        tch[q] = spec && t < kTouchMax ? ws.touched[t] : -1;
+    }
+    const bool fits_win = tid < nb && myoff - e_base <= kWinSlots;
+    if (tid < nb) L.off[tid] = myoff;
     for (int h = tid; h < kEHash; h += NT) L.hk[h] = -1;
     if (tid == 0) { L.s_ne = 0; L.s_nx = 0; }
     nb = __syncthreads_count(fits_win);  // exp_off is non-decreasing: a prefix of the pods
     PDG_AT(0, pt);
-    const int e_cnt = (int)(a.exp_off[start + nb] - e_base);
+    const int e_cnt = (int)(L.off[nb - 1] - e_base);  // exp_off[start + nb] - e_base (nb >= 1: pod 0 fits)
     int rescan = 0;
-    if (spec) rescan = start != spec_in[kCtrStart] || (int64_t)e_cnt + (e1 - e0) + ws.n_touched > kEMax;
+    if (spec) rescan = start != sp_start || (int64_t)e_cnt + (e1 - e0) + n_touched > kEMax;
     const bool touch = spec && !rescan;
+    const int32_t hq = head && tid < e1 - e0 ? a.exp_pod[e0 + tid] : -1;
+    const int32_t wq = tid < e_cnt ? a.exp_pod[e_base + tid] : -1;
+    int32_t hst = 1, hex = 1, hnd = 0, wst = 1, wex = 1, wnd = 0;
+    int64_t hr0 = 0, hr1 = 0, hr2 = 0, wr0 = 0, wr1 = 0, wr2 = 0;
+    if (hq >= 0) {
+        hst = a.b_status[hq]; hex = a.expired[hq]; hnd = a.b_node[hq];
+        const PodRec& p = a.pods[hq];
+        hr0 = p.req[0]; hr1 = p.req[1]; hr2 = p.req[2];
+    }
+    if (wq >= 0) {
+        wst = a.b_status[wq]; wex = a.expired[wq]; wnd = a.b_node[wq];
+        const PodRec& p = a.pods[wq];
+        wr0 = p.req[0]; wr1 = p.req[1]; wr2 = p.req[2];
+    }
     if (head) {  // expire_head's work: the expiries due before the batch's first pod
-        for (int64_t e = e0 + tid; e < e1; e += NT) {
+        if (hq >= 0 && hst == 0 && !hex) {
+            atomicAdd((unsigned long long*)&a.s.rc[hnd], (unsigned long long)(-hr0));
+            atomicAdd((unsigned long long*)&a.s.rm[hnd], (unsigned long long)(-hr1));
+            atomicAdd((unsigned long long*)&a.s.rg[hnd], (unsigned long long)(-hr2));
+            atomicAdd((unsigned long long*)&a.s.nr[hnd], (unsigned long long)(-1ll));
+            a.expired[hq] = 1;
+            if (touch) L.xn[atomicAdd(&L.s_nx, 1)] = hnd;
+        }
+        for (int64_t e = e0 + NT + tid; e < e1; e += NT) {  // (more head expiries than threads)
             const int32_t q = a.exp_pod[e];
             if (a.b_status[q] != 0 || a.expired[q]) continue;
             const int32_t nd = a.b_node[q];
@@ -105,22 +145,21 @@ __device__ __forceinline__ void prep_body(const EngineArgs& a, int64_t start, in
         }
     }
     if (touch) {
-        for (int t = tid; t < ws.n_touched; t += NT) L.xn[atomicAdd(&L.s_nx, 1)] = ws.touched[t];
+#pragma unroll
+        for (int q = 0; q < kTPer; ++q)
+            if (tid + q * NT < n_touched) L.xn[atomicAdd(&L.s_nx, 1)] = tch[q];
     }
     if (tid < nb) {
-        ws.win_hi[tid] = tid >= 1 ? (int32_t)(a.exp_off[start + tid + 1] - e_base) : 0;
-        const int64_t pos = a.exp_pos[start + tid];
-        ws.own[tid] = (pos >= e_base && pos - e_base < e_cnt) ? (int32_t)(pos - e_base) : -1;
+        ws.win_hi[tid] = tid >= 1 ? (int32_t)(myoff - e_base) : 0;
+        ws.own[tid] = (mypos >= e_base && mypos - e_base < e_cnt) ? (int32_t)(mypos - e_base) : -1;
     }
     int32_t my_node = -1, my_k = -1;
     if (tid < e_cnt) {
-        const int32_t q = a.exp_pod[e_base + tid];
-        const PodRec& pq = a.pods[q];
-        ws.ex_q[tid] = q;
-        ws.ex_req[tid][0] = pq.req[0]; ws.ex_req[tid][1] = pq.req[1]; ws.ex_req[tid][2] = pq.req[2];
-        const bool ok = q < start && a.b_status[q] == 0 && !a.expired[q];
+        ws.ex_q[tid] = wq;
+        ws.ex_req[tid][0] = wr0; ws.ex_req[tid][1] = wr1; ws.ex_req[tid][2] = wr2;
+        const bool ok = wq < start && wst == 0 && !wex;
         ws.ex_ok[tid] = ok ? 1 : 0;
-        if (ok) my_node = a.b_node[q];
+        if (ok) my_node = wnd;
     }
     if (my_node >= 0) {
         uint32_t h = ehslot(my_node);

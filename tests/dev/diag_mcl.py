@@ -31,3 +31,6 @@ print(f"   total {sum(d[6:13]) / W:.0f}; wall {32768 / dt:.0f} pods/s")
 P = max(d[23], 1)
 pn = ("loads to count", "head+window loads, hashing", "touched inserts", "counts", "prefix", "slot fill", "sort+e_idx+tail")
 print(f"window preps {P}; cycles each: " + ", ".join(f"{n} {d[16 + q] / P:.0f}" for q, n in enumerate(pn)) + f"; total {sum(d[16:23]) / P:.0f}")
+if "--d2" in sys.argv:  # (DEFS=-DKS_MCL_DIAG=2: waits inserted, timing shifts)
+    print(f"thread 0: to the first reads (counts, pod index, first list) {d[13] / W:.0f}, E chain {d[14] / W:.0f} cycles "
+          f"over {d[24] / W:.2f} E nodes; n_e {d[25] / W:.1f}")
