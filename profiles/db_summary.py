@@ -2,6 +2,9 @@
 
   python profiles/db_summary.py stats DB OUT.csv
       per-kernel dispatch statistics in rocprofv3's --stats CSV layout
+  python profiles/db_summary.py timeline DB OUT.txt
+      the batch chain as the GPU ran it: per kernel the average duration, per (kernel -> next kernel)
+      pair the average idle gap between them, and the busy / idle split of the traced span
   python profiles/db_summary.py pmc FETCH_DB WRITE_DB SQ_DB OUT.json NOTE
       per-kernel averages of the PMC passes (profiles/collect.sh; SQ_DB may be ""); HBM bytes per launch =
       2 x FETCH_SIZE + WRITE_SIZE (KB x 1024), the gfx950 correction of MI355X_MICROARCH.md §HBM
@@ -33,6 +36,28 @@ def stats(db, out):
         for name, v in sorted(rows.items(), key=lambda kv: -sum(kv[1])):
             w.writerow([name, len(v), sum(v), sum(v) / len(v), 100.0 * sum(v) / total, min(v), max(v),
                         statistics.pstdev(v)])
+
+
+def timeline(db, out):
+    c = sqlite3.connect(db)
+    ks = sorted((float(s), float(e), short(n)) for n, s, e in c.execute("select name, start, end from kernels"))
+    dur = collections.defaultdict(list)
+    gaps = collections.defaultdict(list)
+    for i, (s, e, n) in enumerate(ks):
+        dur[n].append(e - s)
+        if i + 1 < len(ks):
+            g = ks[i + 1][0] - e
+            if g < 1e6:  # (host-side pauses between steps, > 1 ms, are not chain gaps)
+                gaps[(n, ks[i + 1][2])].append(g)
+    busy = sum(e - s for s, e, _ in ks)
+    idle = sum(sum(v) for v in gaps.values())
+    with open(out, "w") as f:
+        f.write(f"kernels {len(ks)}, busy {busy / 1e6:.3f} ms, chain gaps {idle / 1e6:.3f} ms\n")
+        for n, v in sorted(dur.items(), key=lambda kv: -sum(kv[1])):
+            f.write(f"  {n}: {len(v)} x {statistics.mean(v) / 1e3:.2f} us\n")
+        f.write("gaps (kernel -> next): count x mean us\n")
+        for (a, b), v in sorted(gaps.items(), key=lambda kv: -sum(kv[1])):
+            f.write(f"  {a} -> {b}: {len(v)} x {statistics.mean(v) / 1e3:.2f} us\n")
 
 
 def per_kernel(db):
@@ -72,7 +97,9 @@ def pmc(fetch_db, write_db, sq_db, out, note):
 
 
 if __name__ == "__main__":
-    if sys.argv[1] == "stats":
+    if sys.argv[1] == "timeline":
+        timeline(sys.argv[2], sys.argv[3])
+    elif sys.argv[1] == "stats":
         stats(sys.argv[2], sys.argv[3])
     elif sys.argv[1] == "pmc":
         pmc(*sys.argv[2:7])
