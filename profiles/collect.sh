@@ -1,8 +1,8 @@
 #!/bin/bash
 # Profile recipe for the committed summaries (run on the GPU box from the repo root):
 #   bash profiles/collect.sh OUTDIR
-# 1. rocprofv3 kernel trace + stats of the C3 bench (short, the line's own chain: overlap on), the
-#    C4 bench and the C5 bench;
+# 1. rocprofv3 kernel trace + stats of the C3 bench (short, the line's own chain: overlap on; with the
+#    batch chain's per-kernel durations and gaps, db_summary.py timeline), the C4 bench and the C5 bench;
 # 2. the PMC passes (one counter group per run): FETCH_SIZE, WRITE_SIZE, and the SQ instruction /
 #    wave-cycle counters, for C3 and C5; 3. CSV / JSON summaries of the result databases
 #    (profiles/db_summary.py).  Every step has its own time limit and the chain stops at the first
@@ -50,6 +50,7 @@ python3 profiles/db_summary.py pmc "$DB/c5fetch/run_results.db" "$DB/c5write/run
     "$OUT/pmc_c5.json" "rocprofv3 --pmc passes over bench.py --config c5 --steps 1 --warmup 0 (C5, 1M nodes), MI355X"
 fi
 python3 profiles/db_summary.py stats "$DB/c3/run_results.db" "$OUT/c3_kernel_stats.csv"
+python3 profiles/db_summary.py timeline "$DB/c3/run_results.db" "$OUT/c3_timeline.txt"
 [ -z "${SKIP_C4:-}" ] && python3 profiles/db_summary.py stats "$DB/c4/run_results.db" "$OUT/c4_kernel_stats.csv"
 python3 profiles/db_summary.py pmc "$DB/fetch/run_results.db" "$DB/write/run_results.db" "$DB/sq/run_results.db" \
     "$OUT/pmc_c3.json" "rocprofv3 --pmc passes over bench.py --steps 1 --warmup 1 --pods-per-step 8192 (C3 alone), MI355X"
