@@ -204,11 +204,9 @@ __device__ __forceinline__ void cand_list(const EngineArgs& a, WinWS& ws, int i,
 // bitmap flags, ks_scan.h).  Every launch clears the pods' bitmaps and thresholds for the next scan.
 constexpr int kMergeMaxWaves = 16;
 template <int kMode, int kLL>
-// (the engine arguments by value: the kernel-argument segment is one scalar round trip; a pointer to
-// the device copy was two before the first vector read)
-__global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs av, const uint64_t* src,
+__global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs* __restrict__ A, const uint64_t* src,
                                                          int64_t pod_stride, int32_t nl, int64_t list_stride) {
-    const EngineArgs& a = av;
+    const EngineArgs& a = A[0];
     WinWS& ws = *a.sw;
     const bool own = src == nullptr;
     if (own) {
@@ -393,16 +391,16 @@ hipError_t launch_window_prep(const EngineArgs* d, bool head, bool spec, int slo
     return hipGetLastError();
 }
 
-hipError_t launch_merge_cl(const EngineArgs& h, int mode, int B, const uint64_t* lists, int64_t pod_stride,
+hipError_t launch_merge_cl(const EngineArgs* d, int mode, int B, const uint64_t* lists, int64_t pod_stride,
                            int32_t nl, int64_t list_stride, int nl_max, hipStream_t st, int L) {
     static_assert(sq::kEPer * 256 >= kEMax, "E keys per thread at 256 threads");
     const dim3 g(B), t(nl_max > 1024 ? 1024 : 256);
 #define KS_MCL(LL)                                                                                                   \
     switch (mode) {                                                                                                  \
-        case kEvalMicro: hipLaunchKernelGGL((sq::merge_cl_kernel<kEvalMicro, LL>), g, t, 0, st, h, lists, pod_stride, nl, list_stride); break; \
-        case kEvalTiny: hipLaunchKernelGGL((sq::merge_cl_kernel<kEvalTiny, LL>), g, t, 0, st, h, lists, pod_stride, nl, list_stride); break;   \
-        case kEvalNarrow: hipLaunchKernelGGL((sq::merge_cl_kernel<kEvalNarrow, LL>), g, t, 0, st, h, lists, pod_stride, nl, list_stride); break; \
-        default: hipLaunchKernelGGL((sq::merge_cl_kernel<kEvalWide, LL>), g, t, 0, st, h, lists, pod_stride, nl, list_stride); break;          \
+        case kEvalMicro: hipLaunchKernelGGL((sq::merge_cl_kernel<kEvalMicro, LL>), g, t, 0, st, d, lists, pod_stride, nl, list_stride); break; \
+        case kEvalTiny: hipLaunchKernelGGL((sq::merge_cl_kernel<kEvalTiny, LL>), g, t, 0, st, d, lists, pod_stride, nl, list_stride); break;   \
+        case kEvalNarrow: hipLaunchKernelGGL((sq::merge_cl_kernel<kEvalNarrow, LL>), g, t, 0, st, d, lists, pod_stride, nl, list_stride); break; \
+        default: hipLaunchKernelGGL((sq::merge_cl_kernel<kEvalWide, LL>), g, t, 0, st, d, lists, pod_stride, nl, list_stride); break;          \
     }
     if (L == kTopL) { KS_MCL(kTopL) }
     else if (L == kTopLOverlap) { KS_MCL(kTopLOverlap) }

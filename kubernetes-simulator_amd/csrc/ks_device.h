@@ -805,8 +805,7 @@ hipError_t launch_window_prep(const EngineArgs* d, bool head, bool spec, int slo
 // merge + candidate lists (ks_cand.hip): per pod the merge kernel's exact top-L over its lists, then
 // its static candidates and their slots
 // L: the lists' length (the engine's block lists, or kTopL for the sharded second merge)
-// (h: the engine arguments' host copy, passed by value)
-hipError_t launch_merge_cl(const EngineArgs& h, int mode, int B, const uint64_t* lists, int64_t pod_stride,
+hipError_t launch_merge_cl(const EngineArgs* d, int mode, int B, const uint64_t* lists, int64_t pod_stride,
                            int32_t nl, int64_t list_stride, int nl_max, hipStream_t st, int L = kTopL);
 struct BindSeg {
     const int32_t* node;

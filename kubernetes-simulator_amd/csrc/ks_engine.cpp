@@ -1270,7 +1270,7 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
             hipEvent_t evx[2] = {ev[5], ev[6]};  // part merges | exchange | merge (sharded engines)
             const int64_t L = ks::kTopL, BL = (int64_t)e->B * L;
             if (G == 1) {
-                HIPCHK(e, fused ? ks::launch_merge_cl(*e->h_args, e->mode, e->B, nullptr, 0, 0, 0, e->nblk, st, e->L)
+                HIPCHK(e, fused ? ks::launch_merge_cl(d, e->mode, e->B, nullptr, 0, 0, 0, e->nblk, st, e->L)
                                 : ks::launch_merge(d, 1, e->B, nullptr, 0, 0, 0, nullptr, e->nblk, st));
             } else {
                 for (int v = 0; v < e->vsh; v++) {
@@ -1296,7 +1296,7 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
                                              hipMemcpyHostToDevice, st));
                 }
                 if (evx[1]) HIPCHK(e, hipEventRecord(evx[1], st));
-                HIPCHK(e, fused ? ks::launch_merge_cl(*e->h_args, e->mode, e->B, e->cand_all, L, G, BL, G, st)
+                HIPCHK(e, fused ? ks::launch_merge_cl(d, e->mode, e->B, e->cand_all, L, G, BL, G, st)
                                 : ks::launch_merge(d, 1, e->B, e->cand_all, L, G, BL, e->cand, G, st));
             }
             if (ev[3]) HIPCHK(e, hipEventRecord(ev[3], st));
