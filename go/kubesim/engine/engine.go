@@ -70,6 +70,13 @@ const (
 	FilterSelector = uint32(C.KS_FILTER_SELECTOR)
 )
 
+// Engine flags of ks_config (include/ks_engine.h): A/B and test switches; the defaults are the
+// engine's choice.
+const (
+	FlagNoOverlap   = uint32(C.KS_ENGINE_NO_OVERLAP)   // the plain batch chain (no fused next-batch scan)
+	FlagPrunedLists = uint32(C.KS_ENGINE_PRUNED_LISTS) // pruned block lists at any cluster size
+)
+
 // ScorerSpec is one registered device scorer (registration order is kept).
 type ScorerSpec struct {
 	Kind, Weight, Value int32
@@ -84,6 +91,7 @@ type Config struct {
 	Scorers     []ScorerSpec
 	Device      int
 	BatchPods   int
+	EngineFlags uint32 // Flag* above (0: the engine's defaults)
 }
 
 func (c Config) toC() (C.ks_config, error) {
@@ -105,6 +113,7 @@ func (c Config) toC() (C.ks_config, error) {
 	}
 	cfg.device = C.int32_t(c.Device)
 	cfg.batch_pods = C.int32_t(c.BatchPods)
+	cfg.engine_flags = C.uint32_t(c.EngineFlags)
 	return cfg, nil
 }
 
@@ -248,6 +257,13 @@ func (e *Engine) Queued() int64 {
 func (e *Engine) Tick() int64 {
 	defer runtime.KeepAlive(e)
 	return int64(C.ks_current_tick(e.h))
+}
+
+// TickSeconds is the simulated seconds per tick (ks_tick_seconds): the submitters' clock is
+// start + Tick() * TickSeconds().
+func (e *Engine) TickSeconds() int64 {
+	defer runtime.KeepAlive(e)
+	return int64(C.ks_tick_seconds(e.h))
 }
 
 // Step advances `ticks` ticks of Run's loop (at most one bind per tick).  Binds made before an
