@@ -360,12 +360,25 @@ __host__ __device__ __forceinline__ uint32_t umad24(uint32_t a, uint32_t b, uint
     return (uint32_t)((uint64_t)a * b) + c;
 #endif
 }
-// |a - b| (v_sad_u32)
+// |a - b| in one v_sad_u32 (__usad compiles to max / min / sub: three instructions)
 __host__ __device__ __forceinline__ uint32_t usad(uint32_t a, uint32_t b) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    return __usad(a, b, 0u);
+    uint32_t r;
+    asm("v_sad_u32 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b));
+    return r;
 #else
     return a > b ? a - b : b - a;
+#endif
+}
+// max(trunc(x), 0) for |x| < 2^31 in one v_cvt_u32_f32 (it saturates negatives to 0); a C cast
+// of a negative float to unsigned is undefined, hence the instruction
+__host__ __device__ __forceinline__ uint32_t f2u_sat(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    asm("v_cvt_u32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+#else
+    return x < 1.f ? 0u : (uint32_t)x;
 #endif
 }
 // largest weight the micro evaluator multiplies with a 24-bit multiply (the host's mode choice)
@@ -414,8 +427,8 @@ __host__ __device__ __forceinline__ uint32_t eval_total1_micro(const Cfg& c, con
     const float iac = micro_ic(n, acs), iam = micro_im(n, ams);  // node-invariant: hoisted
     const float rc10 = 10.f * iac, rm10 = 10.f * iam;
     const float fcf = (float)fc, fmf = (float)fm;  // exact: |f| < 2^24
-    const int32_t lc0 = (int32_t)fmaf(fcf, rc10, kMicroBias), lm0 = (int32_t)fmaf(fmf, rm10, kMicroBias);
-    const uint32_t lrs = (uint32_t)((lc0 > 0 ? lc0 : 0) + (lm0 > 0 ? lm0 : 0)) >> 1;
+    // LeastRequested: max(trunc(fma), 0) per key in one saturating conversion
+    const uint32_t lrs = (f2u_sat(fmaf(fcf, rc10, kMicroBias)) + f2u_sat(fmaf(fmf, rm10, kMicroBias))) >> 1;
     const bool ba_on = (fc < fm ? fc : fm) > 0;
     const uint32_t D = (uint32_t)micro_d(n, acs, ams);
     // X = |uc Am - um Ac| = |fm Ac - fc Am| (u = A - f)
@@ -423,11 +436,11 @@ __host__ __device__ __forceinline__ uint32_t eval_total1_micro(const Cfg& c, con
     const uint32_t X = usad(a, b);
     const uint32_t N = umad24(D - X, 10u, 0u);
     // estimate of 10 (D - X) / D = 10 - 10 |fm/Am - fc/Ac| (within 1e-5; the step below is exact)
-    int32_t q = (int32_t)(10.f - fabsf(fmaf(fmf, rm10, -fcf * rc10)));
-    q = q < 0 ? 0 : (q > 10 ? 10 : q);
-    const uint32_t t = umad24((uint32_t)q, D, 0u);
-    q += (N >= t + D) ? 1 : 0;
-    q -= (N < t) ? 1 : 0;
+    uint32_t q = f2u_sat(10.f - fabsf(fmaf(fmf, rm10, -fcf * rc10)));  // clamp below: the conversion
+    q = q > 10u ? 10u : q;
+    const uint32_t t = umad24(q, D, 0u);
+    q += (N >= t + D) ? 1u : 0u;
+    q -= (N < t) ? 1u : 0u;
     const uint32_t base = umad24((uint32_t)c.w_lr, lrs, (uint32_t)c.const_total + 1u);
     const uint32_t total1 = umad24((uint32_t)c.w_ba, ba_on ? (uint32_t)q : 0u, base);
     return ok ? total1 : 0u;
@@ -498,18 +511,18 @@ __host__ __device__ __forceinline__ uint32_t eval_scan_micro(const Cfg& c, const
     const float iac = micro_ic(n, acs), iam = micro_im(n, ams);  // node-invariant: hoisted
     const float rc10 = 10.f * iac, rm10 = 10.f * iam;
     const float fcf = (float)fc, fmf = (float)fm;  // exact: |f| < 2^24
-    const int32_t lc0 = (int32_t)fmaf(fcf, rc10, kMicroBias), lm0 = (int32_t)fmaf(fmf, rm10, kMicroBias);
-    const uint32_t lrs = (uint32_t)((lc0 > 0 ? lc0 : 0) + (lm0 > 0 ? lm0 : 0)) >> 1;
+    // LeastRequested: max(trunc(fma), 0) per key in one saturating conversion
+    const uint32_t lrs = (f2u_sat(fmaf(fcf, rc10, kMicroBias)) + f2u_sat(fmaf(fmf, rm10, kMicroBias))) >> 1;
     const bool ba_on = (fc < fm ? fc : fm) > 0;
     const uint32_t D = (uint32_t)micro_d(n, acs, ams);
     const uint32_t a = umad24((uint32_t)fm, (uint32_t)acs, 0u), b = umad24((uint32_t)fc, (uint32_t)ams, 0u);
     const uint32_t X = usad(a, b);
     const uint32_t N = umad24(D - X, 10u, 0u);
-    int32_t q = (int32_t)(10.f - fabsf(fmaf(fmf, rm10, -fcf * rc10)));
-    q = q < 0 ? 0 : (q > 10 ? 10 : q);
-    const uint32_t t = umad24((uint32_t)q, D, 0u);
-    q += (N >= t + D) ? 1 : 0;
-    q -= (N < t) ? 1 : 0;
+    uint32_t q = f2u_sat(10.f - fabsf(fmaf(fmf, rm10, -fcf * rc10)));  // clamp below: the conversion
+    q = q > 10u ? 10u : q;
+    const uint32_t t = umad24(q, D, 0u);
+    q += (N >= t + D) ? 1u : 0u;
+    q -= (N < t) ? 1u : 0u;
     const uint32_t base = umad24((uint32_t)c.w_lr, lrs, (uint32_t)c.const_total + 1u);
     const uint32_t total1 = umad24((uint32_t)c.w_ba, ba_on ? (uint32_t)q : 0u, base);
     return bad == 0 ? total1 : 0u;
