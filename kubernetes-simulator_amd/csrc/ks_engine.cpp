@@ -1185,7 +1185,10 @@ static ks_status ensure_window_ws(ks_engine* e) {
         // footprint allows one workgroup per CU)
         int cus = 0;
         HIPCHK(e, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device));
-        e->scan_workers = std::max(15, cus - 1);  // (>= 15: every XCD deals its share to at least one)
+#ifndef KS_SCAN_WORKERS_DIV
+#define KS_SCAN_WORKERS_DIV 1  // (A/B builds: make variant DEFS=-DKS_SCAN_WORKERS_DIV=2)
+#endif
+        e->scan_workers = std::max(15, cus / KS_SCAN_WORKERS_DIV - 1);  // (>= 15: every XCD deals its share to at least one)
     }
     return KS_OK;
 }
