@@ -294,12 +294,22 @@ ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, i
  * [4] batches that committed early (top-L list exhausted), [16..31] resolver phase cycle
  * sums in a -DKS_STAMPS diagnostic build (tests/dev/diag_resolve.py). */
 ks_status ks_debug_counters(ks_engine* eng, int64_t* out32);
+/* Between-step invariants of a chunk-resolver engine (diagnostics / regression tests): out4[0] =
+ * nodes whose candidate-slot mark is set (must be 0: every batch's commit resets the marks of every
+ * node its merge claimed), out4[1] = nodes whose E-index mark is set (must be 0), out4[2] = the most
+ * candidate slots any batch claimed so far, out4[3] = the slots whose records are staged (beyond
+ * them a batch is cut before the first pod that needs one).  All 0 before the first batch. */
+ks_status ks_debug_invariants(ks_engine* eng, int64_t* out4);
 /* Device self-test of an evaluator identity the exactness argument rests on (no engine needed).
  * test 0: the micro evaluator's correction-free LeastRequested floor for every (x, A) with
  * 0 <= x <= A < 2^16 (ks_device.h).  *failures = mismatching cases (0 = pass). */
 enum { KS_SELFTEST_LR_MICRO = 0 };
 ks_status ks_selftest(int32_t device, int32_t test, int64_t* failures);
 void ks_set_profiling(ks_engine* eng, int enable);
+/* Provenance: the first 16 hex digits of the SHA-256 of the sources the library was built from
+ * (kubernetes-simulator_amd/csrc/Makefile HASHED, in that order); the Python binding refuses a
+ * library whose id differs from the hash of the sources beside it. */
+const char* ks_build_id(void);
 
 #ifdef __cplusplus
 }

@@ -76,6 +76,8 @@ ks_status ks_local_allgather(void* user /* ks_local_exchange* */, int32_t rank, 
 /* A rank whose step failed before it reached the exchange would leave the others waiting: its
  * driver calls this, and every current and later ks_local_allgather on x returns KS_EDEVICE. */
 void ks_local_exchange_abort(ks_local_exchange* x);
+/* Provenance of libks_kubesim.so: the same source hash as ks_build_id (ks_engine.h). */
+const char* ks_run_build_id(void);
 
 #ifdef __cplusplus
 }

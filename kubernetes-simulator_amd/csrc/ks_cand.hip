@@ -74,9 +74,8 @@ using prep::pstamp;
 #endif
 constexpr int kRecWords = 12;
 static_assert(kRecWords <= kRecDw, "record size");
-constexpr int kSlotsAll = kWinMaxB * kChR;  // claims a batch can make (slot_node holds every one)
 constexpr int kSlotPending = -2;
-static_assert(kSlotsAll <= 65535, "slot ids in 16 bits");
+static_assert(kSlotIds <= 65535, "slot ids in 16 bits");
 
 __device__ __forceinline__ void put_rec(uint32_t* o, const NodeV& v) {
     o[0] = (uint32_t)v.ac; o[1] = (uint32_t)v.am; o[2] = (uint32_t)v.ag;
@@ -203,10 +202,21 @@ __device__ __forceinline__ void cand_list(const EngineArgs& a, WinWS& ws, int i,
 // launch fewer per batch.  src == nullptr: the engine's own block lists (pruned: only the blocks its
 // bitmap flags, ks_scan.h).  Every launch clears the pods' bitmaps and thresholds for the next scan.
 constexpr int kMergeMaxWaves = 16;
+}  // namespace sq
+#ifdef KS_MCL_BYVAL
+thread_local const EngineArgs* ks_mcl_host_args = nullptr;  // (diagnostic build: set by step_body before each launch)
+#endif
+namespace sq {
 template <int kMode, int kLL>
+#ifdef KS_MCL_BYVAL  // (diagnostic build only: the engine arguments by value, VERDICT r5 item 1's A/B)
+__global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs av, const uint64_t* src,
+                                                         int64_t pod_stride, int32_t nl, int64_t list_stride) {
+    const EngineArgs& a = av;
+#else
 __global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs* __restrict__ A, const uint64_t* src,
                                                          int64_t pod_stride, int32_t nl, int64_t list_stride) {
     const EngineArgs& a = A[0];
+#endif
     WinWS& ws = *a.sw;
     const bool own = src == nullptr;
     if (own) {
@@ -395,6 +405,11 @@ hipError_t launch_merge_cl(const EngineArgs* d, int mode, int B, const uint64_t*
                            int32_t nl, int64_t list_stride, int nl_max, hipStream_t st, int L) {
     static_assert(sq::kEPer * 256 >= kEMax, "E keys per thread at 256 threads");
     const dim3 g(B), t(nl_max > 1024 ? 1024 : 256);
+#ifdef KS_MCL_BYVAL
+    if (!ks_mcl_host_args) return hipErrorInvalidValue;
+    const EngineArgs hv = *ks_mcl_host_args;  // (diagnostic: the host copy, as commit 63524d5 passed it)
+#define d hv
+#endif
 #define KS_MCL(LL)                                                                                                   \
     switch (mode) {                                                                                                  \
         case kEvalMicro: hipLaunchKernelGGL((sq::merge_cl_kernel<kEvalMicro, LL>), g, t, 0, st, d, lists, pod_stride, nl, list_stride); break; \
@@ -406,6 +421,9 @@ hipError_t launch_merge_cl(const EngineArgs* d, int mode, int B, const uint64_t*
     else if (L == kTopLOverlap) { KS_MCL(kTopLOverlap) }
     else return hipErrorInvalidValue;
 #undef KS_MCL
+#ifdef KS_MCL_BYVAL
+#undef d
+#endif
     return hipGetLastError();
 }
 

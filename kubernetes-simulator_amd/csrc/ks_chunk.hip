@@ -1116,7 +1116,10 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
             if (sh.fhead[k] >= 0) wo.touched[atomicAdd(&sh.nbc, 1)] = sh.cnode[k];
         if (tid < n_e) wo.touched[atomicAdd(&sh.nbc, 1)] = enode[0];  // (every slot-E node has slots)
         __syncthreads();
-        if (tid == 0) wo.n_touched = sh.nbc;
+        if (tid == 0) {
+            wo.n_touched = sh.nbc;
+            if (ws.nslot > wo.nslot_hw) wo.nslot_hw = ws.nslot;  // (diagnostics: ks_debug_invariants)
+        }
     }
     if (tid == 0) {
         a.ctr[kCtrStart] = start + c;

@@ -678,7 +678,10 @@ constexpr int kWinSlots = 512;
 #endif
 constexpr int kChR = KS_CHR;  // static candidates kept per pod
 constexpr int kRecDw = 20;  // a candidate node's record, dwords (the widest format: ten int64, ks_cand.hip)
-constexpr int kSlotMax = 1536;  // distinct candidate nodes per batch (the sequential resolver's slots)
+constexpr int kSlotMax = 1536;  // candidate slots whose record / E index merge_cl stages
+// claims a batch can make: every kept entry of every pod (slot_node holds each one, so the commit
+// can reset node_slot for every claimed node — the slots past kSlotMax included)
+constexpr int kSlotIds = kWinMaxB * kChR;
 constexpr int kEMax = 2048;     // E nodes per batch: the window's expiry nodes + the overlap's touched nodes
 constexpr int kTouchMax = kWinMaxB + kWinSlots;
 constexpr int kSpecStride = 8;  // int64 counters per speculative set  // nodes a batch changes: its binds + its window's expiry nodes
@@ -708,7 +711,16 @@ struct WinWS {
     // read node_slot; -3: no slot left)
     int32_t cl_slot[kWinMaxB][kChR];
     int32_t nslot;                        // slots handed out (may exceed kSlotMax: overflow)
+    int32_t nslot_hw;                     // the largest nslot any batch reached (ks_debug_invariants)
+    // slot -> node for every claim.  (Until round 6 this array had kSlotMax entries: a batch with more
+    // than kSlotMax distinct candidates wrote slot_node[kSlotMax + s] over slot_eix[s] — racing the
+    // claimer of slot s, so a candidate's E index could come out as a node id — and the commit's
+    // reset missed the claims past kSlotMax.)
+#ifdef KS_SLOT_IDS_LEGACY  // (diagnostic build only: the round-3..5 layout, for the regression test's A/B)
     int32_t slot_node[kSlotMax];
+#else
+    int32_t slot_node[kSlotIds];
+#endif
     int32_t slot_eix[kSlotMax];           // the node's index in E, -1 if not an E node
     uint32_t slot_rec[kSlotMax][kRecDw];  // the node's record at the batch start (narrow: 12 dwords)
     // overlap (scan of batch k+1 beside the resolve of batch k): the nodes batch k changed (its
@@ -818,6 +830,9 @@ hipError_t launch_window_prep(const EngineArgs* d, bool head, bool spec, int slo
 // merge + candidate lists (ks_cand.hip): per pod the merge kernel's exact top-L over its lists, then
 // its static candidates and their slots
 // L: the lists' length (the engine's block lists, or kTopL for the sharded second merge)
+#ifdef KS_MCL_BYVAL
+extern thread_local const EngineArgs* ks_mcl_host_args;
+#endif
 hipError_t launch_merge_cl(const EngineArgs* d, int mode, int B, const uint64_t* lists, int64_t pod_stride,
                            int32_t nl, int64_t list_stride, int nl_max, hipStream_t st, int L = kTopL);
 struct BindSeg {

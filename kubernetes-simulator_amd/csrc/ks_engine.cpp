@@ -1173,6 +1173,7 @@ static ks_status ensure_window_ws(ks_engine* e) {
     }
     if (e->d_sweep || r != kResolveChunk) return KS_OK;
     HIPCHK(e, hipMalloc(&e->d_sweep, sizeof(ks::WinWS)));
+    HIPCHK(e, hipMemsetAsync(e->d_sweep, 0, sizeof(ks::WinWS), e->st));
     HIPCHK(e, hipMalloc(&e->d_eidx, sizeof(int32_t) * e->n_pad));
     HIPCHK(e, hipMemsetAsync(e->d_eidx, 0xFF, sizeof(int32_t) * e->n_pad, e->st));
     HIPCHK(e, hipMalloc(&e->d_nslot, sizeof(int32_t) * e->n_pad));
@@ -1238,6 +1239,9 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
     }
     HIPCHK(e, hipEventRecord(e->ev[0], st));
     const ks::EngineArgs* d = e->d_args;
+#ifdef KS_MCL_BYVAL
+    ks::ks_mcl_host_args = e->h_args;  // (diagnostic build only; one engine per thread at a time is not guaranteed)
+#endif
     int64_t start = e->done;
     int64_t launches = 0;
     double scan_ms = 0, res_ms = 0;
@@ -1905,6 +1909,31 @@ ks_status ks_debug_counters(ks_engine* e, int64_t* out32) {
     HIPCHK(e, hipSetDevice(e->device));
     HIPCHK(e, hipMemcpyAsync(out32, e->d_ctr, 32 * sizeof(int64_t), hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
+    return KS_OK;
+}
+
+#ifndef KS_SRC_HASH
+#define KS_SRC_HASH "unhashed"
+#endif
+const char* ks_build_id(void) { return KS_SRC_HASH; }
+
+ks_status ks_debug_invariants(ks_engine* e, int64_t* out4) {
+    if (!e || !out4) return KS_EINVAL;
+    out4[0] = out4[1] = out4[2] = out4[3] = 0;
+    if (!e->d_sweep) return KS_OK;  // (no chunk-resolver batch ran: nothing to check)
+    HIPCHK(e, hipSetDevice(e->device));
+    std::vector<int32_t> ns(e->n_pad), ei(e->n_pad);
+    int32_t hw = 0;
+    HIPCHK(e, hipMemcpyAsync(ns.data(), e->d_nslot, sizeof(int32_t) * e->n_pad, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(ei.data(), e->d_eidx, sizeof(int32_t) * e->n_pad, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(&hw, &e->d_sweep->nslot_hw, sizeof hw, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    for (int64_t i = 0; i < e->n_pad; i++) {
+        out4[0] += ns[i] != -1;
+        out4[1] += ei[i] != -1;
+    }
+    out4[2] = hw;
+    out4[3] = ks::kSlotMax;
     return KS_OK;
 }
 

@@ -117,17 +117,20 @@ __global__ __launch_bounds__(256) void expire_head_kernel(const EngineArgs* __re
 // ------------------------------------------------------------------------------------------
 // KT: the key table's word, uint16_t when every total + 1 < 2^16 (the host's check on the scorer
 // weights) — half the LDS per workgroup, so more workgroups fit a CU.
+constexpr int kStageWgs = 8;  // workgroups staging the E records (grid-stride over n_e <= kEMax)
 template <int kMode, typename KT, bool kPrune, int kLL>
 __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict__ A, int xcd, int cond, int stage) {
     extern __shared__ uint32_t kv_raw[];
     KT* const kv = reinterpret_cast<KT*>(kv_raw);  // [PG][kBlockNodes]: total+1 per (pod, node of the block)
     const EngineArgs& a = A[blockIdx.z];
-    // stage: the chunk class — the first kEMax / 256 workgroups also stage the batch's E records
-    // for merge_cl (WinWS::e_rec; one node per thread), before their own work
-    if (stage && blockIdx.x < kEMax / kBlockNodes) {
+    // stage: the chunk class — the first kStageWgs workgroups also stage the batch's E records for
+    // merge_cl (WinWS::e_rec; one node per thread, grid-stride), before their own work.  launch_scan
+    // launches at least kStageWgs workgroups when staging, also for a rank with no scan blocks.
+    if (stage && blockIdx.x < kStageWgs) {
         const WinWS& ws = *a.sw;
-        const int k = (int)blockIdx.x * kBlockNodes + (int)threadIdx.x;
-        if (k < ws.n_e) put_rec12(a.sw->e_rec[k], load_node(a.s, ws.e_node[k]));
+        const int n_e = ws.n_e;
+        for (int k = (int)blockIdx.x * kBlockNodes + (int)threadIdx.x; k < n_e; k += kStageWgs * kBlockNodes)
+            put_rec12(a.sw->e_rec[k], load_node(a.s, ws.e_node[k]));
     }
     // cond: the overlap's fallback scan, needed only when window prep flagged a rescan
     if (cond && *(volatile const int32_t*)&a.sw->rescan == 0) return;
@@ -1132,12 +1135,14 @@ static void launch_scan_t(const EngineArgs* d, const dim3& g, size_t lds, int mo
 
 hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int mode, bool key16, hipStream_t st,
                        bool cond, bool prune, int L, bool stage) {
-    if (blk_n > 0 && S > 0) {
+    // (a staging launch runs even when this rank scans no blocks: merge_cl reads the E records)
+    if ((blk_n > 0 || (stage && S == 1)) && S > 0) {
         // one (block, pod group) item per workgroup; one engine: the XCD-aware 1-D deal
         const int groups = (B + PG - 1) / PG;
         const size_t lds = (key16 ? sizeof(uint16_t) : sizeof(uint32_t)) * kBlockNodes * PG;
         const bool xcd = S == 1;
-        const dim3 g = xcd ? dim3((unsigned)(((int64_t)blk_n * groups + 7) / 8 * 8), 1, 1) : dim3(blk_n, groups, S);
+        const int64_t wgs = std::max<int64_t>(((int64_t)blk_n * groups + 7) / 8 * 8, stage ? kStageWgs : 0);
+        const dim3 g = xcd ? dim3((unsigned)wgs, 1, 1) : dim3(blk_n, groups, S);
         const int x = xcd ? 1 : 0, c = cond ? 1 : 0, sg = stage && xcd ? 1 : 0;
         if (L != kTopL) {  // the overlap's single-shard lists: 16-bit keys, not pruned (ks_engine.cpp)
             if (!key16 || prune || L != kTopLOverlap) return hipErrorInvalidValue;

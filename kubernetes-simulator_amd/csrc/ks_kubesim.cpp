@@ -142,4 +142,9 @@ ks_status ks_local_allgather(void* user, int32_t rank, int32_t world, void* buf,
     return KS_OK;
 }
 
+#ifndef KS_SRC_HASH
+#define KS_SRC_HASH "unhashed"
+#endif
+const char* ks_run_build_id(void) { return KS_SRC_HASH; }
+
 }  // extern "C"

@@ -34,7 +34,7 @@ STATUS_NAMES = {KS_OK: "OK", KS_EINVAL: "InvalidArgument", KS_ENOTFOUND: "NotFou
 # every symbol include/*.h declares
 EXPORTED_SYMBOLS = ("ks_create", "ks_destroy", "ks_load_nodes", "ks_submit_pods", "ks_step",
                     "ks_filter", "ks_score", "ks_usage", "ks_current_tick", "ks_tick_seconds", "ks_queued_pods",
-                    "ks_last_error", "ks_last_step_stats", "ks_last_step_kernels", "ks_set_profiling", "ks_debug_counters", "ks_selftest",
+                    "ks_last_error", "ks_last_step_stats", "ks_last_step_kernels", "ks_set_profiling", "ks_debug_counters", "ks_debug_invariants", "ks_build_id", "ks_selftest",
                     "ks_comm_unique_id", "ks_shard", "ks_shard_host", "ks_group_create", "ks_group_destroy",
                     "ks_group_add", "ks_group_size", "ks_group_step", "ks_pod_status",
                     "ks_usage_at", "ks_usage_digest", "ks_node_mix", "ks_pod_lookup", "ks_node_pods",
@@ -46,7 +46,7 @@ EXPORTED_SYMBOLS = ("ks_create", "ks_destroy", "ks_load_nodes", "ks_submit_pods"
 KS_COMM_ID_BYTES = 128
 # include/ks_kubesim.h (libks_kubesim.so)
 RUN_SYMBOLS = ("ks_run", "ks_trace_submit", "ks_local_exchange_create", "ks_local_exchange_destroy",
-               "ks_local_allgather", "ks_local_exchange_abort")
+               "ks_local_allgather", "ks_local_exchange_abort", "ks_run_build_id")
 
 
 class KsScorer(C.Structure):
@@ -96,6 +96,33 @@ class KsTraceSubmitter(C.Structure):
 
 _lib = None
 _run_lib = None
+CSRC = os.path.join(os.path.dirname(HERE), "csrc")
+
+
+def source_hash():
+    """The provenance hash the Makefile embeds (ks_build_id): SHA-256 of the files its HASHED list
+    names, in that order, first 16 hex digits; None when the sources are not beside the package."""
+    import hashlib
+    mk = os.path.join(CSRC, "Makefile")
+    if not os.path.exists(mk):
+        return None
+    with open(mk) as f:
+        line = next((x for x in f if x.startswith("HASHED =")), None)
+    if line is None:
+        return None
+    h = hashlib.sha256()
+    for name in line.split("=", 1)[1].split():
+        with open(os.path.join(CSRC, name), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def _check_build(path, got):
+    want = source_hash()
+    got = got.decode() if got else ""
+    if want is not None and got != want:
+        raise ImportError(f"{path} was built from other sources (build id {got!r}, sources {want!r}): "
+                          "run __graft_entry__.build()")
 
 
 def load_run():
@@ -107,6 +134,8 @@ def load_run():
     if not os.path.exists(RUN_LIB_PATH):
         raise ImportError(f"{RUN_LIB_PATH} is missing: run __graft_entry__.build()")
     L = C.CDLL(RUN_LIB_PATH)
+    L.ks_run_build_id.restype = C.c_char_p
+    _check_build(RUN_LIB_PATH, L.ks_run_build_id())
     p = C.c_void_p
     L.ks_run.argtypes = [p, C.c_int64, C.c_int64, C.c_int32, p, p, p, C.c_int64, C.POINTER(C.c_int64),
                          C.POINTER(C.c_double)]
@@ -133,6 +162,8 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc, gfx950)")
     L = C.CDLL(LIB_PATH)
+    L.ks_build_id.restype = C.c_char_p
+    _check_build(LIB_PATH, L.ks_build_id())
     p = C.c_void_p
     L.ks_create.argtypes = [C.POINTER(KsConfig), C.POINTER(C.c_void_p)]
     L.ks_create.restype = C.c_int
@@ -171,6 +202,8 @@ def load():
     L.ks_last_step_kernels.restype = C.c_int
     L.ks_debug_counters.argtypes = [p, p]
     L.ks_debug_counters.restype = C.c_int
+    L.ks_debug_invariants.argtypes = [p, p]
+    L.ks_debug_invariants.restype = C.c_int
     L.ks_set_profiling.argtypes = [p, C.c_int]
     L.ks_set_profiling.restype = None
     L.ks_selftest.argtypes = [C.c_int32, C.c_int32, p]

@@ -244,6 +244,14 @@ class Engine:
         self._check(self._L.ks_debug_counters(self.h, _p(out)))
         return out
 
+    def debug_invariants(self):
+        """Between-step invariants (include/ks_engine.h ks_debug_invariants): slot marks left set,
+        E-index marks left set (both must be 0), the most candidate slots a batch claimed, the staged
+        slots."""
+        out = np.zeros(4, np.int64)
+        self._check(self._L.ks_debug_invariants(self.h, _p(out)))
+        return dict(slot_marks=int(out[0]), e_marks=int(out[1]), nslot_hw=int(out[2]), slot_max=int(out[3]))
+
     def set_profiling(self, on: bool):
         self._L.ks_set_profiling(self.h, 1 if on else 0)
 

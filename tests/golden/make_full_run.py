@@ -42,7 +42,12 @@ RUNS = {
     # the first 131,072 pods of the 1M-pod trace bench.py's c3q leg uses
     "c3q": (lambda: tracegen.slice_pods(tracegen.c3q_trace(n_nodes=50_000, n_pods=1_000_000), 0, 131_072),
             131_072, 16_384, 2),
+    # the reference-literal filter mode (kubesim/kubesim.go:182: the Filter result is discarded)
+    # on the whole C3 trace: bench.py's c3_literal leg
+    "c3lit": (lambda: tracegen.c3_trace(n_nodes=50_000, n_pods=1_000_000), 1_000_000, 32_768, 2),
 }
+# name -> (filter_mode, mode name in tests/harness.py MODES); default feeds mode
+FILTER = {"c3lit": (0, "literal_lrba_filters_ignored")}
 
 
 def digest(*arrays):
@@ -61,7 +66,8 @@ def run(name, threads):
     t0 = time.time()
     tr = make()
     assert tr["pods"]["m"] == pods
-    ora = COracle(tr, filter_mode=1, filters=7, scorers=SCORERS)
+    fm, mode = FILTER.get(name, (1, "feeds_all_lrba"))
+    ora = COracle(tr, filter_mode=fm, filters=7, scorers=SCORERS)
     ora.set_threads(threads)
     ora.submit(tr)
     wins, usage = [], []
@@ -75,7 +81,7 @@ def run(name, threads):
         if (w + 1) % every == 0 or w == nwin - 1:
             usage.append([int(ora.tick), digest(ora.usage().astype(np.int64))])
         print(f"{name}: window {w + 1}/{nwin} ({time.time() - t0:.0f} s)", flush=True)
-    return dict(pods=pods, window=window, nodes=tr["nodes"]["n"], mode="feeds_all_lrba",
+    return dict(pods=pods, window=window, nodes=tr["nodes"]["n"], mode=mode,
                 scorers=[list(s) for s in SCORERS], bind_digests=wins, usage_digests=usage,
                 oracle_seconds=round(time.time() - t0, 1), threads=threads)
 

@@ -82,3 +82,13 @@ def test_node_mix_matches_documented_formula():
     L = _lib.load()
     for nd in (0, 1, 2, 63, 50_000, (1 << 24) - 1):
         assert L.ks_node_mix(nd) == node_mix(nd)
+
+
+def test_library_built_from_these_sources():
+    """Provenance: both libraries carry the hash of the sources they were built
+    from (csrc/Makefile HASHED), and it is the hash of the sources in this tree — _lib.load()
+    refuses any other library, so a GPU record cannot come from a stale binary."""
+    want = _lib.source_hash()
+    assert want is not None and len(want) == 16
+    assert _lib.load().ks_build_id().decode() == want
+    assert _lib.load_run().ks_run_build_id().decode() == want

@@ -12,7 +12,7 @@ import pytest
 
 import full_run_digest
 from harness import assert_same_binds, encoded, make_engine, make_oracle, small_trace
-from kubesim_amd import _lib, tracegen
+from kubesim_amd import _lib, shard, tracegen
 from kubesim_amd.engine import LocalExchange
 
 pytestmark = pytest.mark.gpu
@@ -114,22 +114,68 @@ def test_c5_whole_trace_two_ranks_match_oracle_golden():
         done += k
 
 
-def test_c5_whole_trace_sixteen_ranks_overlapped_match_oracle_golden():
-    """BASELINE configs[4] as 16 ranks: 256 scan blocks per rank, so every rank runs the overlap
-    (its speculative scan fused into its chunk kernel; ks_engine.cpp kOverlapMaxBlocks) on pruned
-    lists (1M nodes), with the exchange every batch — every pod of the C5 leg against
-    tests/golden/full_run.json on every rank."""
+def _c5_golden_ranks(world, **kw):
+    """Every pod of the C5 leg on `world` thread-ranks (one part each) against the committed oracle
+    digests, window by window on every rank, with the between-step invariants of every rank's
+    engine (ks_debug_invariants: no candidate-slot or E-index mark left set).  Returns the largest
+    number of candidate slots a batch claimed on any rank."""
     g = full_run_digest.load("c5")
     if g is None:
         pytest.skip("no c5 golden")
     tr = tracegen.c5_trace(n_pods=g["pods"])
     enc = encoded(tr)
-    engs, _x = _ranks(tr, enc, 16, 1)
+    engs, _x = _ranks(tr, enc, world, 1, **kw)
     done = 0
+    hw = 0
     for w, want in enumerate(g["bind_digests"]):
         k = min(g["window"], g["pods"] - done)
         bs = _step_all(engs, k, _x)
         for r, b in enumerate(bs):
             assert len(b) == k and int(b["pod"][0]) == done
             assert full_run_digest.bind_digest(b) == want, f"rank {r}: window {w} differs"
+            inv = engs[r].debug_invariants()
+            assert inv["slot_marks"] == 0 and inv["e_marks"] == 0, (r, w, inv)
+            hw = max(hw, inv["nslot_hw"])
         done += k
+    return hw
+
+
+def test_c5_whole_trace_sixteen_ranks_overlapped_match_oracle_golden():
+    """BASELINE configs[4] as 16 ranks: 256 scan blocks per rank, so every rank runs the overlap
+    (its speculative scan fused into its chunk kernel; ks_engine.cpp kOverlapMaxBlocks) on pruned
+    lists (1M nodes), with the exchange every batch — every pod of the C5 leg against
+    tests/golden/full_run.json on every rank.  This is the configuration whose batches claim more
+    than kSlotMax candidate slots (the round-6 slot_node overflow, ks_device.h WinWS): the test
+    asserts that the overflow path runs."""
+    hw = _c5_golden_ranks(16)
+    assert hw > 1536, hw  # (ks_device.h kSlotMax: the overflow path ran)
+
+
+def test_c5_whole_trace_eight_ranks_deployment_layout_match_oracle_golden():
+    """BASELINE configs[4] in the 8-GPU deployment layout: 8 thread-ranks x 1 part, 512 scan blocks
+    per rank — above kOverlapMaxBlocks, so every rank runs the plain chain on pruned lists (1M
+    nodes) with the exchange every batch; every pod against tests/golden/full_run.json on every
+    rank."""
+    _c5_golden_ranks(8)
+
+
+def test_ranks_without_scan_blocks_match_oracle():
+    """A chunk-resolver cluster smaller than its shard layout: 600 nodes = 3 scan blocks
+    over 4 ranks, so one rank scans nothing and its scan launch only stages the batch's E records
+    for merge_cl (ks_kernels.hip scan_kernel).  Every rank bind-for-bind against the oracle."""
+    tr = small_trace(11, n_nodes=600, n_pods=1500, arrival="stream")
+    enc = encoded(tr)
+    engs, _x = _ranks(tr, enc, 4, 1, batch_pods=64, engine_flags=_lib.KS_ENGINE_CHUNK_RESOLVER)
+    assert 0 in np.diff(shard.engine_part_blocks(600, 4)), "a rank without scan blocks"
+    ora = make_oracle(tr, MODE)
+    ora.submit(tr)
+    for k in (1, 500, 999):
+        bs = _step_all(engs, k, _x)
+        ob, rc = ora.step(k, cap=k)
+        for b in bs:
+            assert_same_binds(b, ob)
+        assert rc == 0
+    for e in engs:
+        np.testing.assert_array_equal(e.usage(), ora.usage())
+        inv = e.debug_invariants()
+        assert inv["slot_marks"] == 0 and inv["e_marks"] == 0, inv
