@@ -264,6 +264,7 @@ def main():
     ap.add_argument("--no-c5", action="store_true", help="c3: skip the C5 node-sharded leg")
     ap.add_argument("--no-dropin", action="store_true", help="c3: skip the drop-in Run-loop leg")
     ap.add_argument("--no-c3q", action="store_true", help="c3: skip the decimal-SI memory (C3q) leg")
+    ap.add_argument("--no-c3-literal", action="store_true", help="c3: skip the reference-literal filter-mode leg")
     ap.add_argument("--no-c4", action="store_true", help="c3: skip the C4 what-if scenario leg")
     ap.add_argument("--c4-steps", type=int, default=2, help="c3: timed steps of the C4 leg")
     ap.add_argument("--c5-steps", type=int, default=4, help="c3: timed steps of the C5 leg")
@@ -354,12 +355,17 @@ def main():
     eng.close()
     dropin = dropin_leg(trace, enc, scorers, local) if rank == 0 and not args.no_dropin else None
     c3q = c3q_leg(args, scorers, local) if rank == 0 and not args.no_c3q else None
+    c3lit = c3_literal_leg(args, trace, enc, scorers, local) if rank == 0 and not args.no_c3_literal else None
     # C4 (BASELINE configs[3]) on every rank: disjoint scenario ranges, weak scaling
     c4 = None
     if not args.no_c4:
         try:
             c4 = c4_leg(args, rank, world, local, dist)
-        except Exception as ex:  # never fatal to the headline line
+        except Exception as ex:  # never fatal to the headline line on one rank
+            if world > 1:
+                # (a rank that skipped the leg's collectives would pair the C5 leg's
+                # collectives with the other ranks' C4 ones — fail the run cleanly instead)
+                raise
             log(f"[rank {rank}] C4 leg failed: {ex!r}")
             c4 = {"error": repr(ex)[:500]}
     line = None
@@ -407,6 +413,7 @@ def main():
                                     "24 B/node copy to the host; digest = every tick of the last step's window"},
             "dropin": dropin,
             "c3q": c3q,
+            "c3_literal": c3lit,
             "c4": c4,
             "c5_sharded": None,
             "cpu_baseline": cpu,
@@ -453,6 +460,35 @@ def c3q_leg(args, scorers, device, steps=3, warmup=1, S=32768):
             "pods_per_launch": st["pods"] / L, "scan_avg_ms": st["scan_ms"] / L,
             "resolve_avg_ms": st["resolve_ms"] / L, "other_avg_ms": st["other_ms"] / L,
             "workload": "C3q: C3 with decimal-SI memory requests on binary-SI capacities"}
+
+
+def c3_literal_leg(args, trace, enc, scorers, device, steps=3, warmup=1, S=32768):
+    """C3 in the reference's own filter mode: scheduleOneFilter's result is
+    discarded (kubesim/kubesim.go:182), so every node is scored and admission alone decides Ok vs
+    OverCapacity — the same trace and timing bracket as the headline, fewer steps.  The whole trace
+    in this mode is pinned by tests/golden/full_run.json "c3lit"."""
+    from kubesim_amd.engine import Engine
+    eng = Engine(tick_seconds=trace["tick_seconds"], filter_mode=0, filters=7, scorers=scorers, device=device)
+    eng.load_nodes(enc["alloc"], enc["taint"], enc["label"])
+    eng.submit(enc["pods"])
+    for _ in range(warmup):
+        eng.step(S)
+    t0 = time.perf_counter()
+    binds, over = 0, 0
+    for _ in range(steps):
+        b = eng.step(S)
+        binds += len(b)
+        over += int((b["status"] == 1).sum())
+    dt = time.perf_counter() - t0
+    eng.set_profiling(True)
+    eng.step(S)
+    st = eng.last_step_stats()
+    eng.close()
+    L = max(st["launches"], 1)
+    return {"evals_per_s": binds * args.nodes / dt, "pods_per_s": binds / dt, "steps": steps, "pods_per_step": S,
+            "over_capacity_binds": over, "pods_per_launch": st["pods"] / L, "scan_avg_ms": st["scan_ms"] / L,
+            "resolve_avg_ms": st["resolve_ms"] / L, "other_avg_ms": st["other_ms"] / L,
+            "workload": "C3, reference-literal filter mode (kubesim.go:182: Filter result discarded), LR+BA"}
 
 
 def dropin_leg(trace, enc, scorers, device, per_tick=4000, probe_ticks=400, windowed=65536, window=1024):

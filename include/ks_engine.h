@@ -300,6 +300,11 @@ ks_status ks_debug_counters(ks_engine* eng, int64_t* out32);
  * candidate slots any batch claimed so far, out4[3] = the slots whose records are staged (beyond
  * them a batch is cut before the first pod that needs one).  All 0 before the first batch. */
 ks_status ks_debug_invariants(ks_engine* eng, int64_t* out4);
+/* Diagnostics: the raw batch window workspace (ks_device.h WinWS; *size_out = its size, up to cap
+ * bytes copied to out), and — in a -DKS_BATCH_LOG diagnostic build only (KS_EINVAL otherwise) — the
+ * pod whose batch the chunk resolver records in it (tests/dev/byval_diag.py). */
+ks_status ks_debug_window(ks_engine* eng, void* out, int64_t cap, int64_t* size_out);
+ks_status ks_debug_watch(ks_engine* eng, int64_t pod);
 /* Device self-test of an evaluator identity the exactness argument rests on (no engine needed).
  * test 0: the micro evaluator's correction-free LeastRequested floor for every (x, A) with
  * 0 <= x <= A < 2^16 (ks_device.h).  *failures = mismatching cases (0 = pass). */

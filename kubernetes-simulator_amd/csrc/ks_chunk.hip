@@ -942,7 +942,19 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
                 }
                 DG(cs_x += dstamp() - c_b;)
                 const int gsh = lane & ~(G - 1);
+                // Both ballots with every lane active: each pod's rows are spread over all 16 lanes
+                // of the group (pod B's row j on lane (j + g) % 16, either half).  (Until round 6 the
+                // ballots sat in the two arms of `half ? ... : ...` — a divergent branch, so each
+                // ballot saw only its own half's lanes: a row whose state overflowed its segments on
+                // the other half's lane was dropped from D instead of stopping the batch, and the pod
+                // could bind a lower node — tests/test_resolvers_gpu.py segment-overflow test.)
+#ifdef KS_BALLOT_LEGACY  // (diagnostic build only: the pre-round-6 form, for the regression test's A/B)
                 const bool bad = half ? ((__ballot(badB) >> gsh) & 0xFFFFu) != 0 : ((__ballot(badA) >> gsh) & 0xFFFFu) != 0;
+#else
+                const uint64_t bmA = __ballot(badA), bmB = __ballot(badB);
+                const bool bad = (((half ? bmB : bmA) >> gsh) & 0xFFFFull) != 0;
+#endif
+                DG(int wa = 0; for (int o = 0; o < G; ++o) wa |= __shfl(dwhy, gsh + o);)  // (the group's stop reasons)
                 const uint64_t dk = half ? dkB : dkA;
                 const int dc = half ? dcB : dcA;
                 if (s8 == 0 && ih < c1) {
@@ -957,8 +969,6 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
                         if (bad || (fl & kFlOvf)) {
                             code = 1;
                             DG({
-                                int wa = 0;  // the group's reasons for this half's pod
-                                for (int o = 0; o < G; ++o) wa |= __shfl(dwhy, (lane & ~(G - 1)) + o);
                                 const int mine = half ? (wa >> 3) & 7 : wa & 7;
                                 sh.why[i] = !bad ? 1 : (mine & 4) ? 6 : (mine & 2) ? 5 : 0;
                             })
@@ -985,6 +995,17 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
                         nw = sh.w[par][i];
                         code = sh.code[par][i];
                     }
+#ifdef KS_BATCH_LOG
+                    if (start + i == a.sw->watch_pod && !a.sw->watch_done) {
+                        WinWS& wl = *a.sw;
+                        const int k = wl.w_nsw;
+                        if (k < 64) {
+                            wl.w_dec[k][0] = fresh; wl.w_dec[k][1] = lo; wl.w_dec[k][2] = bad; wl.w_dec[k][3] = code;
+                            wl.w_dec[k][4] = nw; wl.w_dec[k][5] = dc; wl.w_dec[k][6] = (int)(dk >> 32); wl.w_dec[k][7] = c0;
+                        }
+                        wl.w_nsw = k + 1;
+                    }
+#endif
                     sh.w[par ^ 1][i] = (int16_t)nw;
                     sh.code[par ^ 1][i] = (int8_t)code;
                     if (code != 0) atomicMin(&sh.fs[par], i);
@@ -1007,6 +1028,16 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
         }
         DG(uint64_t t2 = dstamp(); acc_sw += t2 - t1;)
 
+#ifdef KS_BATCH_LOG
+        {
+            WinWS& wl = *a.sw;
+            const int64_t wi = (int64_t)wl.watch_pod - start;
+            if (!wl.watch_done && wi >= c0 && wi < c1 && tid < kC) {
+                for (int q = 0; q < 8; ++q) wl.w_smeta[tid][q] = sh.smeta[c0 + tid][q];
+                wl.w_rowcid[tid] = sh.w[par][c0 + tid];
+            }
+        }
+#endif
         // (3) finalize the chunk's prefix [c0, cend): admissions known, final bind lists
         int cend = fsv < c1 ? fsv : c1;
         if (tid < kC) {
@@ -1062,6 +1093,27 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
 
     // ---- commit pods [0, c): outputs, expiry marks, node state write-back
     const int c = committed;
+#ifdef KS_BATCH_LOG  // (diagnostic builds only)
+    {
+        WinWS& wl = *a.sw;
+        if (tid == 0) {
+            const int k = wl.blog_n;
+            if (k < 16384) {
+                wl.blog[k][0] = (int32_t)(start & 0x7FFFFFFF); wl.blog[k][1] = c; wl.blog[k][2] = stop_code; wl.blog[k][3] = nb;
+            }
+            wl.blog_n = k + 1;
+        }
+        const int64_t wp = wl.watch_pod;
+        if (!wl.watch_done && wp >= start && wp < start + c) {
+            for (int q = tid; q < nb * kR; q += kThreads) wl.w_cl_key[q / kR][q % kR] = ws.cl_key[q / kR][q % kR];
+            if (tid < nb) { wl.w_cl_info[tid] = ws.cl_info[tid]; wl.w_cl_thr[tid] = ws.cl_thr[tid]; }
+            for (int q = tid; q < n_eall; q += kThreads) wl.w_e_node[q] = ws.e_node[q];
+            if (tid < c) { wl.w_bind[tid] = sh.cnode[sh.wf[tid]]; wl.w_adm[tid] = sh.adm[tid]; }
+            __syncthreads();
+            if (tid == 0) { wl.w_start = (int32_t)start; wl.w_nb = nb; wl.w_c = c; wl.w_n_e = n_eall; wl.w_n_es = n_e; wl.watch_done = 1; }
+        }
+    }
+#endif
     const int h_end = c >= 1 ? sh.win_hi[c - 1] : 0;  // slots applied: < win_hi[c - 1]
     if (tid < c) {
         const int64_t j = start + tid;

@@ -729,6 +729,21 @@ struct WinWS {
     int32_t touched[kTouchMax];
     int32_t n_touched, rescan;
     int32_t lset, pad_;                   // pruned lists: the set holding this batch's lists (EngineArgs)
+#ifdef KS_BATCH_LOG  // (diagnostic builds only: per-batch log and one watched pod's batch, ks_debug_window)
+    int32_t blog_n, watch_pod, watch_done, wpad_;
+    int32_t blog[16384][4];               // per chunk-resolver batch: start (low 31 bits), committed, stop code, nb
+    int32_t w_start, w_nb, w_c, w_n_e, w_n_es, w_pad[3];
+    uint64_t w_cl_key[kWinMaxB][kChR];
+    int32_t w_cl_info[kWinMaxB];
+    uint64_t w_cl_thr[kWinMaxB];
+    int32_t w_e_node[kEMax];
+    int32_t w_bind[kWinMaxB];             // the batch's committed binds (node)
+    int32_t w_adm[kWinMaxB];
+    int32_t w_nsw, w_pad2;
+    int32_t w_dec[64][8];                 // watched pod, per sweep: fresh, lo, bad, code, nw cid, dc cid, dk total, c0
+    int16_t w_smeta[64][8];               // its chunk's rows at the chunk's end
+    int32_t w_rowcid[64];
+#endif
 };
 
 // Arguments of the batch kernels (expire_head / scan / resolve).

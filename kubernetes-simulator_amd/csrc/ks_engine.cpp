@@ -1937,6 +1937,31 @@ ks_status ks_debug_invariants(ks_engine* e, int64_t* out4) {
     return KS_OK;
 }
 
+ks_status ks_debug_window(ks_engine* e, void* out, int64_t cap, int64_t* size_out) {
+    if (!e || !size_out) return KS_EINVAL;
+    *size_out = (int64_t)sizeof(ks::WinWS);
+    if (!e->d_sweep || !out || cap <= 0) return KS_OK;
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipMemcpyAsync(out, e->d_sweep, std::min<int64_t>(cap, sizeof(ks::WinWS)), hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    return KS_OK;
+}
+
+ks_status ks_debug_watch(ks_engine* e, int64_t pod) {
+    if (!e) return KS_EINVAL;
+#ifdef KS_BATCH_LOG
+    if (ks_status r = ensure_window_ws(e); r != KS_OK) return r;
+    const int32_t w[2] = {(int32_t)pod, 0};
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipMemcpyAsync(&e->d_sweep->watch_pod, w, sizeof w, hipMemcpyHostToDevice, e->st));
+    HIPCHK(e, hipStreamSynchronize(e->st));
+    return KS_OK;
+#else
+    (void)pod;
+    return KS_EINVAL;  // (a KS_BATCH_LOG diagnostic build only)
+#endif
+}
+
 void ks_set_profiling(ks_engine* e, int enable) {
     if (e) e->profiling = enable != 0;
 }

@@ -34,7 +34,7 @@ STATUS_NAMES = {KS_OK: "OK", KS_EINVAL: "InvalidArgument", KS_ENOTFOUND: "NotFou
 # every symbol include/*.h declares
 EXPORTED_SYMBOLS = ("ks_create", "ks_destroy", "ks_load_nodes", "ks_submit_pods", "ks_step",
                     "ks_filter", "ks_score", "ks_usage", "ks_current_tick", "ks_tick_seconds", "ks_queued_pods",
-                    "ks_last_error", "ks_last_step_stats", "ks_last_step_kernels", "ks_set_profiling", "ks_debug_counters", "ks_debug_invariants", "ks_build_id", "ks_selftest",
+                    "ks_last_error", "ks_last_step_stats", "ks_last_step_kernels", "ks_set_profiling", "ks_debug_counters", "ks_debug_invariants", "ks_debug_window", "ks_debug_watch", "ks_build_id", "ks_selftest",
                     "ks_comm_unique_id", "ks_shard", "ks_shard_host", "ks_group_create", "ks_group_destroy",
                     "ks_group_add", "ks_group_size", "ks_group_step", "ks_pod_status",
                     "ks_usage_at", "ks_usage_digest", "ks_node_mix", "ks_pod_lookup", "ks_node_pods",
@@ -204,6 +204,10 @@ def load():
     L.ks_debug_counters.restype = C.c_int
     L.ks_debug_invariants.argtypes = [p, p]
     L.ks_debug_invariants.restype = C.c_int
+    L.ks_debug_window.argtypes = [p, p, C.c_int64, C.POINTER(C.c_int64)]
+    L.ks_debug_window.restype = C.c_int
+    L.ks_debug_watch.argtypes = [p, C.c_int64]
+    L.ks_debug_watch.restype = C.c_int
     L.ks_set_profiling.argtypes = [p, C.c_int]
     L.ks_set_profiling.restype = None
     L.ks_selftest.argtypes = [C.c_int32, C.c_int32, p]

@@ -252,6 +252,18 @@ class Engine:
         self._check(self._L.ks_debug_invariants(self.h, _p(out)))
         return dict(slot_marks=int(out[0]), e_marks=int(out[1]), nslot_hw=int(out[2]), slot_max=int(out[3]))
 
+    def debug_window(self) -> bytes:
+        """The raw batch window workspace (include/ks_engine.h ks_debug_window; diagnostics)."""
+        n = C.c_int64(0)
+        self._check(self._L.ks_debug_window(self.h, None, 0, C.byref(n)))
+        buf = C.create_string_buffer(n.value)
+        self._check(self._L.ks_debug_window(self.h, buf, n.value, C.byref(n)))
+        return buf.raw
+
+    def debug_watch(self, pod: int):
+        """Record pod's batch in the window workspace (a -DKS_BATCH_LOG diagnostic build only)."""
+        self._check(self._L.ks_debug_watch(self.h, pod))
+
     def set_profiling(self, on: bool):
         self._L.ks_set_profiling(self.h, 1 if on else 0)
 

@@ -37,6 +37,55 @@ for r in range(world):
     e.load_nodes(enc["alloc"], enc["taint"], enc["label"])
     e.submit(enc["pods"])
     es.append(e)
+WATCH = int(os.environ.get("WATCH", "-1"))
+if WATCH >= 0:
+    es[0].debug_watch(WATCH)
+
+
+def win_dtype():
+    """ks_device.h WinWS of a -DKS_BATCH_LOG build, field for field (C alignment)."""
+    B, S, R, E = 256, 512, 20, 2048
+    return np.dtype([
+        ("nb", "i4"), ("e_cnt", "i4"), ("n_e", "i4"), ("n_es", "i4"),
+        ("win_hi", "i4", B), ("own", "i4", B), ("ex_q", "i4", S), ("ex_ok", "i4", S), ("ex_req", "i8", (S, 3)),
+        ("e_node", "i4", E), ("e_off", "i4", S + 1), ("e_slot", "i4", S), ("e_rec", "u4", (E, 12)),
+        ("cl_key", "u8", (B, R)), ("cl_info", "i4", B), ("cl_thr", "u8", B), ("cl_slot", "i4", (B, R)),
+        ("nslot", "i4"), ("nslot_hw", "i4"), ("slot_node", "i4", B * R), ("slot_eix", "i4", 1536),
+        ("slot_rec", "u4", (1536, 20)), ("touched", "i4", B + S), ("n_touched", "i4"), ("rescan", "i4"),
+        ("lset", "i4"), ("pad_", "i4"),
+        ("blog_n", "i4"), ("watch_pod", "i4"), ("watch_done", "i4"), ("wpad_", "i4"), ("blog", "i4", (16384, 4)),
+        ("w_start", "i4"), ("w_nb", "i4"), ("w_c", "i4"), ("w_n_e", "i4"), ("w_n_es", "i4"), ("w_pad", "i4", 3),
+        ("w_cl_key", "u8", (B, R)), ("w_cl_info", "i4", B), ("w_cl_thr", "u8", B), ("w_e_node", "i4", E),
+        ("w_bind", "i4", B), ("w_adm", "i4", B)], align=True)
+
+
+def show_watch(e, nodes_of_interest):
+    raw = e.debug_window()
+    dt = win_dtype()
+    assert len(raw) == dt.itemsize, (len(raw), dt.itemsize)
+    w = np.frombuffer(raw, dt)[0]
+    n = int(w["blog_n"])
+    lg = w["blog"][:min(n, 16384)]
+    near = [tuple(int(x) for x in r) for r in lg if r[0] <= WATCH + 400 and r[0] + r[3] >= WATCH - 600]
+    print(f"batches logged {n}; around pod {WATCH} (start, committed, stop, nb): {near}")
+    if not w["watch_done"]:
+        print("watched pod not recorded")
+        return
+    s0, nb, c = int(w["w_start"]), int(w["w_nb"]), int(w["w_c"])
+    i = WATCH - s0
+    E = set(int(x) for x in w["w_e_node"][:int(w["w_n_e"])])
+    print(f"watch batch: start {s0} nb {nb} committed {c} n_e {int(w['w_n_e'])} (slot-E {int(w['w_n_es'])}); pod index {i} (chunk {i // 64})")
+    info = int(w["w_cl_info"][i])
+    keys = [int(k) for k in w["w_cl_key"][i][:info & 0xFF]]
+    print(f"pod {WATCH}: info kept {info & 0xFF} trunc {bool(info & 256)} full {bool(info & 512)} ovf {bool(info & 1024)}; "
+          f"thr total {int(w['w_cl_thr'][i]) >> 32} node {0xFFFFFFFF - (int(w['w_cl_thr'][i]) & 0xFFFFFFFF)}")
+    print("   cl (node, total):", [(0xFFFFFFFF - (k & 0xFFFFFFFF), (k >> 32) - 1) for k in keys])
+    for nd in nodes_of_interest:
+        js = [s0 + j for j in range(c) if int(w["w_bind"][j]) == nd]
+        print(f"   node {nd}: in E {nd in E}; binds in the batch at pods {js}")
+    print("   batch binds before the pod:", [(s0 + j, int(w["w_bind"][j]), int(w["w_adm"][j])) for j in range(max(0, i - 8), i + 1)])
+
+
 done = 0
 nodes, stats = [], []
 first_bad = None
@@ -60,6 +109,8 @@ for w, want in enumerate(g["bind_digests"]):
                 print(f"   rank {r} differs from rank 0 first at pod {done + int(d[0])}", flush=True)
     if first_bad is None and not all(ok):
         first_bad = w
+    if WATCH >= 0 and done <= WATCH < done + k:
+        show_watch(es[0], [int(x) for x in os.environ.get("WATCH_NODES", "").split(",") if x])
     nodes.append(np.stack([b["node"] for b in res]))
     stats.append(np.stack([b["status"] for b in res]))
     done += k

@@ -84,3 +84,36 @@ def test_c5_whole_trace_sharded_and_unsharded_match_oracle_golden(c5):
     for k in range(3):
         has = alloc[:, k] >= 0
         assert (u[has, k] <= alloc[has, k]).all(), f"resource {k} over capacity"
+
+
+@pytest.mark.parametrize("s0", [167_117, 167_120, 167_127, 166_989, 167_053, 167_128])
+def test_c5_segment_overflow_row_on_either_lane_half(c5, s0):
+    """Regression test of the round-6 chunk-resolver fix (ks_chunk.hip phase C).
+    A batch forced to start at s0 (ks_step(s0), then the rest: a step's first batch starts at its
+    first pod) puts pods 167,117 .. 167,180 in one 64-pod chunk in which node 46 changes state six
+    times before pod 167,180 (a window expiry, three binds, a second window expiry) — more than the
+    five state segments a row holds, so the row's state is unknown for pod 167,180 and the batch must
+    stop before it.  The row sits on a lane of the other half of the pod's 16-lane group, whose
+    stop flag the old divergent ballot dropped: pod 167,180 then took node 84 instead of node 46
+    (both total 18; 46 is the lower index).  Window 10 of the C5 golden (pods 163,840 .. 180,223)
+    bind-for-bind against the oracle's digest, with the first ten windows as the run's prefix.
+    (s0 = 167,128 is the alignment that never overflowed: the first expiry becomes a head expiry.)"""
+    tr, enc = c5
+    g = full_run_digest.load("c5")
+    if g is None:
+        pytest.skip("no c5 golden")
+    W = g["window"]
+    eng = make_engine(tr, enc, MODE)
+    eng.submit(enc["pods"])
+    done = 0
+    w = 0
+    while done + W <= s0:
+        b = eng.step(W)
+        assert full_run_digest.bind_digest(b) == g["bind_digests"][w], f"window {w}"
+        done += W
+        w += 1
+    parts = [eng.step(s0 - done)] if s0 > done else []
+    parts.append(eng.step(done + W - s0))
+    b = np.concatenate(parts)
+    assert len(b) == W and int(b["pod"][0]) == done
+    assert full_run_digest.bind_digest(b) == g["bind_digests"][w], f"window {w} with a batch forced to start at {s0}"

@@ -157,6 +157,21 @@ def test_c3_reference_literal_prefix(c3):
     np.testing.assert_array_equal(eng.usage(), ora.usage())
 
 
+def test_c3_whole_trace_reference_literal_matches_oracle_golden(c3):
+    """The reference's own filter behaviour over the WHOLE 1M-pod C3 trace:
+    scheduleOneFilter's result is discarded (kubesim/kubesim.go:182), every node is scored and only
+    admission (kubesim/node/node.go:44-47) decides Ok vs OverCapacity — every window bind-for-bind
+    and every other window's usage against the oracle's committed digests (tests/golden/full_run.json
+    "c3lit"), at the bench's batch (bench.py's c3_literal leg)."""
+    tr, enc = c3
+    g = full_run_digest.load("c3lit")
+    assert g is not None and g["pods"] == tr["pods"]["m"] and g["mode"] == "literal_lrba_filters_ignored"
+    eng = make_engine(tr, enc, g["mode"])
+    eng.submit(enc["pods"])
+    b = full_run_digest.check_engine_run(eng, g, "c3lit")
+    assert (b["status"] == 1).any(), "the literal mode binds OverCapacity pods"
+
+
 def test_c3_full_trace_batch_independent_and_invariants(c3):
     tr, enc = c3
     m, n = tr["pods"]["m"], tr["nodes"]["n"]
