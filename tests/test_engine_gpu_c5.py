@@ -117,3 +117,18 @@ def test_c5_segment_overflow_row_on_either_lane_half(c5, s0):
     b = np.concatenate(parts)
     assert len(b) == W and int(b["pod"][0]) == done
     assert full_run_digest.bind_digest(b) == g["bind_digests"][w], f"window {w} with a batch forced to start at {s0}"
+
+
+@pytest.mark.parametrize("batch", list(range(128, 257, 16)) + [132, 188, 196, 252])
+def test_c5_whole_trace_at_other_batch_sizes(c5, batch):
+    """The whole C5 run against the oracle's digests at other batch sizes: each moves every batch
+    and chunk boundary, so the chunk resolver's alignment-dependent stops (segment overflow,
+    exhausted or truncated lists, slot cuts) fall on other pods (round 6: the lost stop flag above
+    showed under 33 of 192 alignments of one batch)."""
+    tr, enc = c5
+    g = full_run_digest.load("c5")
+    if g is None:
+        pytest.skip("no c5 golden")
+    eng = make_engine(tr, enc, MODE, batch_pods=batch)
+    eng.submit(enc["pods"])
+    full_run_digest.check_engine_run(eng, g, f"c5 batch {batch}")

@@ -105,6 +105,17 @@ def test_c3_40k_pods_bit_exact_with_usage_samples(c3):
     assert_same_binds(eb, ob)
 
 
+@pytest.mark.parametrize("batch", [160, 176, 208, 256])
+def test_c3_whole_trace_at_other_batch_sizes(c3, batch):
+    """The whole 1M-pod C3 trace against the oracle's digests at other batch sizes (every batch and
+    chunk boundary moves: the chunk resolver's alignment-dependent stops fall on other pods)."""
+    tr, enc = c3
+    g = full_run_digest.load("c3")
+    eng = make_engine(tr, enc, MODE, batch_pods=batch)
+    eng.submit(enc["pods"])
+    full_run_digest.check_engine_run(eng, g, f"c3 batch {batch}")
+
+
 @pytest.mark.parametrize("flags", [0, _lib.KS_ENGINE_PRUNED_LISTS], ids=["default", "pruned_lists"])
 def test_c3_whole_trace_matches_oracle_golden(c3, flags):
     """Every pod of the 1M-pod trace — the whole range bench.py times — bind-for-bind against the
