@@ -164,6 +164,56 @@ def load_pmc(config: str = "c3"):
     return {"per_role": per, "source": d.get("source", p), "file": os.path.relpath(p, ROOT)}
 
 
+def usage_roofline(trace, kept, q_ticks, ku):
+    """The per-tick usage kernel's roofline.  Algorithmic
+    bytes of one query at tick t (§8(d)): per pod running at t, 16 B (node, t0, phase offset, phase
+    count) + 4 B per phase scanned (the cumulative seconds up to its current phase) + 24 B of usage
+    read + 24 B accumulated into its node — computed here from the binds and the trace.  achieved =
+    those bytes / the kernel's HIP-event time (ks_last_step_kernels usage_ms / usage_n, the same ten
+    queries); frac = achieved / 8,000 GB/s.  Beside it the committed PMC bytes of the kernel
+    (profiles/pmc_c3.json "ks::usage_kernel": 2 x FETCH_SIZE + WRITE_SIZE, its own short run)."""
+    import numpy as np
+    if not ku.get("usage_n"):
+        return None
+    b = np.concatenate(kept)
+    p = trace["pods"]
+    tick = trace["tick_seconds"]
+    off = p["phase_off"].astype(np.int64)
+    sec = p["phase_sec"].astype(np.int64)
+    q = b["pod"].astype(np.int64)
+    tot = np.add.reduceat(sec, off[:-1])[q] if len(sec) else np.zeros(len(q), np.int64)
+    tot = np.where(off[q + 1] > off[q], tot, 0)
+    dur = -(-tot // tick)
+    alg, nrun = [], []
+    for t in q_ticks:
+        run = (b["status"] == 0) & (b["tick"] <= t) & (t < b["tick"] + dur)
+        nrun.append(int(run.sum()))
+        nbytes = 0
+        for j in np.nonzero(run)[0]:
+            passed = (t - int(b["tick"][j])) * tick
+            cs = np.cumsum(sec[off[q[j]]:off[q[j] + 1]])
+            k = int(np.searchsorted(cs, passed, side="right"))  # first phase whose end is past `passed`
+            nbytes += 16 + 4 * min(k + 1, len(cs)) + 24 + 24
+        alg.append(nbytes)
+    ms = ku["usage_ms"] / ku["usage_n"]
+    a = float(np.mean(alg))
+    achieved = a / (ms * 1e-3) / 1e9 if ms > 0 else None
+    pmc = None
+    pth = os.path.join(ROOT, "profiles", "pmc_c3.json")
+    if os.path.exists(pth):
+        with open(pth) as f:
+            v = json.load(f).get("per_kernel", {}).get("ks::usage_kernel")
+        if v and "FETCH_SIZE_KB_avg" in v and "WRITE_SIZE_KB_avg" in v:
+            pmc = int((2 * v["FETCH_SIZE_KB_avg"] + v["WRITE_SIZE_KB_avg"]) * 1024)
+    return {"bound": "latency (one small launch)", "kernel": "usage_kernel", "launch_ms": ms,
+            "algorithmic_bytes": a, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS if achieved else None,
+            "running_pods": float(np.mean(nrun)),
+            "pods_read_per_launch": ku["usage_pods"] / ku["usage_n"], "traffic_pmc": pmc,
+            "model": "per running pod 16 B + 4 B per phase scanned + 24 B usage read + 24 B node accumulate "
+                     "(SURVEY.md 8(d)); the [N][3] zeroing and copy are outside the kernel"}
+
+
 def roofline_block(value, st, ks, nodes, config, stream_gbs=None):
     """The roofline object: one formula, one configuration.
 
@@ -301,8 +351,9 @@ def main():
     log(f"[rank {rank}] trace {args.nodes} nodes x {n_pods} pods ready in {time.perf_counter() - t0:.1f}s")
 
     S = args.pods_per_step
+    kept = []  # every step's binds (the usage kernel's algorithmic bytes need the placements)
     for _ in range(args.warmup):
-        eng.step(S)
+        kept.append(eng.step(S))
 
     def barrier():
         # ks_step synchronises the engine's stream before returning; the extra device-wide
@@ -320,7 +371,9 @@ def main():
     t_start = time.perf_counter()
     binds = 0
     for _ in range(args.steps):
-        binds += len(eng.step(S))   # ks_step returns after its last kernel has completed
+        b = eng.step(S)   # ks_step returns after its last kernel has completed
+        binds += len(b)
+        kept.append(b)
     t_el = time.perf_counter() - t_start
     barrier()
     if dist is not None:
@@ -336,7 +389,7 @@ def main():
 
     # per-kernel breakdown on one more (profiled) step: HIP events on the engine's stream
     eng.set_profiling(True)
-    eng.step(S)
+    kept.append(eng.step(S))
     st = eng.last_step_stats()
     kst = eng.last_step_kernels()
     eng.set_profiling(False)
@@ -346,9 +399,17 @@ def main():
     t_now = eng.tick
     eng.usage_at(t_now)
     t_u = time.perf_counter()
-    for k in range(10):
-        eng.usage_at(max(0, t_now - 1000 * k))
+    q_ticks = [max(0, t_now - 1000 * k) for k in range(10)]
+    for t_q in q_ticks:
+        eng.usage_at(t_q)
     usage_ms = (time.perf_counter() - t_u) * 100.0
+    # the usage kernel's roofline: the same ten queries with HIP events around the kernel alone
+    eng.set_profiling(True)
+    for t_q in q_ticks:
+        eng.usage_at(t_q)
+    ku = eng.last_step_kernels()
+    eng.set_profiling(False)
+    usage_roof = usage_roofline(trace, kept, q_ticks, ku)
     t_u = time.perf_counter()
     eng.usage_digest(max(0, t_now - S + 1), t_now + 1)
     digest_ms = (time.perf_counter() - t_u) * 1e3
@@ -408,7 +469,7 @@ def main():
                         "other_avg_ms": other_avg_ms,
                         "profiled_step_ms": st["step_ms"], "per_kernel": kst},
             "usage_query": {"ms_per_call": usage_ms, "nodes": nodes, "tick": t_now,
-                            "digest_ms": digest_ms, "digest_ticks": S,
+                            "digest_ms": digest_ms, "digest_ticks": S, "roofline": usage_roof,
                             "note": "ks_usage_at wall time at ticks near the end of the run, incl. the "
                                     "24 B/node copy to the host; digest = every tick of the last step's window"},
             "dropin": dropin,

@@ -286,6 +286,15 @@ ks_status ks_last_step_stats(const ks_engine* eng, ks_step_stats* out);
 typedef struct {
     double prep_ms, scan_ms, merge_ms, resolve_ms, fused_ms, part_ms, xchg_ms;
     int64_t prep_n, scan_n, merge_n, resolve_n, fused_n, xchg_n;
+    /* the pipelined sharded chain (engines the fused overlap does not take): the next batch's
+     * speculative scan, part merges and exchange on the second stream beside the resolve (side_n
+     * batches), and the main stream's wait for that exchange (inside merge_ms's batches) */
+    double side_scan_ms, side_part_ms, side_xchg_ms, wait_ms;
+    int64_t side_n;
+    /* ks_usage_at calls made while profiling is on (summed since the last ks_step): the usage kernel's
+     * HIP-event ms, its launches, and the pods of the candidate blocks it read */
+    double usage_ms;
+    int64_t usage_n, usage_pods;
 } ks_kernel_stats;
 ks_status ks_last_step_kernels(const ks_engine* eng, ks_kernel_stats* out);
 ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, int64_t* n_out,

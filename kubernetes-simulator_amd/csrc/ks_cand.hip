@@ -98,6 +98,7 @@ constexpr int kEPer = kEMax / 256;
 // in the snapshot order, and the list's own order bounds every node outside it.  (kLL = kTopL: the
 // list's entries outside E and thr = its last key; the overlap's longer lists keep kTopL exact
 // entries even when the previous batch bound some of the top ones.)
+static_assert(kTopLOverlap >= kTopL, "merged lists kept at the longest list length");
 template <int kMode, int kLL>
 __device__ __forceinline__ void cand_list(const EngineArgs& a, WinWS& ws, int i, const uint64_t* cand,
                                           const uint64_t* ek, int n_e) {
@@ -210,15 +211,16 @@ namespace sq {
 template <int kMode, int kLL>
 #ifdef KS_MCL_BYVAL  // (diagnostic build only: the engine arguments by value, VERDICT r5 item 1's A/B)
 __global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs av, const uint64_t* src,
-                                                         int64_t pod_stride, int32_t nl, int64_t list_stride) {
+                                                         int64_t pod_stride, int32_t nl, int64_t list_stride, int own_fb) {
     const EngineArgs& a = av;
 #else
 __global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs* __restrict__ A, const uint64_t* src,
-                                                         int64_t pod_stride, int32_t nl, int64_t list_stride) {
+                                                         int64_t pod_stride, int32_t nl, int64_t list_stride, int own_fb) {
     const EngineArgs& a = A[0];
 #endif
     WinWS& ws = *a.sw;
-    const bool own = src == nullptr;
+    // (own_fb: a pipelined engine's rescan scanned every block locally — its own lists, not src)
+    const bool own = src == nullptr || (own_fb && ws.rescan);
     if (own) {
         src = a.lists;
         pod_stride = (int64_t)a.nblk * kLL;
@@ -231,21 +233,28 @@ __global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs* __rest
     const bool prn = a.lbit != nullptr;
     const int lset = prn ? ws.lset : 1;
     const bool pruned = own && prn;
+    // the previous batch stopped early (ks_prep.h): pods b < split take the merged lists kept for
+    // them, the others the speculative scan's lists at slot sb = b - split
+    const int nbw = ws.nb, split = ws.split, moff = ws.moff, mpar = ws.mpar;
+    const bool reuse = b < split;
+    const int sb = b - split;
     // pruned: the flagged blocks of the batch's set (one round trip for the bitmap words); then both
-    // sets' bitmaps and thresholds of pod b are cleared for the next scans (every pod slot: b >= nb too)
+    // sets' bitmaps and thresholds of one pod slot are cleared for the next scans — every slot once:
+    // this workgroup's own slot sb, the slots no pod reads ([nb - split, B)) by the others
     __shared__ scn::FlagLDS F;
-    int nfl = nl;
-    if (b < ws.nb && pruned) nfl = scn::flagged_index(lbit_of(a, lset, b), 0, nl, F);
+    int nfl = reuse ? 0 : nl;
+    if (b < nbw && !reuse && pruned) nfl = scn::flagged_index(lbit_of(a, lset, sb), 0, nl, F);
     if (prn) {
-        for (int w = tid; w < 2 * a.nwl; w += nthr) lbit_of(a, w / a.nwl, b)[w % a.nwl] = 0;
-        if (tid < 2 * kThrCopies) *lthr_of(a, tid / kThrCopies, tid % kThrCopies, b) = 0;
+        const int cs = b < split ? nbw - split + b : (b < nbw ? sb : b);
+        for (int w = tid; w < 2 * a.nwl; w += nthr) lbit_of(a, w / a.nwl, cs)[w % a.nwl] = 0;
+        if (tid < 2 * kThrCopies) *lthr_of(a, tid / kThrCopies, tid % kThrCopies, cs) = 0;
     }
-    if (b >= ws.nb) return;  // (the window prep cut the batch; errors left nb = 0)
+    if (b >= nbw) return;  // (the window prep cut the batch; errors left nb = 0)
     PDG(uint64_t pt = pstamp(); if (tid == 0) atomicAdd((unsigned long long*)&a.ctr[5], 1ull);)
     uint64_t top[kLL];
 #pragma unroll
     for (int k = 0; k < kLL; ++k) top[k] = 0;
-    const uint64_t* lists = src + (int64_t)b * pod_stride;
+    const uint64_t* lists = src + (int64_t)(reuse ? 0 : sb) * pod_stride;
     // independent reads first: this thread's first block list, then the E nodes' keys (dependent
     // chains: node, slots, expiring requests) while it is in flight
     uint64_t lv0[kLL];
@@ -389,6 +398,11 @@ __global__ __launch_bounds__(1024) void merge_cl_kernel(const EngineArgs* __rest
         }
     }
     __syncthreads();
+    // a reused pod's merged list as merge_cl kept it for the previous batch; every pod's merged list
+    // kept for the next (its possible reuse)
+    if (reuse && tid < kLL) pc[tid] = ws.mrg[mpar ^ 1][b + moff][tid];
+    if (reuse) __syncthreads();
+    if (tid < kLL) ws.mrg[mpar][b][tid] = pc[tid];
     PDG(MDG_AT(8, pt);)
     cand_list<kMode, kLL>(a, ws, b, pc, ek, n_e);
 }
@@ -402,7 +416,8 @@ hipError_t launch_window_prep(const EngineArgs* d, bool head, bool spec, int slo
 }
 
 hipError_t launch_merge_cl(const EngineArgs* d, int mode, int B, const uint64_t* lists, int64_t pod_stride,
-                           int32_t nl, int64_t list_stride, int nl_max, hipStream_t st, int L) {
+                           int32_t nl, int64_t list_stride, int nl_max, hipStream_t st, int L, bool own_fallback) {
+    const int fb = own_fallback ? 1 : 0;
     static_assert(sq::kEPer * 256 >= kEMax, "E keys per thread at 256 threads");
     const dim3 g(B), t(nl_max > 1024 ? 1024 : 256);
 #ifdef KS_MCL_BYVAL
@@ -412,10 +427,10 @@ hipError_t launch_merge_cl(const EngineArgs* d, int mode, int B, const uint64_t*
 #endif
 #define KS_MCL(LL)                                                                                                   \
     switch (mode) {                                                                                                  \
-        case kEvalMicro: hipLaunchKernelGGL((sq::merge_cl_kernel<kEvalMicro, LL>), g, t, 0, st, d, lists, pod_stride, nl, list_stride); break; \
-        case kEvalTiny: hipLaunchKernelGGL((sq::merge_cl_kernel<kEvalTiny, LL>), g, t, 0, st, d, lists, pod_stride, nl, list_stride); break;   \
-        case kEvalNarrow: hipLaunchKernelGGL((sq::merge_cl_kernel<kEvalNarrow, LL>), g, t, 0, st, d, lists, pod_stride, nl, list_stride); break; \
-        default: hipLaunchKernelGGL((sq::merge_cl_kernel<kEvalWide, LL>), g, t, 0, st, d, lists, pod_stride, nl, list_stride); break;          \
+        case kEvalMicro: hipLaunchKernelGGL((sq::merge_cl_kernel<kEvalMicro, LL>), g, t, 0, st, d, lists, pod_stride, nl, list_stride, fb); break; \
+        case kEvalTiny: hipLaunchKernelGGL((sq::merge_cl_kernel<kEvalTiny, LL>), g, t, 0, st, d, lists, pod_stride, nl, list_stride, fb); break;   \
+        case kEvalNarrow: hipLaunchKernelGGL((sq::merge_cl_kernel<kEvalNarrow, LL>), g, t, 0, st, d, lists, pod_stride, nl, list_stride, fb); break; \
+        default: hipLaunchKernelGGL((sq::merge_cl_kernel<kEvalWide, LL>), g, t, 0, st, d, lists, pod_stride, nl, list_stride, fb); break;          \
     }
     if (L == kTopL) { KS_MCL(kTopL) }
     else if (L == kTopLOverlap) { KS_MCL(kTopLOverlap) }

@@ -684,7 +684,8 @@ constexpr int kSlotMax = 1536;  // candidate slots whose record / E index merge_
 constexpr int kSlotIds = kWinMaxB * kChR;
 constexpr int kEMax = 2048;     // E nodes per batch: the window's expiry nodes + the overlap's touched nodes
 constexpr int kTouchMax = kWinMaxB + kWinSlots;
-constexpr int kSpecStride = 8;  // int64 counters per speculative set  // nodes a batch changes: its binds + its window's expiry nodes
+constexpr int kSpecStride = 8;  // int64 counters per speculative set
+constexpr int kSpecPrev = 3;    // (in a set: the start of the batch that wrote it)
 enum : int32_t { kClTrunc = 1 << 8, kClFull = 1 << 9, kClOvf = 1 << 10 };
 struct WinWS {
     int32_t nb, e_cnt, n_e, n_es;         // E nodes; the first n_es have window slots (<= kWinSlots)
@@ -729,6 +730,12 @@ struct WinWS {
     int32_t touched[kTouchMax];
     int32_t n_touched, rescan;
     int32_t lset, pad_;                   // pruned lists: the set holding this batch's lists (EngineArgs)
+    // Early stop without a rescan (round 6): when the previous batch k stopped early, this batch's
+    // first `split` pods are batch k's pods [moff, moff + split) and take the merged top-L lists
+    // merge_cl kept for them (mrg[mpar ^ 1]); the others take the speculative scan's lists at slot
+    // b - split.  merge_cl keeps every batch's merged lists in mrg[mpar] (mpar = the batch parity).
+    int32_t split, moff, mpar, pad2_;
+    uint64_t mrg[2][kWinMaxB][kTopLOverlap];
 #ifdef KS_BATCH_LOG  // (diagnostic builds only: per-batch log and one watched pod's batch, ks_debug_window)
     int32_t blog_n, watch_pod, watch_done, wpad_;
     int32_t blog[16384][4];               // per chunk-resolver batch: start (low 31 bits), committed, stop code, nb
@@ -807,17 +814,20 @@ hipError_t launch_expire_head(const EngineArgs* d, int S, hipStream_t st);
 // prune: the pruned-list form (the engine's lbit / lthr set, ks_scan.h)
 // L: the block lists' length (kTopL; kTopLOverlap for the overlap's single-shard engines: key16, not
 // pruned)
+// pw > 0 (one engine): a grid of at most pw workgroups, each looping over its XCD's items (the
+// pipelined engines' conditional rescan: cheap to launch when nothing is flagged)
 hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int mode, bool key16, hipStream_t st,
-                       bool cond = false, bool prune = false, int L = kTopL, bool stage = false);
+                       bool cond = false, bool prune = false, int L = kTopL, bool stage = false, int pw = 0);
 // per scenario and pod b < batch size: exact top-L over nl sorted lists
 // lists[b*pod_stride + k*list_stride] into out (lists == nullptr: the scenario's own block lists
 // into its candidate lists)
 // nl_max: the largest nl of the launch (<= 64 / L candidates per pod: one wave per pod)
 // bits (pruned lists, ks_scan.h; nullptr: read every list): the pods' bitmaps ([B][nwl]); list k of
 // the range is block blk0 + k
+// lset_fixed >= 0: read that list set's bitmaps (not the window's WinWS::lset)
 hipError_t launch_merge(const EngineArgs* d, int S, int B, const uint64_t* lists, int64_t pod_stride, int32_t nl,
                         int64_t list_stride, uint64_t* out, int nl_max, hipStream_t st, const uint64_t* bits = nullptr,
-                        int32_t nwl = 0, int32_t blk0 = 0);
+                        int32_t nwl = 0, int32_t blk0 = 0, int32_t lset_fixed = -1);
 // the role-split resolver (ks_kernels.hip): batches of up to max_batch_pods() pods, any cluster
 hipError_t launch_resolve(const EngineArgs* d, int S, int mode, hipStream_t st);
 // the register-table resolver (ks_resolve.hip): batches of <= small_resolver_max_batch() pods of
@@ -848,8 +858,11 @@ hipError_t launch_window_prep(const EngineArgs* d, bool head, bool spec, int slo
 #ifdef KS_MCL_BYVAL
 extern thread_local const EngineArgs* ks_mcl_host_args;
 #endif
+// own_fallback: when the window prep flagged a rescan, read the engine's own block lists over the
+// whole cluster instead of `lists` (the pipelined engines' rescan scans every block locally)
 hipError_t launch_merge_cl(const EngineArgs* d, int mode, int B, const uint64_t* lists, int64_t pod_stride,
-                           int32_t nl, int64_t list_stride, int nl_max, hipStream_t st, int L = kTopL);
+                           int32_t nl, int64_t list_stride, int nl_max, hipStream_t st, int L = kTopL,
+                           bool own_fallback = false);
 struct BindSeg {
     const int32_t* node;
     const int32_t* status;

@@ -56,7 +56,9 @@ constexpr int64_t kStageMaxPods = 4096;  // submits of up to this many pods are 
 #ifndef KS_PG_MIN_WG
 #define KS_PG_MIN_WG 2048  // scan workgroups to keep when raising the pods per workgroup
 #endif
-constexpr int kProfEv = 7;  // per launch: prep | scan | part merges | exchange | merge | resolve
+constexpr int kProfEv = 11;  // per launch: prep | scan | part merges | exchange | merge | resolve (+ 4 on the
+                             // pipelined chain's second stream)
+constexpr int kRescanWgs = 1024;  // the pipelined chain's conditional local rescan: workgroups
 constexpr int64_t kNever = std::numeric_limits<int64_t>::max();
 constexpr int64_t kUBlk = 256;   // usage index: pods per block (= the usage kernels' workgroup)
 constexpr int64_t kUSup = 64;    // blocks per super block
@@ -226,6 +228,13 @@ struct ks_engine {
     int64_t* d_spec = nullptr;
     ks::EngineArgs* d_args_spec = nullptr;  // [2]: ctr = d_spec + kSpecStride * parity
     ks::EngineArgs* h_args_spec = nullptr;
+    // the pipelined sharded chain (round 6, step_body): the next batch's speculative scan, per-part
+    // merges and exchange on a second stream beside the resolve; a rescan scans every block locally
+    // (d_args_full: the whole block range, the engine's own list set)
+    hipStream_t st2 = nullptr;
+    hipEvent_t pev_m = nullptr, pev_x = nullptr;
+    ks::EngineArgs* d_args_full = nullptr;
+    ks::EngineArgs* h_args_full = nullptr;
     // group membership (ks_group_add): stream, counters and argument slots belong to the group
     ks_group* group = nullptr;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -557,6 +566,12 @@ void engine_free(ks_engine* e) {
     if (e->d_spec) (void)hipFree(e->d_spec);
     if (e->d_args_spec) (void)hipFree(e->d_args_spec);
     if (e->h_args_spec) (void)hipHostFree(e->h_args_spec);
+    if (e->st2) (void)hipStreamSynchronize(e->st2);
+    if (e->d_args_full) (void)hipFree(e->d_args_full);
+    if (e->h_args_full) (void)hipHostFree(e->h_args_full);
+    if (e->pev_m) (void)hipEventDestroy(e->pev_m);
+    if (e->pev_x) (void)hipEventDestroy(e->pev_x);
+    if (e->st2) (void)hipStreamDestroy(e->st2);
     if (e->d_usage) (void)hipFree(e->d_usage);
     if (e->stage) (void)hipHostFree(e->stage);
     if (e->segs) (void)hipHostFree(e->segs);
@@ -1191,6 +1206,103 @@ static ks_status ensure_window_ws(ks_engine* e) {
 #endif
         e->scan_workers = std::max(15, cus / KS_SCAN_WORKERS_DIV - 1);  // (>= 15: every XCD deals its share to at least one)
     }
+    if (e->world * e->vsh > 1) {  // the pipelined sharded chain's stream, events and full-range arguments
+        HIPCHK(e, hipStreamCreateWithFlags(&e->st2, hipStreamNonBlocking));
+        HIPCHK(e, hipEventCreateWithFlags(&e->pev_m, hipEventDisableTiming));
+        HIPCHK(e, hipEventCreateWithFlags(&e->pev_x, hipEventDisableTiming));
+        HIPCHK(e, hipMalloc(&e->d_args_full, sizeof(ks::EngineArgs)));
+        HIPCHK(e, hipHostMalloc(&e->h_args_full, sizeof(ks::EngineArgs), hipHostMallocDefault));
+    }
+    return KS_OK;
+}
+
+// This rank's per-part merges of its block lists into its parts' slices of cand_all (a: the
+// argument record whose counters name the batch; lset_fixed >= 0: that list set's bitmaps)
+static hipError_t part_merges(ks_engine* e, const ks::EngineArgs* a, hipStream_t s, int lset_fixed) {
+    const int64_t L = ks::kTopL, BL = (int64_t)e->B * L;
+    for (int v = 0; v < e->vsh; v++) {
+        const int p = e->rank * e->vsh + v;
+        const int nlp = e->part_lo[p + 1] - e->part_lo[p];
+        const hipError_t r = ks::launch_merge(a, 1, e->B, e->lists + (int64_t)e->part_lo[p] * L, (int64_t)e->nblk * L, nlp,
+                                              L, e->cand_all + p * BL, nlp, s, e->prune ? e->lbit : nullptr, e->nwl,
+                                              e->part_lo[p], lset_fixed);
+        if (r != hipSuccess) return r;
+    }
+    return hipSuccess;
+}
+
+// The all-gather of every rank's parts of cand_all on stream s: RCCL, or the host callback
+static ks_status exchange(ks_engine* e, hipStream_t s) {
+    const int64_t BL = (int64_t)e->B * ks::kTopL;
+    if (e->comm) {
+        const ncclResult_t nr = ncclAllGather(e->cand_all + (int64_t)e->rank * e->vsh * BL, e->cand_all,
+                                              (size_t)e->vsh * BL, ncclUint64, e->comm, s);
+        if (nr != ncclSuccess) return fail(e, KS_EDEVICE, "ncclAllGather: %s", ncclGetErrorString(nr));
+    } else if (e->xfn) {  // host exchange: this rank's parts out, every rank's parts back
+        const int64_t slice = (int64_t)e->vsh * BL, off = (int64_t)e->rank * slice;
+        HIPCHK(e, hipMemcpyAsync(e->h_xbuf + off, e->cand_all + off, sizeof(uint64_t) * slice, hipMemcpyDeviceToHost, s));
+        HIPCHK(e, hipStreamSynchronize(s));
+        const ks_status xr = e->xfn(e->xuser, e->rank, e->world, e->h_xbuf, (int64_t)sizeof(uint64_t) * slice);
+        if (xr != KS_OK) return fail(e, KS_EDEVICE, "host exchange failed (%d)", (int)xr);
+        HIPCHK(e, hipMemcpyAsync(e->cand_all, e->h_xbuf, sizeof(uint64_t) * slice * e->world, hipMemcpyHostToDevice, s));
+    }
+    return KS_OK;
+}
+
+// One batch of the pipelined sharded chain (step_body).  Main stream: [the pass's first batch: window
+// prep, scan of this rank's blocks, part merges, exchange | later batches: wait for the second
+// stream's exchange, the conditional local rescan (E overflow only) with the E staging] -> merge_cl
+// -> the resolve with the next batch's window in its tail.  Second stream, once merge_cl has read
+// the lists and cleared the speculative set: the next batch's speculative scan of this rank's blocks
+// (the counters this batch's window prep wrote), its part merges and the exchange — beside the
+// resolve.  cand_all and the block lists are single-buffered: each side pass starts after the
+// merge_cl that read the previous one.
+static ks_status pipe_batch(ks_engine* e, int64_t b, int64_t nbat, hipEvent_t* ev) {
+    hipStream_t st = e->st, s2 = e->st2;
+    const ks::EngineArgs* d = e->d_args;
+    const int G = e->world * e->vsh;
+    const int64_t L = ks::kTopL, BL = (int64_t)e->B * L;
+    const bool first = b == 0, more = b + 1 < nbat;
+    if (ev[0]) HIPCHK(e, hipEventRecord(ev[0], st));
+    if (first) {
+        HIPCHK(e, ks::launch_window_prep(d, true, false, (int)(b & 1), st));
+        if (ev[1]) HIPCHK(e, hipEventRecord(ev[1], st));
+        HIPCHK(e, ks::launch_scan(d, 1, e->blk_n, e->B, e->PG, e->mode, key16(e), st, false, e->prune, (int)L, true));
+        if (ev[2]) HIPCHK(e, hipEventRecord(ev[2], st));
+        HIPCHK(e, part_merges(e, d, st, -1));
+        if (ev[5]) HIPCHK(e, hipEventRecord(ev[5], st));
+        if (ks_status r = exchange(e, st); r != KS_OK) return r;
+        if (ev[6]) HIPCHK(e, hipEventRecord(ev[6], st));
+    } else {
+        HIPCHK(e, hipStreamWaitEvent(st, e->pev_x, 0));
+        if (ev[1]) HIPCHK(e, hipEventRecord(ev[1], st));
+        HIPCHK(e, ks::launch_scan(e->d_args_full, 1, e->nblk, e->B, e->PG, e->mode, key16(e), st, true, e->prune, (int)L,
+                                  true, kRescanWgs));
+        if (ev[2]) HIPCHK(e, hipEventRecord(ev[2], st));
+        if (ev[5]) HIPCHK(e, hipEventRecord(ev[5], st));
+        if (ev[6]) HIPCHK(e, hipEventRecord(ev[6], st));
+    }
+    HIPCHK(e, ks::launch_merge_cl(d, e->mode, e->B, e->cand_all, L, G, BL, G, st, (int)L, !first));
+    if (ev[3]) HIPCHK(e, hipEventRecord(ev[3], st));
+    if (more) {
+        HIPCHK(e, hipEventRecord(e->pev_m, st));
+        HIPCHK(e, ks::launch_chunk_scan(d, e->d_args_spec + (b & 1), 0, (int)((b + 1) & 1), e->mode, e->prune, (int)L, st));
+    } else {
+        HIPCHK(e, ks::launch_chunk_only(d, e->mode, st));
+    }
+    if (ev[4]) HIPCHK(e, hipEventRecord(ev[4], st));
+    if (more) {
+        const ks::EngineArgs* ds = e->d_args_spec + (b & 1);
+        HIPCHK(e, hipStreamWaitEvent(s2, e->pev_m, 0));
+        if (ev[7]) HIPCHK(e, hipEventRecord(ev[7], s2));
+        HIPCHK(e, ks::launch_scan(ds, 1, e->blk_n, e->B, e->PG, e->mode, key16(e), s2, false, e->prune, (int)L, false));
+        if (ev[8]) HIPCHK(e, hipEventRecord(ev[8], s2));
+        HIPCHK(e, part_merges(e, ds, s2, 0));
+        if (ev[9]) HIPCHK(e, hipEventRecord(ev[9], s2));
+        if (ks_status r = exchange(e, s2); r != KS_OK) return r;
+        if (ev[10]) HIPCHK(e, hipEventRecord(ev[10], s2));
+        HIPCHK(e, hipEventRecord(e->pev_x, s2));
+    }
     return KS_OK;
 }
 
@@ -1227,9 +1339,23 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
     // 129 us against a 78 us resolve + a 37 us scan; C3: 196 blocks hide under the resolve)
     // (profiling keeps it: the per-kernel events bracket the same launches)
     const bool overlap = fused && e->overlap && e->d_args_spec && key16(e) && e->blk_n <= kOverlapMaxBlocks;
+    // The pipelined sharded chain (round 6; sharded engines the fused overlap does not take, e.g. C5 on
+    // 8 ranks, 512 blocks each): batch b + 1's speculative scan of this rank's blocks, its per-part
+    // merges and the exchange run on a second stream beside batch b's resolve, so only the resolve
+    // (with the next window in its tail), the E staging and merge_cl stay on the critical path.  A
+    // batch that starts inside its predecessor (an early stop) reuses its merged lists (ks_prep.h),
+    // so the exchanged lists always serve; when E overflows, the conditional rescan scans every block
+    // locally (no second exchange: every rank holds the whole table) and merge_cl merges those.
+    const bool pipe = fused && !overlap && e->overlap && e->st2 && e->world * e->vsh > 1;
     // the overlap's single-shard lists are longer (ks_device.h kTopLOverlap, ks_cand.hip cand_list)
     e->L = overlap && e->world * e->vsh == 1 && !e->prune ? ks::kTopLOverlap : ks::kTopL;
-    if (overlap) {
+    if (pipe) {
+        *e->h_args_full = *e->h_args;
+        e->h_args_full->blk_lo = 0;
+        e->h_args_full->blk_n = e->nblk;
+        HIPCHK(e, hipMemcpyAsync(e->d_args_full, e->h_args_full, sizeof(ks::EngineArgs), hipMemcpyHostToDevice, st));
+    }
+    if (overlap || pipe) {
         for (int k = 0; k < 2; k++) {
             e->h_args_spec[k] = *e->h_args;
             e->h_args_spec[k].ctr = e->d_spec + ks::kSpecStride * k;
@@ -1261,6 +1387,13 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
                 }
                 for (int k = 0; k < kProfEv; k++) ev[k] = e->prof_ev[kProfEv * launches + k];
             }
+            if (pipe) {
+                ks_status pr = pipe_batch(e, b, nbat, ev);
+                if (pr != KS_OK) return pr;
+                if (e->profiling) kind.push_back((uint8_t)(8 | (b == 0 ? 1 : 0) | (b + 1 < nbat ? 2 : 0)));
+                launches++;
+                continue;
+            }
             // the chunk resolver's chain is fused: window prep with the head's expiries, the scan,
             // merge with the candidate lists, the resolver (four launches per batch)
             // overlap: batch b > 0 of this pass takes the speculative scan's lists (a conditional
@@ -1280,28 +1413,9 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
                 HIPCHK(e, fused ? ks::launch_merge_cl(d, e->mode, e->B, nullptr, 0, 0, 0, e->nblk, st, e->L)
                                 : ks::launch_merge(d, 1, e->B, nullptr, 0, 0, 0, nullptr, e->nblk, st));
             } else {
-                for (int v = 0; v < e->vsh; v++) {
-                    const int p = e->rank * e->vsh + v;
-                    const int nlp = e->part_lo[p + 1] - e->part_lo[p];
-                    HIPCHK(e, ks::launch_merge(d, 1, e->B, e->lists + (int64_t)e->part_lo[p] * L, (int64_t)e->nblk * L,
-                                               nlp, L, e->cand_all + p * BL, nlp, st, e->prune ? e->lbit : nullptr,
-                                               e->nwl, e->part_lo[p]));
-                }
+                HIPCHK(e, part_merges(e, d, st, -1));
                 if (evx[0]) HIPCHK(e, hipEventRecord(evx[0], st));
-                if (e->comm) {
-                    const ncclResult_t nr = ncclAllGather(e->cand_all + (int64_t)e->rank * e->vsh * BL, e->cand_all,
-                                                          (size_t)e->vsh * BL, ncclUint64, e->comm, st);
-                    if (nr != ncclSuccess) return fail(e, KS_EDEVICE, "ncclAllGather: %s", ncclGetErrorString(nr));
-                } else if (e->xfn) {  // host exchange: this rank's parts out, every rank's parts back
-                    const int64_t slice = (int64_t)e->vsh * BL, off = (int64_t)e->rank * slice;
-                    HIPCHK(e, hipMemcpyAsync(e->h_xbuf + off, e->cand_all + off, sizeof(uint64_t) * slice,
-                                             hipMemcpyDeviceToHost, st));
-                    HIPCHK(e, hipStreamSynchronize(st));
-                    const ks_status xr = e->xfn(e->xuser, e->rank, e->world, e->h_xbuf, (int64_t)sizeof(uint64_t) * slice);
-                    if (xr != KS_OK) return fail(e, KS_EDEVICE, "host exchange failed (%d)", (int)xr);
-                    HIPCHK(e, hipMemcpyAsync(e->cand_all, e->h_xbuf, sizeof(uint64_t) * slice * e->world,
-                                             hipMemcpyHostToDevice, st));
-                }
+                if (ks_status r = exchange(e, st); r != KS_OK) return r;
                 if (evx[1]) HIPCHK(e, hipEventRecord(evx[1], st));
                 HIPCHK(e, fused ? ks::launch_merge_cl(d, e->mode, e->B, e->cand_all, L, G, BL, G, st)
                                 : ks::launch_merge(d, 1, e->B, e->cand_all, L, G, BL, e->cand, G, st));
@@ -1340,6 +1454,30 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
         for (int64_t l = 0; l < launches; l++) {
             float t[4] = {};
             hipEvent_t* E = &e->prof_ev[kProfEv * l];
+            if (kind[l] & 8) {  // pipelined: [0,1) exchange wait, [1,2) scan / rescan + staging, [2,5) part merges,
+                                // [5,6) exchange (the pass's first batch), [6,3) merge_cl, [3,4) resolve; side [7..10]
+                float w = 0, sc = 0, pm = 0, xc = 0, mg = 0, rs = 0;
+                (void)hipEventElapsedTime(&w, E[0], E[1]);
+                (void)hipEventElapsedTime(&sc, E[1], E[2]);
+                (void)hipEventElapsedTime(&pm, E[2], E[5]);
+                (void)hipEventElapsedTime(&xc, E[5], E[6]);
+                (void)hipEventElapsedTime(&mg, E[6], E[3]);
+                (void)hipEventElapsedTime(&rs, E[3], E[4]);
+                ks.wait_ms += w;
+                ks.scan_ms += sc; ks.scan_n += 1; scan_ms += sc;
+                ks.merge_ms += pm + xc + mg; ks.merge_n += 1; other_ms += pm + xc + mg + w;
+                if (kind[l] & 1) { ks.part_ms += pm; ks.xchg_ms += xc; ks.xchg_n += 1; }
+                if (kind[l] & 2) { ks.fused_ms += rs; ks.fused_n += 1; } else { ks.resolve_ms += rs; ks.resolve_n += 1; }
+                res_ms += rs;
+                if (kind[l] & 2) {
+                    float a0 = 0, a1 = 0, a2 = 0;
+                    (void)hipEventElapsedTime(&a0, E[7], E[8]);
+                    (void)hipEventElapsedTime(&a1, E[8], E[9]);
+                    (void)hipEventElapsedTime(&a2, E[9], E[10]);
+                    ks.side_scan_ms += a0; ks.side_part_ms += a1; ks.side_xchg_ms += a2; ks.side_n += 1;
+                }
+                continue;
+            }
             for (int k = 0; k < 4; k++) (void)hipEventElapsedTime(&t[k], E[k], E[k + 1]);
             if (kind[l] & 4) {  // sharded: [2, 5) part merges, [5, 6) exchange, [6, 3) merge
                 float pm = 0, xc = 0;
@@ -1762,11 +1900,21 @@ ks_status ks_usage_at(ks_engine* e, int64_t t, int64_t* usage_out) {
     if (nb) {
         HIPCHK(e, e->d_blk.reserve(nb, e->st));
         HIPCHK(e, hipMemcpyAsync(e->d_blk.p, e->h_blk.data(), sizeof(int32_t) * nb, hipMemcpyHostToDevice, e->st));
+        // (profiling: HIP events around the usage kernel alone — its roofline in bench.py)
+        if (e->profiling && e->ev[2]) HIPCHK(e, hipEventRecord(e->ev[2], e->st));
         HIPCHK(e, ks::launch_usage(e->d_blk.p, nb, q_hi, t, e->cfg.tick_seconds, e->b_node.p, e->b_status.p, e->t0.p,
                                    e->dur.p, e->phase_off.p, e->cum_sec.p, e->use.p, e->d_usage, e->st));
+        if (e->profiling && e->ev[3]) HIPCHK(e, hipEventRecord(e->ev[3], e->st));
     }
     HIPCHK(e, hipMemcpyAsync(usage_out, e->d_usage, sizeof(int64_t) * 3 * e->n, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
+    if (e->profiling && nb && e->ev[2]) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, e->ev[2], e->ev[3]);
+        e->kstats.usage_ms += ms;
+        e->kstats.usage_n += 1;
+        e->kstats.usage_pods += (int64_t)nb * ks::usage_block_pods();
+    }
     return KS_OK;
 }
 

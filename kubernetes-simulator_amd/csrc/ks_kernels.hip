@@ -119,7 +119,8 @@ __global__ __launch_bounds__(256) void expire_head_kernel(const EngineArgs* __re
 // weights) — half the LDS per workgroup, so more workgroups fit a CU.
 constexpr int kStageWgs = 8;  // workgroups staging the E records (grid-stride over n_e <= kEMax)
 template <int kMode, typename KT, bool kPrune, int kLL>
-__global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict__ A, int xcd, int cond, int stage) {
+__global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict__ A, int xcd, int cond, int stage,
+                                                   int pers) {
     extern __shared__ uint32_t kv_raw[];
     KT* const kv = reinterpret_cast<KT*>(kv_raw);  // [PG][kBlockNodes]: total+1 per (pod, node of the block)
     const EngineArgs& a = A[blockIdx.z];
@@ -146,6 +147,15 @@ __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict_
     // XCD back to back: the block's node records come from HBM once and from that XCD's L2 for
     // the other groups (the placement is for speed only; any placement gives the same lists)
     int64_t it_lo;
+    if (xcd && pers) {  // (the pipelined engines' rescan: a fixed grid, each workgroup loops over its XCD's items)
+        const int64_t tot = (int64_t)a.blk_n * groups, per = (tot + 7) / 8;
+        const int64_t lo = (int64_t)(blockIdx.x % 8) * per, hi = min<int64_t>(tot, lo + per);
+        for (int64_t it = lo + blockIdx.x / 8; it < hi; it += gridDim.x / 8) {
+            if (it != lo + blockIdx.x / 8) __syncthreads();  // (the previous item's extraction has read kv)
+            scn::scan_item<kMode, KT, kPrune, kLL>(a, kv, start, nb, groups, it, true, threadIdx.x, (int)(blockIdx.x % kThrCopies));
+        }
+        return;
+    }
     if (xcd) {
         const int64_t tot = (int64_t)a.blk_n * groups, per = (tot + 7) / 8;
         const int64_t k = blockIdx.x / 8;
@@ -169,7 +179,8 @@ constexpr int kMergeMaxWaves = 16;
 // bits[b * nwl ...] flags among blocks [blk0, blk0 + nl) (list k = block blk0 + k) are read
 __global__ __launch_bounds__(1024) void merge_kernel(const EngineArgs* __restrict__ A, const uint64_t* src,
                                                       int64_t pod_stride, int32_t nl, int64_t list_stride,
-                                                      uint64_t* out, const uint64_t* bits, int32_t nwl, int32_t blk0) {
+                                                      uint64_t* out, const uint64_t* bits, int32_t nwl, int32_t blk0,
+                                                      int32_t lset_fixed) {
     const EngineArgs a = A[blockIdx.y];
     if (src == nullptr) {
         src = a.lists;
@@ -192,7 +203,9 @@ __global__ __launch_bounds__(1024) void merge_kernel(const EngineArgs* __restric
     __shared__ scn::FlagLDS F;
     // (a sharded chunk engine's per-part merge: bits = the two sets, [2][B][nwl]; the batch's set is
     // the one its window prep named)
-    const int lset = bits && a.sw ? a.sw->lset : 1;
+    // (lset_fixed >= 0: the pipelined engines' speculative part merges, which run beside the window
+    // prep that rewrites a.sw->lset)
+    const int lset = lset_fixed >= 0 ? lset_fixed : (bits && a.sw ? a.sw->lset : 1);
     const int nfl = bits ? scn::flagged_index(bits + ((int64_t)lset * a.B + b) * nwl, blk0, nl, F) : nl;
     for (int j = tid; j < nfl; j += nthr) {
         const int blk = bits ? scn::flagged_block(j, blk0, nl, F) : j;
@@ -1124,35 +1137,37 @@ hipError_t launch_expire_head(const EngineArgs* d, int S, hipStream_t st) {
 }
 
 template <typename KT, bool kPrune, int kLL>
-static void launch_scan_t(const EngineArgs* d, const dim3& g, size_t lds, int mode, int xcd, int cond, int stage, hipStream_t st) {
+static void launch_scan_t(const EngineArgs* d, const dim3& g, size_t lds, int mode, int xcd, int cond, int stage, int pers,
+                          hipStream_t st) {
     switch (mode) {
-        case kEvalMicro: hipLaunchKernelGGL((scan_kernel<kEvalMicro, KT, kPrune, kLL>), g, dim3(kBlockNodes), lds, st, d, xcd, cond, stage); break;
-        case kEvalTiny: hipLaunchKernelGGL((scan_kernel<kEvalTiny, KT, kPrune, kLL>), g, dim3(kBlockNodes), lds, st, d, xcd, cond, stage); break;
-        case kEvalNarrow: hipLaunchKernelGGL((scan_kernel<kEvalNarrow, KT, kPrune, kLL>), g, dim3(kBlockNodes), lds, st, d, xcd, cond, stage); break;
-        default: hipLaunchKernelGGL((scan_kernel<kEvalWide, KT, kPrune, kLL>), g, dim3(kBlockNodes), lds, st, d, xcd, cond, stage); break;
+        case kEvalMicro: hipLaunchKernelGGL((scan_kernel<kEvalMicro, KT, kPrune, kLL>), g, dim3(kBlockNodes), lds, st, d, xcd, cond, stage, pers); break;
+        case kEvalTiny: hipLaunchKernelGGL((scan_kernel<kEvalTiny, KT, kPrune, kLL>), g, dim3(kBlockNodes), lds, st, d, xcd, cond, stage, pers); break;
+        case kEvalNarrow: hipLaunchKernelGGL((scan_kernel<kEvalNarrow, KT, kPrune, kLL>), g, dim3(kBlockNodes), lds, st, d, xcd, cond, stage, pers); break;
+        default: hipLaunchKernelGGL((scan_kernel<kEvalWide, KT, kPrune, kLL>), g, dim3(kBlockNodes), lds, st, d, xcd, cond, stage, pers); break;
     }
 }
 
 hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int mode, bool key16, hipStream_t st,
-                       bool cond, bool prune, int L, bool stage) {
+                       bool cond, bool prune, int L, bool stage, int pw) {
     // (a staging launch runs even when this rank scans no blocks: merge_cl reads the E records)
     if ((blk_n > 0 || (stage && S == 1)) && S > 0) {
         // one (block, pod group) item per workgroup; one engine: the XCD-aware 1-D deal
         const int groups = (B + PG - 1) / PG;
         const size_t lds = (key16 ? sizeof(uint16_t) : sizeof(uint32_t)) * kBlockNodes * PG;
         const bool xcd = S == 1;
-        const int64_t wgs = std::max<int64_t>(((int64_t)blk_n * groups + 7) / 8 * 8, stage ? kStageWgs : 0);
+        int64_t wgs = std::max<int64_t>(((int64_t)blk_n * groups + 7) / 8 * 8, stage ? kStageWgs : 0);
+        if (pw > 0 && S == 1) wgs = std::max<int64_t>(std::min<int64_t>(wgs, pw / 8 * 8), kStageWgs);  // (persistent)
         const dim3 g = xcd ? dim3((unsigned)wgs, 1, 1) : dim3(blk_n, groups, S);
         const int x = xcd ? 1 : 0, c = cond ? 1 : 0, sg = stage && xcd ? 1 : 0;
         if (L != kTopL) {  // the overlap's single-shard lists: 16-bit keys, not pruned (ks_engine.cpp)
             if (!key16 || prune || L != kTopLOverlap) return hipErrorInvalidValue;
-            launch_scan_t<uint16_t, false, kTopLOverlap>(d, g, lds, mode, x, c, sg, st);
+            launch_scan_t<uint16_t, false, kTopLOverlap>(d, g, lds, mode, x, c, sg, pw > 0 ? 1 : 0, st);
         } else if (key16) {
-            if (prune) launch_scan_t<uint16_t, true, kTopL>(d, g, lds, mode, x, c, sg, st);
-            else launch_scan_t<uint16_t, false, kTopL>(d, g, lds, mode, x, c, sg, st);
+            if (prune) launch_scan_t<uint16_t, true, kTopL>(d, g, lds, mode, x, c, sg, pw > 0 ? 1 : 0, st);
+            else launch_scan_t<uint16_t, false, kTopL>(d, g, lds, mode, x, c, sg, pw > 0 ? 1 : 0, st);
         } else {
-            if (prune) launch_scan_t<uint32_t, true, kTopL>(d, g, lds, mode, x, c, sg, st);
-            else launch_scan_t<uint32_t, false, kTopL>(d, g, lds, mode, x, c, sg, st);
+            if (prune) launch_scan_t<uint32_t, true, kTopL>(d, g, lds, mode, x, c, sg, pw > 0 ? 1 : 0, st);
+            else launch_scan_t<uint32_t, false, kTopL>(d, g, lds, mode, x, c, sg, pw > 0 ? 1 : 0, st);
         }
     }
     return hipGetLastError();
@@ -1160,13 +1175,13 @@ hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int
 
 hipError_t launch_merge(const EngineArgs* d, int S, int B, const uint64_t* lists, int64_t pod_stride, int32_t nl,
                         int64_t list_stride, uint64_t* out, int nl_max, hipStream_t st, const uint64_t* bits,
-                        int32_t nwl, int32_t blk0) {
+                        int32_t nwl, int32_t blk0, int32_t lset_fixed) {
     if ((int64_t)nl_max * kL <= kWave && !bits)
         hipLaunchKernelGGL(merge_small_kernel, dim3((B + 3) / 4, S), dim3(256), 0, st, d, lists, pod_stride, nl,
                            list_stride, out);
     else
         hipLaunchKernelGGL(merge_kernel, dim3(B, S), dim3(nl_max > 1024 ? 1024 : 256), 0, st, d, lists, pod_stride, nl,
-                           list_stride, out, bits, nwl, blk0);
+                           list_stride, out, bits, nwl, blk0, lset_fixed);
     return hipGetLastError();
 }
 

@@ -76,7 +76,8 @@ __device__ __forceinline__ void prep_body(const EngineArgs& a, int64_t start, in
     if (err != 0 || nb <= 0) {
         if (tid == 0) {
             ws.nb = 0; ws.e_cnt = 0; ws.n_e = 0; ws.n_es = 0; ws.rescan = 0; ws.lset = 1;
-            spec_out[kCtrStart] = end; spec_out[kCtrEnd] = end; spec_out[kCtrErr] = 0;
+            ws.split = 0; ws.moff = 0; ws.mpar = slot;
+            spec_out[kCtrStart] = end; spec_out[kCtrEnd] = end; spec_out[kCtrErr] = 0; spec_out[kSpecPrev] = start;
         }
         return;
     }
@@ -90,7 +91,17 @@ __device__ __forceinline__ void prep_body(const EngineArgs& a, int64_t start, in
     const int64_t myoff = tid < nb ? a.exp_off[start + tid + 1] : 0;
     const int64_t mypos = tid < nb ? a.exp_pos[start + tid] : 0;
     const int64_t sp_start = spec ? spec_in[kCtrStart] : 0;
+    const int64_t prev_start = spec ? spec_in[kSpecPrev] : 0;
     const int n_touched = spec ? ws.n_touched : 0;
+    // the previous batch's E (its nodes join this batch's E when this batch reuses its lists)
+    const int n_eold = spec ? ws.n_e : 0;
+    constexpr int kOPer = (kEMax + NT - 1) / NT;
+    int32_t eold[kOPer];
+#pragma unroll
+    for (int q = 0; q < kOPer; ++q) {
+        const int t = tid + q * NT;
+        eold[q] = spec && t < kEMax ? ws.e_node[t] : -1;
+    }
     constexpr int kTPer = (kTouchMax + NT - 1) / NT;
     int32_t tch[kTPer];
 #pragma unroll
@@ -105,8 +116,14 @@ __device__ __forceinline__ void prep_body(const EngineArgs& a, int64_t start, in
     nb = __syncthreads_count(fits_win);  // exp_off is non-decreasing: a prefix of the pods
     PDG_AT(0, pt);
     const int e_cnt = (int)(L.off[nb - 1] - e_base);  // exp_off[start + nb] - e_base (nb >= 1: pod 0 fits)
+    // reuse: the previous batch stopped early (this batch starts inside it): its unbound pods keep
+    // the merged lists merge_cl kept for them, the rest take the speculative scan's (which covered
+    // the pods after the previous batch) — no rescan.  Every node changed since either scan read the
+    // table is in the previous batch's E or was changed by that batch (touched) or this batch's head.
+    const bool reuse = spec && start != sp_start && start > prev_start && start < sp_start;
     int rescan = 0;
-    if (spec) rescan = start != sp_start || (int64_t)e_cnt + (e1 - e0) + n_touched > kEMax;
+    if (spec) rescan = (start != sp_start && !reuse) ||
+                       (int64_t)e_cnt + (e1 - e0) + n_touched + (reuse ? n_eold : 0) > kEMax;
     const bool touch = spec && !rescan;
     const int32_t hq = head && tid < e1 - e0 ? a.exp_pod[e0 + tid] : -1;
     const int32_t wq = tid < e_cnt ? a.exp_pod[e_base + tid] : -1;
@@ -148,6 +165,11 @@ __device__ __forceinline__ void prep_body(const EngineArgs& a, int64_t start, in
 #pragma unroll
         for (int q = 0; q < kTPer; ++q)
             if (tid + q * NT < n_touched) L.xn[atomicAdd(&L.s_nx, 1)] = tch[q];
+        if (reuse) {
+#pragma unroll
+            for (int q = 0; q < kOPer; ++q)
+                if (tid + q * NT < n_eold) L.xn[atomicAdd(&L.s_nx, 1)] = eold[q];
+        }
     }
     if (tid < nb) {
         ws.win_hi[tid] = tid >= 1 ? (int32_t)(myoff - e_base) : 0;
@@ -236,8 +258,12 @@ __device__ __forceinline__ void prep_body(const EngineArgs& a, int64_t start, in
     if (tid == 0) {
         ws.nb = nb; ws.e_cnt = e_cnt; ws.n_e = n_e; ws.n_es = n_es; ws.nslot = 0; ws.rescan = rescan;
         ws.lset = touch ? 0 : 1;  // pruned lists: the speculative scan's set, or the engine's own scan's
+        ws.split = touch && reuse ? (int32_t)(sp_start - start) : 0;
+        ws.moff = (int32_t)(start - prev_start);
+        ws.mpar = slot;
         // the next speculative scan: the pods after this batch, if it commits them all
         spec_out[kCtrStart] = start + nb; spec_out[kCtrEnd] = end; spec_out[kCtrErr] = 0;
+        spec_out[kSpecPrev] = start;
     }
     PDG(__syncthreads(); PDG_AT(6, pt); if (tid == 0) atomicAdd((unsigned long long*)&a.ctr[23], 1ull);)
 }

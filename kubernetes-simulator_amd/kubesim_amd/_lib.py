@@ -81,7 +81,10 @@ class KsKernelStats(C.Structure):
     _fields_ = [("prep_ms", C.c_double), ("scan_ms", C.c_double), ("merge_ms", C.c_double),
                 ("resolve_ms", C.c_double), ("fused_ms", C.c_double), ("part_ms", C.c_double),
                 ("xchg_ms", C.c_double), ("prep_n", C.c_int64), ("scan_n", C.c_int64), ("merge_n", C.c_int64),
-                ("resolve_n", C.c_int64), ("fused_n", C.c_int64), ("xchg_n", C.c_int64)]
+                ("resolve_n", C.c_int64), ("fused_n", C.c_int64), ("xchg_n", C.c_int64),
+                ("side_scan_ms", C.c_double), ("side_part_ms", C.c_double), ("side_xchg_ms", C.c_double),
+                ("wait_ms", C.c_double), ("side_n", C.c_int64),
+                ("usage_ms", C.c_double), ("usage_n", C.c_int64), ("usage_pods", C.c_int64)]
 
 
 class KsPods(C.Structure):

@@ -12,7 +12,8 @@ def win_dtype():
         ("cl_key", "u8", (B, R)), ("cl_info", "i4", B), ("cl_thr", "u8", B), ("cl_slot", "i4", (B, R)),
         ("nslot", "i4"), ("nslot_hw", "i4"), ("slot_node", "i4", B * R), ("slot_eix", "i4", 1536),
         ("slot_rec", "u4", (1536, 20)), ("touched", "i4", B + S), ("n_touched", "i4"), ("rescan", "i4"),
-        ("lset", "i4"), ("pad_", "i4"),
+        ("lset", "i4"), ("pad_", "i4"), ("split", "i4"), ("moff", "i4"), ("mpar", "i4"), ("pad2_", "i4"),
+        ("mrg", "u8", (2, B, 12)),
         ("blog_n", "i4"), ("watch_pod", "i4"), ("watch_done", "i4"), ("wpad_", "i4"), ("blog", "i4", (16384, 4)),
         ("w_start", "i4"), ("w_nb", "i4"), ("w_c", "i4"), ("w_n_e", "i4"), ("w_n_es", "i4"), ("w_pad", "i4", 3),
         ("w_cl_key", "u8", (B, R)), ("w_cl_info", "i4", B), ("w_cl_thr", "u8", B), ("w_e_node", "i4", E),
