@@ -300,12 +300,13 @@ ks_status ks_last_step_kernels(const ks_engine* eng, ks_kernel_stats* out);
 ks_status ks_group_step(ks_group* g, int64_t ticks, ks_bind* out, int64_t cap, int64_t* n_out,
                         int32_t* status_out, ks_step_stats* stats);
 /* Device counters (diagnostics): [0] next pod, [1] step end, [2] error, [3] error pod,
- * [4] batches that committed early (top-L list exhausted), [16..31] resolver phase cycle
+ * [4] batches that committed early (top-L list exhausted), [5] / [6] batches whose lists were
+ * rescanned / reused from the previous batch (cumulative, chunk resolver), [16..31] resolver phase cycle
  * sums in a -DKS_STAMPS diagnostic build (tests/dev/diag_resolve.py). */
 ks_status ks_debug_counters(ks_engine* eng, int64_t* out32);
 /* Between-step invariants of a chunk-resolver engine (diagnostics / regression tests): out4[0] =
- * nodes whose candidate-slot mark is set (must be 0: every batch's commit resets the marks of every
- * node its merge claimed), out4[1] = nodes whose E-index mark is set (must be 0), out4[2] = the most
+ * nodes whose candidate-slot or first-entry mark is set (must be 0: every batch's commit resets the
+ * marks of every node its merge claimed), out4[1] = nodes whose E-index mark is set (must be 0), out4[2] = the most
  * candidate slots any batch claimed so far, out4[3] = the slots whose records are staged (beyond
  * them a batch is cut before the first pod that needs one).  All 0 before the first batch. */
 ks_status ks_debug_invariants(ks_engine* eng, int64_t* out4);

@@ -158,6 +158,9 @@ __device__ __forceinline__ void cand_list(const EngineArgs& a, WinWS& ws, int i,
         NodeV rec{};
         int32_t eix = -1;
         if (valid) { rec = load_node(a.s, nd); eix = a.e_idx[nd]; }
+        // the node's first kept entry in pod order (the chunk kernel numbers the batch's candidates by
+        // it: deterministic ids, so every rank cuts a batch at the same pod)
+        if (valid && a.det_cids) atomicMin(&a.n_first[nd], i * kR + lane);
         int sl = valid ? atomicCAS(&a.n_slot[nd], -1, kSlotPending) : 0;
         const bool claim = valid && sl == -1;
         const uint64_t cm = __ballot(claim);

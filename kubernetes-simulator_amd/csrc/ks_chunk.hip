@@ -35,7 +35,7 @@ constexpr int kC = 64;          // pods per chunk: one lane each
 constexpr int kR = kChR;        // static candidates kept per pod
 constexpr int kCid = 1024;      // candidate ids per batch (the batch's candidate slots)
 constexpr int kMaxPGScan = 32;  // pods per scan group (the host's PG bound, ks_kernels.hip kMaxPG)
-constexpr int kCidSlots = kCid - kR;  // slots that are cids; the rest: pod 0's private cids
+constexpr int kCidSlots = kCid - kR;  // claim-order cids: slots that are cids; the rest: pod 0's private cids
 constexpr int kSlots = kWinSlots;
 constexpr int kSeg = 5;         // stored state segments per replayed node within a chunk
 constexpr int kPend = 4;        // pending own expiries per replayed node
@@ -413,14 +413,20 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
     if (err0 != 0 || nb <= 0) return;
     const int n_e = ws.n_es, n_eall = ws.n_e, e_cnt = ws.e_cnt;  // (n_e: the slot-E nodes)
 
-    // ---- setup: pods, window, candidate ids, records.  The candidate ids are the batch's
-    // candidate slots (ks_cand.hip cand_list: one per distinct node of the lists, claimed through
-    // node_slot, its record staged): slots < kCidSlots are cids; a pod with an entry on a later slot
-    // cuts the batch before it — except pod 0, whose entries there take the private cids
-    // kCidSlots + r (its record read here), so every launch binds at least one pod.
+    // ---- setup: pods, window, candidate ids, records.  The candidate ids (cids) number the batch's
+    // distinct candidate nodes in the order of their first kept entry (pod-major: merge_cl's
+    // n_first, ks_cand.hip cand_list) — deterministic, so every rank of a sharded engine cuts a batch
+    // at the same pod (round 6: the claim-order slot ids made the cut timing-dependent, and ranks
+    // that cut differently issued different numbers of exchanges).  A pod with an entry whose cid is
+    // >= kCid cuts the batch before it (never pod 0: its entries are the first cids).  Each cid's
+    // record is its candidate slot's, staged by merge_cl (a direct read past the kCid staged slots).
     DG(uint64_t t_setup = dstamp(); uint64_t acc_cd = 0, acc_sw = 0, acc_fin = 0, acc_ph[4] = {0, 0, 0, 0}, acc_cs = 0, acc_rb = 0, acc_cdp = 0, acc_rbase = 0, acc_red = 0, acc_crep = 0; int n_sweeps = 0, n_sonly = 0, n_chunks = 0;)
     const int nslot = ws.nslot < kWinMaxB * kR ? ws.nslot : kWinMaxB * kR;
-    const int nlo = nslot < kCidSlots ? nslot : kCidSlots;
+    // (det: first-appearance cids, every slot < kCid staged; otherwise the claim-order slots are the
+    // cids, slots >= kCidSlots cut the batch and pod 0 takes private cids there)
+    const bool det = a.det_cids != 0;
+    const int ncap = det ? kCid : kCidSlots;
+    const int nlo = nslot < ncap ? nslot : ncap;
     // (1) every global read of the setup issued before any is used: one round trip (the lists and
     // records were written by other workgroups, on other XCDs — each dependent read is a fabric
     // round trip)
@@ -447,7 +453,7 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
     int32_t eo[2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) eo[q] = tid + q * kThreads <= n_e ? ws.e_off[tid + q * kThreads] : 0;
-    static_assert(kCidSlots <= 2 * kThreads, "two slot records per thread");
+    static_assert(kCid <= 2 * kThreads, "two slot records per thread");
     int32_t snd[2], sex[2];
     uint4 srec[2][3];
 #pragma unroll
@@ -487,6 +493,15 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
         sh.smeta[tid][kMCid] = -1;
         sh.code[0][tid] = 0; sh.code[1][tid] = 0;
     }
+    // cid numbering scratch in the (idle until the sweeps) segment states: per pod the mask of its
+    // first-appearance entries and their pod-prefix count; slot -> cid
+    uint32_t* omask = reinterpret_cast<uint32_t*>(&sh.sst[0][0][0]);
+    int32_t* opre = reinterpret_cast<int32_t*>(omask + kB);
+    int16_t* sc = reinterpret_cast<int16_t*>(opre + kB + 4);
+    static_assert(sizeof(sh.sst) >= (2 * kB + 4) * 4 + kSlotIds * 2, "cid numbering scratch");
+    if (tid < kB) omask[tid] = 0;
+    if (det)
+        for (int k = tid; k < nlo; k += kThreads) sc[k] = -1;
     // slot x's request words, staged in the cache buffer (idle until the first chunk's cache)
     int32_t (*xtmp)[4] = reinterpret_cast<int32_t (*)[4]>(&sh.x.k[0][0][0]);
     static_assert(sizeof(sh.x.k) >= kSlots * 4 * sizeof(int32_t), "slot request staging");
@@ -502,44 +517,134 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
     for (int k = tid; k < kCid; k += kThreads) { sh.ceix[k] = -1; sh.cnode[k] = -1; }
     __syncthreads();
     DG(uint64_t ts1 = dstamp();)
-    // slot i is applied from the first pod i >= 1 with win_hi[i] > x
-    for (int i = tid + 1; i < nb; i += kThreads)
-        for (int x = sh.win_hi[i - 1]; x < sh.win_hi[i]; ++x) sh.xeff[x] = (int16_t)i;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {  // slot records; the other cids inert
-        const int k = tid + q * kThreads;
-        if (k < nlo) {
-            sh.cnode[k] = snd[q];
-            sh.ceix[k] = (int16_t)sex[q];
-            if (sex[q] >= 0) sh.e2c[sex[q]] = (int16_t)k;
-            store_prec(sh, k, srec[q]);
+    if (det) {
+        // (3) each kept entry's node's first entry (a dependent read: the lists' nodes), then the owners
+        // (first-appearance entries) per pod
+        int32_t fe[kEntPer];
+    #pragma unroll
+        for (int q = 0; q < kEntPer; ++q) {
+            const int idx = tid + q * kThreads, i = idx / kR, r = idx % kR;
+            const bool v = i < nb && r < sh.clcnt[i];
+            fe[q] = v ? a.n_first[key_node(ekey[q])] : kNoFirst;
         }
-    }
-    for (int k = tid; k < kCid; k += kThreads)
-        if (k >= nlo) store_book(sh, k);
-#pragma unroll
-    for (int q = 0; q < kEntPer; ++q) {
-        const int idx = tid + q * kThreads, i = idx / kR, r = idx % kR;
-        if (i >= nb || r >= sh.clcnt[i] || eslt[q] < 0) continue;
-        const uint64_t key = ekey[q];
-        const int sl = eslt[q];
-        int cid = sl;
-        if (sl >= kCidSlots) {
-            if (i > 0) { atomicMin(&sh.nbc, i); continue; }
-            cid = kCidSlots + r;  // pod 0's private cid
-            const int32_t nd = key_node(key);
-            int ex = a.e_idx[nd];
-            if (ex >= n_e) ex = -1;  // (an E node without slots)
-            sh.cnode[cid] = nd;
-            sh.ceix[cid] = (int16_t)ex;
-            if (ex >= 0) sh.e2c[ex] = (int16_t)cid;
-            const NodeV v = load_node(a.s, nd);
-            const uint4 rr[3] = {make_uint4((uint32_t)v.ac, (uint32_t)v.am, (uint32_t)v.ag, (uint32_t)clamp32(v.ap)),
-                                 make_uint4((uint32_t)v.rc, (uint32_t)v.rm, (uint32_t)v.rg, (uint32_t)v.nr),
-                                 make_uint4((uint32_t)v.taint, (uint32_t)(v.taint >> 32), (uint32_t)v.label, (uint32_t)(v.label >> 32))};
-            store_prec(sh, cid, rr);
+        // slot i is applied from the first pod i >= 1 with win_hi[i] > x
+        for (int i = tid + 1; i < nb; i += kThreads)
+            for (int x = sh.win_hi[i - 1]; x < sh.win_hi[i]; ++x) sh.xeff[x] = (int16_t)i;
+    #pragma unroll
+        for (int q = 0; q < kEntPer; ++q) {
+            const int idx = tid + q * kThreads;
+            if (fe[q] == idx) atomicOr(&omask[idx / kR], 1u << (idx % kR));
         }
-        sh.cl[i][r] = ((uint32_t)cid << 16) | (uint32_t)(key >> 32);
+        __syncthreads();
+        if (wave == 0) {  // exclusive prefix of the pods' owner counts (four pods per lane)
+            int c[4], sum = 0;
+    #pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = lane * 4 + u;
+                c[u] = i < nb ? __popc(omask[i]) : 0;
+                sum += c[u];
+            }
+            int incl = sum;
+    #pragma unroll
+            for (int o = 1; o < kWave; o <<= 1) {
+                const int v = __shfl_up(incl, o);
+                if (lane >= o) incl += v;
+            }
+            int run = incl - sum;
+    #pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                opre[lane * 4 + u] = run;
+                run += c[u];
+            }
+        }
+        static_assert(kB == 4 * kWave, "four pods per lane");
+        __syncthreads();
+        // (4) every entry's cid: its node's first entry's rank in pod-major order; owners map their slot
+        // to it (the slot records below) or, past the staged slots, read the node directly
+    #pragma unroll
+        for (int q = 0; q < kEntPer; ++q) {
+            const int idx = tid + q * kThreads, i = idx / kR, r = idx % kR;
+            if (fe[q] == kNoFirst) continue;
+            const int f = fe[q], fi = f / kR, fr = f % kR;
+            const int cid = opre[fi] + __popc(omask[fi] & ((1u << fr) - 1u));
+            if (cid >= kCid) { atomicMin(&sh.nbc, i); continue; }  // (i > 0: pod 0's entries are cids < kR)
+            const uint64_t key = ekey[q];
+            sh.cl[i][r] = ((uint32_t)cid << 16) | (uint32_t)(key >> 32);
+            if (f != idx) continue;
+            const int sl = eslt[q];
+            if (sl >= 0 && sl < nlo) {
+                sc[sl] = (int16_t)cid;
+            } else {  // (a slot past the staged records: the node read here)
+                const int32_t nd = key_node(key);
+                int ex = a.e_idx[nd];
+                if (ex >= n_e) ex = -1;  // (an E node without slots)
+                sh.cnode[cid] = nd;
+                sh.ceix[cid] = (int16_t)ex;
+                if (ex >= 0) sh.e2c[ex] = (int16_t)cid;
+                const NodeV v = load_node(a.s, nd);
+                const uint4 rr[3] = {make_uint4((uint32_t)v.ac, (uint32_t)v.am, (uint32_t)v.ag, (uint32_t)clamp32(v.ap)),
+                                     make_uint4((uint32_t)v.rc, (uint32_t)v.rm, (uint32_t)v.rg, (uint32_t)v.nr),
+                                     make_uint4((uint32_t)v.taint, (uint32_t)(v.taint >> 32), (uint32_t)v.label, (uint32_t)(v.label >> 32))};
+                store_prec(sh, cid, rr);
+            }
+        }
+        __syncthreads();
+        const int n_cid = opre[kB - 1] + __popc(omask[kB - 1]) < kCid ? opre[kB - 1] + __popc(omask[kB - 1]) : kCid;
+    #pragma unroll
+        for (int q = 0; q < 2; ++q) {  // the staged slot records at their cids; the other cids inert
+            const int k = tid + q * kThreads;
+            if (k < nlo) {
+                const int c = sc[k];
+                if (c >= 0 && c < kCid) {
+                    sh.cnode[c] = snd[q];
+                    sh.ceix[c] = (int16_t)sex[q];
+                    if (sex[q] >= 0) sh.e2c[sex[q]] = (int16_t)c;
+                    store_prec(sh, c, srec[q]);
+                }
+            }
+        }
+        for (int k = tid; k < kCid; k += kThreads)
+            if (k >= n_cid) store_book(sh, k);
+    } else {
+        // claim-order cids (one engine: its batching may depend on claim timing — results do not)
+        for (int i = tid + 1; i < nb; i += kThreads)
+            for (int x = sh.win_hi[i - 1]; x < sh.win_hi[i]; ++x) sh.xeff[x] = (int16_t)i;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {  // slot records; the other cids inert
+            const int k = tid + q * kThreads;
+            if (k < nlo) {
+                sh.cnode[k] = snd[q];
+                sh.ceix[k] = (int16_t)sex[q];
+                if (sex[q] >= 0) sh.e2c[sex[q]] = (int16_t)k;
+                store_prec(sh, k, srec[q]);
+            }
+        }
+        for (int k = tid; k < kCid; k += kThreads)
+            if (k >= nlo) store_book(sh, k);
+#pragma unroll
+        for (int q = 0; q < kEntPer; ++q) {
+            const int idx = tid + q * kThreads, i = idx / kR, r = idx % kR;
+            if (i >= nb || r >= sh.clcnt[i] || eslt[q] < 0) continue;
+            const uint64_t key = ekey[q];
+            const int sl = eslt[q];
+            int cid = sl;
+            if (sl >= kCidSlots) {
+                if (i > 0) { atomicMin(&sh.nbc, i); continue; }
+                cid = kCidSlots + r;  // pod 0's private cid
+                const int32_t nd = key_node(key);
+                int ex = a.e_idx[nd];
+                if (ex >= n_e) ex = -1;  // (an E node without slots)
+                sh.cnode[cid] = nd;
+                sh.ceix[cid] = (int16_t)ex;
+                if (ex >= 0) sh.e2c[ex] = (int16_t)cid;
+                const NodeV v = load_node(a.s, nd);
+                const uint4 rr[3] = {make_uint4((uint32_t)v.ac, (uint32_t)v.am, (uint32_t)v.ag, (uint32_t)clamp32(v.ap)),
+                                     make_uint4((uint32_t)v.rc, (uint32_t)v.rm, (uint32_t)v.rg, (uint32_t)v.nr),
+                                     make_uint4((uint32_t)v.taint, (uint32_t)(v.taint >> 32), (uint32_t)v.label, (uint32_t)(v.label >> 32))};
+                store_prec(sh, cid, rr);
+            }
+            sh.cl[i][r] = ((uint32_t)cid << 16) | (uint32_t)(key >> 32);
+        }
     }
     __syncthreads();
     nb = sh.nbc < nb ? sh.nbc : nb;
@@ -1156,8 +1261,15 @@ __device__ __forceinline__ void chunk_body(const EngineArgs* __restrict__ A, ChS
         if (tid + q * kThreads < n_eall) a.e_idx[enode[q]] = -1;
 #pragma unroll
     for (int q = 0; q < 2; ++q)
-        if (tid + q * kThreads < nlo) a.n_slot[snd[q]] = -1;
-    for (int k = nlo + tid; k < nslot; k += kThreads) a.n_slot[ws.slot_node[k]] = -1;
+        if (tid + q * kThreads < nlo) {
+            a.n_slot[snd[q]] = -1;
+            if (det) a.n_first[snd[q]] = kNoFirst;
+        }
+    for (int k = nlo + tid; k < nslot; k += kThreads) {
+        const int32_t nd = ws.slot_node[k];
+        a.n_slot[nd] = -1;
+        if (det) a.n_first[nd] = kNoFirst;
+    }
     // the nodes this batch changed — its binds' nodes (every cid with a final bind) and its window's
     // expiry nodes — for the next batch's overlapped scan (ks_cand.hip window_prep_kernel)
     {

@@ -663,7 +663,9 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 }
 
 // ctr[] slots of a batch (EngineArgs::ctr), pod flags the resolvers stop on, error codes
-enum : int64_t { kCtrStart = 0, kCtrEnd = 1, kCtrErr = 2, kCtrErrPod = 3, kCtrEarly = 4 };
+// (5, 6: cumulative counts of the window prep's rescans and list reuses — diagnostic builds use
+// ctr[5..31] for their own counters)
+enum : int64_t { kCtrStart = 0, kCtrEnd = 1, kCtrErr = 2, kCtrErrPod = 3, kCtrEarly = 4, kCtrRescan = 5, kCtrReuse = 6 };
 enum : uint32_t { kFlagBadKey = 1, kFlagBadSpec = 2 };
 enum : int64_t { kErrEinval = 1, kErrNotFound = 2 };
 
@@ -682,6 +684,7 @@ constexpr int kSlotMax = 1536;  // candidate slots whose record / E index merge_
 // claims a batch can make: every kept entry of every pod (slot_node holds each one, so the commit
 // can reset node_slot for every claimed node — the slots past kSlotMax included)
 constexpr int kSlotIds = kWinMaxB * kChR;
+constexpr int32_t kNoFirst = 0x7F7F7F7F;  // (a byte-filled memset value above every entry index)
 constexpr int kEMax = 2048;     // E nodes per batch: the window's expiry nodes + the overlap's touched nodes
 constexpr int kTouchMax = kWinMaxB + kWinSlots;
 constexpr int kSpecStride = 8;  // int64 counters per speculative set
@@ -776,6 +779,8 @@ struct EngineArgs {
     WinWS* sw;               // batch window workspace (nullptr unless allocated)
     int32_t* e_idx;          // [n_pad] node -> index in the window's E, -1 otherwise
     int32_t* n_slot;         // [n_pad] node -> its candidate slot in this batch, -1 otherwise
+    int32_t* n_first;        // [n_pad] node -> its first kept entry (pod * kChR + rank) in this batch,
+                             // kNoFirst otherwise (ks_cand.hip cand_list, ks_chunk.hip setup)
     int64_t* spec_ctr;       // the speculative scan's counters, two sets of kSpecStride (window prep
                              // writes: the next batch if this one commits all its pods)
     // pruned block lists (ks_scan.h; nullptr: every block writes its whole list): per pod a bitmap of
@@ -788,6 +793,9 @@ struct EngineArgs {
     uint64_t* lthr;
     int32_t nwl;             // bitmap words per pod: ceil(nblk / 64)
     int32_t lset;            // the set this argument record's scans write
+    int32_t det_cids;        // chunk resolver: number the candidates by first appearance (sharded engines:
+                             // every rank must cut its batches at the same pods), not by claim order
+    int32_t pad3_;
     const ScanRec* srec;     // [P] the pods' scan records (the micro evaluator's scan form)
 };
 // pruned lists: pod b's bitmap / threshold in set `set`
@@ -825,9 +833,10 @@ hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int
 // bits (pruned lists, ks_scan.h; nullptr: read every list): the pods' bitmaps ([B][nwl]); list k of
 // the range is block blk0 + k
 // lset_fixed >= 0: read that list set's bitmaps (not the window's WinWS::lset)
+// L: the lists' length (kTopL, or kTopLOverlap for the pipelined sharded engines' part merges)
 hipError_t launch_merge(const EngineArgs* d, int S, int B, const uint64_t* lists, int64_t pod_stride, int32_t nl,
                         int64_t list_stride, uint64_t* out, int nl_max, hipStream_t st, const uint64_t* bits = nullptr,
-                        int32_t nwl = 0, int32_t blk0 = 0, int32_t lset_fixed = -1);
+                        int32_t nwl = 0, int32_t blk0 = 0, int32_t lset_fixed = -1, int L = kTopL);
 // the role-split resolver (ks_kernels.hip): batches of up to max_batch_pods() pods, any cluster
 hipError_t launch_resolve(const EngineArgs* d, int S, int mode, hipStream_t st);
 // the register-table resolver (ks_resolve.hip): batches of <= small_resolver_max_batch() pods of

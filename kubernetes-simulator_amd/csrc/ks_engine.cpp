@@ -248,6 +248,7 @@ struct ks_engine {
     ks::WinWS* d_sweep = nullptr;    // batch window workspace and node -> E index (n_pad, -1)
     int32_t* d_eidx = nullptr;
     int32_t* d_nslot = nullptr;      // node -> candidate slot of the batch (ks_cand.hip), -1
+    int32_t* d_first = nullptr;      // node -> its first kept entry of the batch, kNoFirst
     unsigned long long* d_usage = nullptr;
     DVec<int32_t> d_blk;                  // usage query: candidate pod blocks
     std::vector<int32_t> h_blk;
@@ -306,6 +307,8 @@ ks::EngineArgs make_args(ks_engine* e) {
     a.sw = e->d_sweep;
     a.e_idx = e->d_eidx;
     a.n_slot = e->d_nslot;
+    a.n_first = e->d_first;
+    a.det_cids = e->world * e->vsh > 1 ? 1 : 0;
     a.spec_ctr = e->d_spec;
     a.lbit = e->prune ? e->lbit : nullptr;
     a.lthr = e->prune ? e->lthr : nullptr;
@@ -563,6 +566,7 @@ void engine_free(ks_engine* e) {
     if (e->d_sweep) (void)hipFree(e->d_sweep);
     if (e->d_eidx) (void)hipFree(e->d_eidx);
     if (e->d_nslot) (void)hipFree(e->d_nslot);
+    if (e->d_first) (void)hipFree(e->d_first);
     if (e->d_spec) (void)hipFree(e->d_spec);
     if (e->d_args_spec) (void)hipFree(e->d_args_spec);
     if (e->h_args_spec) (void)hipHostFree(e->h_args_spec);
@@ -738,11 +742,12 @@ ks_status ks_load_nodes(ks_engine* e, int64_t n, const int64_t* alloc, const uin
         pg *= 2;
     e->PG = pg;
     // (the overlap's single-shard engines may scan lists of kTopLOverlap keys: step_body)
-    const int lmax = G == 1 && e->blk_n <= kOverlapMaxBlocks ? ks::kTopLOverlap : ks::kTopL;
+    // (and the pipelined sharded engines': every sharded engine may)
+    const int lmax = (G == 1 && e->blk_n <= kOverlapMaxBlocks) || G > 1 ? ks::kTopLOverlap : ks::kTopL;
     HIPCHK(e, hipMalloc(&e->lists, sizeof(uint64_t) * (size_t)e->B * e->nblk * lmax));
     HIPCHK(e, hipMalloc(&e->cand, sizeof(uint64_t) * (size_t)e->B * ks::kTopL));
-    if (G > 1) HIPCHK(e, hipMalloc(&e->cand_all, sizeof(uint64_t) * (size_t)G * e->B * ks::kTopL));
-    if (G > 1 && e->xfn) HIPCHK(e, hipHostMalloc(&e->h_xbuf, sizeof(uint64_t) * (size_t)G * e->B * ks::kTopL, hipHostMallocDefault));
+    if (G > 1) HIPCHK(e, hipMalloc(&e->cand_all, sizeof(uint64_t) * (size_t)G * e->B * ks::kTopLOverlap));
+    if (G > 1 && e->xfn) HIPCHK(e, hipHostMalloc(&e->h_xbuf, sizeof(uint64_t) * (size_t)G * e->B * ks::kTopLOverlap, hipHostMallocDefault));
     HIPCHK(e, hipMalloc(&e->d_mask, std::max<int64_t>(n, 1)));
     HIPCHK(e, hipMalloc(&e->d_score, sizeof(int64_t) * std::max<int64_t>(n, 1)));
     HIPCHK(e, hipMalloc(&e->d_usage, sizeof(unsigned long long) * 3 * std::max<int64_t>(n, 1)));
@@ -1193,6 +1198,8 @@ static ks_status ensure_window_ws(ks_engine* e) {
     HIPCHK(e, hipMemsetAsync(e->d_eidx, 0xFF, sizeof(int32_t) * e->n_pad, e->st));
     HIPCHK(e, hipMalloc(&e->d_nslot, sizeof(int32_t) * e->n_pad));
     HIPCHK(e, hipMemsetAsync(e->d_nslot, 0xFF, sizeof(int32_t) * e->n_pad, e->st));
+    HIPCHK(e, hipMalloc(&e->d_first, sizeof(int32_t) * e->n_pad));
+    HIPCHK(e, hipMemsetAsync(e->d_first, 0x7F, sizeof(int32_t) * e->n_pad, e->st));  // kNoFirst
     HIPCHK(e, hipMalloc(&e->d_spec, 2 * ks::kSpecStride * sizeof(int64_t)));
     HIPCHK(e, hipMemsetAsync(e->d_spec, 0, 2 * ks::kSpecStride * sizeof(int64_t), e->st));
     HIPCHK(e, hipMalloc(&e->d_args_spec, 2 * sizeof(ks::EngineArgs)));
@@ -1219,13 +1226,13 @@ static ks_status ensure_window_ws(ks_engine* e) {
 // This rank's per-part merges of its block lists into its parts' slices of cand_all (a: the
 // argument record whose counters name the batch; lset_fixed >= 0: that list set's bitmaps)
 static hipError_t part_merges(ks_engine* e, const ks::EngineArgs* a, hipStream_t s, int lset_fixed) {
-    const int64_t L = ks::kTopL, BL = (int64_t)e->B * L;
+    const int64_t L = e->L, BL = (int64_t)e->B * L;
     for (int v = 0; v < e->vsh; v++) {
         const int p = e->rank * e->vsh + v;
         const int nlp = e->part_lo[p + 1] - e->part_lo[p];
         const hipError_t r = ks::launch_merge(a, 1, e->B, e->lists + (int64_t)e->part_lo[p] * L, (int64_t)e->nblk * L, nlp,
                                               L, e->cand_all + p * BL, nlp, s, e->prune ? e->lbit : nullptr, e->nwl,
-                                              e->part_lo[p], lset_fixed);
+                                              e->part_lo[p], lset_fixed, (int)L);
         if (r != hipSuccess) return r;
     }
     return hipSuccess;
@@ -1233,7 +1240,7 @@ static hipError_t part_merges(ks_engine* e, const ks::EngineArgs* a, hipStream_t
 
 // The all-gather of every rank's parts of cand_all on stream s: RCCL, or the host callback
 static ks_status exchange(ks_engine* e, hipStream_t s) {
-    const int64_t BL = (int64_t)e->B * ks::kTopL;
+    const int64_t BL = (int64_t)e->B * e->L;
     if (e->comm) {
         const ncclResult_t nr = ncclAllGather(e->cand_all + (int64_t)e->rank * e->vsh * BL, e->cand_all,
                                               (size_t)e->vsh * BL, ncclUint64, e->comm, s);
@@ -1261,7 +1268,7 @@ static ks_status pipe_batch(ks_engine* e, int64_t b, int64_t nbat, hipEvent_t* e
     hipStream_t st = e->st, s2 = e->st2;
     const ks::EngineArgs* d = e->d_args;
     const int G = e->world * e->vsh;
-    const int64_t L = ks::kTopL, BL = (int64_t)e->B * L;
+    const int64_t L = e->L, BL = (int64_t)e->B * L;  // (kTopLOverlap: step_body)
     const bool first = b == 0, more = b + 1 < nbat;
     if (ev[0]) HIPCHK(e, hipEventRecord(ev[0], st));
     if (first) {
@@ -1286,7 +1293,8 @@ static ks_status pipe_batch(ks_engine* e, int64_t b, int64_t nbat, hipEvent_t* e
     if (ev[3]) HIPCHK(e, hipEventRecord(ev[3], st));
     if (more) {
         HIPCHK(e, hipEventRecord(e->pev_m, st));
-        HIPCHK(e, ks::launch_chunk_scan(d, e->d_args_spec + (b & 1), 0, (int)((b + 1) & 1), e->mode, e->prune, (int)L, st));
+        // (no scan workers: the resolver and the next window only; the list length is the workers')
+        HIPCHK(e, ks::launch_chunk_scan(d, e->d_args_spec + (b & 1), 0, (int)((b + 1) & 1), e->mode, e->prune, ks::kTopL, st));
     } else {
         HIPCHK(e, ks::launch_chunk_only(d, e->mode, st));
     }
@@ -1348,7 +1356,8 @@ static ks_status step_body(ks_engine* e, int64_t ticks, ks_bind* out, int64_t ca
     // locally (no second exchange: every rank holds the whole table) and merge_cl merges those.
     const bool pipe = fused && !overlap && e->overlap && e->st2 && e->world * e->vsh > 1;
     // the overlap's single-shard lists are longer (ks_device.h kTopLOverlap, ks_cand.hip cand_list)
-    e->L = overlap && e->world * e->vsh == 1 && !e->prune ? ks::kTopLOverlap : ks::kTopL;
+    // (and the pipelined chain's: its speculative lists go stale like the overlap's)
+    e->L = (overlap && e->world * e->vsh == 1 && !e->prune) || pipe ? ks::kTopLOverlap : ks::kTopL;
     if (pipe) {
         *e->h_args_full = *e->h_args;
         e->h_args_full->blk_lo = 0;
@@ -2070,14 +2079,15 @@ ks_status ks_debug_invariants(ks_engine* e, int64_t* out4) {
     out4[0] = out4[1] = out4[2] = out4[3] = 0;
     if (!e->d_sweep) return KS_OK;  // (no chunk-resolver batch ran: nothing to check)
     HIPCHK(e, hipSetDevice(e->device));
-    std::vector<int32_t> ns(e->n_pad), ei(e->n_pad);
+    std::vector<int32_t> ns(e->n_pad), ei(e->n_pad), fi(e->n_pad);
     int32_t hw = 0;
     HIPCHK(e, hipMemcpyAsync(ns.data(), e->d_nslot, sizeof(int32_t) * e->n_pad, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(e, hipMemcpyAsync(fi.data(), e->d_first, sizeof(int32_t) * e->n_pad, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipMemcpyAsync(ei.data(), e->d_eidx, sizeof(int32_t) * e->n_pad, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipMemcpyAsync(&hw, &e->d_sweep->nslot_hw, sizeof hw, hipMemcpyDeviceToHost, e->st));
     HIPCHK(e, hipStreamSynchronize(e->st));
     for (int64_t i = 0; i < e->n_pad; i++) {
-        out4[0] += ns[i] != -1;
+        out4[0] += ns[i] != -1 || fi[i] != ks::kNoFirst;
         out4[1] += ei[i] != -1;
     }
     out4[2] = hw;

@@ -177,6 +177,8 @@ __global__ __launch_bounds__(256) void scan_kernel(const EngineArgs* __restrict_
 constexpr int kMergeMaxWaves = 16;
 // bits != nullptr (a pruned engine's per-part merge, ks_scan.h): only the blocks pod b's bitmap
 // bits[b * nwl ...] flags among blocks [blk0, blk0 + nl) (list k = block blk0 + k) are read
+// kLL: the lists' length (kTopL; kTopLOverlap for the pipelined sharded engines' per-part merges)
+template <int kLL>
 __global__ __launch_bounds__(1024) void merge_kernel(const EngineArgs* __restrict__ A, const uint64_t* src,
                                                       int64_t pod_stride, int32_t nl, int64_t list_stride,
                                                       uint64_t* out, const uint64_t* bits, int32_t nwl, int32_t blk0,
@@ -184,9 +186,9 @@ __global__ __launch_bounds__(1024) void merge_kernel(const EngineArgs* __restric
     const EngineArgs a = A[blockIdx.y];
     if (src == nullptr) {
         src = a.lists;
-        pod_stride = (int64_t)a.nblk * kL;
+        pod_stride = (int64_t)a.nblk * kLL;
         nl = a.nblk;
-        list_stride = kL;
+        list_stride = kLL;
         out = a.cand;
     }
     const int64_t start = a.ctr[kCtrStart], end = a.ctr[kCtrEnd];
@@ -195,9 +197,9 @@ __global__ __launch_bounds__(1024) void merge_kernel(const EngineArgs* __restric
     const int b = blockIdx.x;
     if (b >= nb) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint64_t top[kL];  // per-thread sorted (descending) top-L over its blocks
+    uint64_t top[kLL];  // per-thread sorted (descending) top-L over its blocks
 #pragma unroll
-    for (int k = 0; k < kL; ++k) top[k] = 0;
+    for (int k = 0; k < kLL; ++k) top[k] = 0;
     const uint64_t* lists = src + (int64_t)b * pod_stride;
     const int nthr = blockDim.x, nwav = nthr / kWave;
     __shared__ scn::FlagLDS F;
@@ -209,25 +211,25 @@ __global__ __launch_bounds__(1024) void merge_kernel(const EngineArgs* __restric
     const int nfl = bits ? scn::flagged_index(bits + ((int64_t)lset * a.B + b) * nwl, blk0, nl, F) : nl;
     for (int j = tid; j < nfl; j += nthr) {
         const int blk = bits ? scn::flagged_block(j, blk0, nl, F) : j;
-        // the whole list in one round trip (four 16-byte loads), then the insertions
+        // the whole list in one round trip (16-byte loads), then the insertions
         const ulonglong2* lp = reinterpret_cast<const ulonglong2*>(lists + (int64_t)blk * list_stride);
-        uint64_t lv[kL];
+        uint64_t lv[kLL];
 #pragma unroll
-        for (int k = 0; k < kL / 2; ++k) {
+        for (int k = 0; k < kLL / 2; ++k) {
             const ulonglong2 w = lp[k];
             lv[2 * k] = w.x;
             lv[2 * k + 1] = w.y;
         }
-        topl_insert(top, lv);
+        topl_insert<kLL>(top, lv);
     }
     // each wave: L rounds of its max thread head (the owner advances), no barrier; then wave 0
-    // merges the wave lists (<= 128 candidates, two per lane) the same way
-    __shared__ uint64_t wl[kMergeMaxWaves][kL];
+    // merges the wave lists (<= 16 x kLL candidates, kPer per lane) the same way
+    __shared__ uint64_t wl[kMergeMaxWaves][kLL];
     int head = 0;
-    for (int r = 0; r < kL; ++r) {
+    for (int r = 0; r < kLL; ++r) {
         uint64_t h = 0;
 #pragma unroll
-        for (int k = 0; k < kL; ++k) h = (k == head) ? top[k] : h;
+        for (int k = 0; k < kLL; ++k) h = (k == head) ? top[k] : h;
         const uint64_t m = wave_max_u64(h);
         const uint64_t hit = __ballot(h == m && m != 0);
         if (lane == 0) wl[wave][r] = m;
@@ -235,17 +237,29 @@ __global__ __launch_bounds__(1024) void merge_kernel(const EngineArgs* __restric
     }
     __syncthreads();
     if (wave != 0) return;
-    const int nc = nwav * kL;  // candidates: lane l holds c[l] and c[l + 64]
-    uint64_t v0 = lane < nc ? wl[lane / kL][lane % kL] : 0ull;
-    uint64_t v1 = lane + kWave < nc ? wl[(lane + kWave) / kL][(lane + kWave) % kL] : 0ull;
+    constexpr int kPer = (kMergeMaxWaves * kLL + kWave - 1) / kWave;
+    const int nc = nwav * kLL;
+    uint64_t v[kPer];
 #pragma unroll
-    for (int r = 0; r < kL; ++r) {
-        const uint64_t m = wave_max_u64(v0 > v1 ? v0 : v1);
-        if (lane == 0) out[(int64_t)b * kL + r] = m;
+    for (int q = 0; q < kPer; ++q) {
+        const int c = lane + q * kWave;
+        v[q] = c < nc ? wl[c / kLL][c % kLL] : 0ull;
+    }
+#pragma unroll
+    for (int r = 0; r < kLL; ++r) {
+        uint64_t lm = v[0];
+#pragma unroll
+        for (int q = 1; q < kPer; ++q) lm = lm > v[q] ? lm : v[q];
+        const uint64_t m = wave_max_u64(lm);
+        if (lane == 0) out[(int64_t)b * kLL + r] = m;
         if (m == 0) continue;
-        const uint64_t h0 = __ballot(v0 == m), h1 = __ballot(v1 == m);  // keys are distinct
-        if (h0 && lane == __ffsll((unsigned long long)h0) - 1) v0 = 0;
-        if (!h0 && h1 && lane == __ffsll((unsigned long long)h1) - 1) v1 = 0;
+        bool done = false;  // keys are distinct: exactly one holder
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            const uint64_t h = __ballot(!done && v[q] == m);
+            if (h && lane == __ffsll((unsigned long long)h) - 1) v[q] = 0;
+            done = done || h != 0;
+        }
     }
 }
 
@@ -1159,9 +1173,15 @@ hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int
         if (pw > 0 && S == 1) wgs = std::max<int64_t>(std::min<int64_t>(wgs, pw / 8 * 8), kStageWgs);  // (persistent)
         const dim3 g = xcd ? dim3((unsigned)wgs, 1, 1) : dim3(blk_n, groups, S);
         const int x = xcd ? 1 : 0, c = cond ? 1 : 0, sg = stage && xcd ? 1 : 0;
-        if (L != kTopL) {  // the overlap's single-shard lists: 16-bit keys, not pruned (ks_engine.cpp)
-            if (!key16 || prune || L != kTopLOverlap) return hipErrorInvalidValue;
-            launch_scan_t<uint16_t, false, kTopLOverlap>(d, g, lds, mode, x, c, sg, pw > 0 ? 1 : 0, st);
+        if (L != kTopL) {  // the overlap's single-shard lists and the pipelined sharded engines' (ks_engine.cpp)
+            if (L != kTopLOverlap) return hipErrorInvalidValue;
+            if (key16) {
+                if (prune) launch_scan_t<uint16_t, true, kTopLOverlap>(d, g, lds, mode, x, c, sg, pw > 0 ? 1 : 0, st);
+                else launch_scan_t<uint16_t, false, kTopLOverlap>(d, g, lds, mode, x, c, sg, pw > 0 ? 1 : 0, st);
+            } else {
+                if (prune) launch_scan_t<uint32_t, true, kTopLOverlap>(d, g, lds, mode, x, c, sg, pw > 0 ? 1 : 0, st);
+                else launch_scan_t<uint32_t, false, kTopLOverlap>(d, g, lds, mode, x, c, sg, pw > 0 ? 1 : 0, st);
+            }
         } else if (key16) {
             if (prune) launch_scan_t<uint16_t, true, kTopL>(d, g, lds, mode, x, c, sg, pw > 0 ? 1 : 0, st);
             else launch_scan_t<uint16_t, false, kTopL>(d, g, lds, mode, x, c, sg, pw > 0 ? 1 : 0, st);
@@ -1175,13 +1195,20 @@ hipError_t launch_scan(const EngineArgs* d, int S, int blk_n, int B, int PG, int
 
 hipError_t launch_merge(const EngineArgs* d, int S, int B, const uint64_t* lists, int64_t pod_stride, int32_t nl,
                         int64_t list_stride, uint64_t* out, int nl_max, hipStream_t st, const uint64_t* bits,
-                        int32_t nwl, int32_t blk0, int32_t lset_fixed) {
-    if ((int64_t)nl_max * kL <= kWave && !bits)
+                        int32_t nwl, int32_t blk0, int32_t lset_fixed, int L) {
+    const dim3 g(B, S), t(nl_max > 1024 ? 1024 : 256);
+    if (L == kTopLOverlap && L != kTopL) {
+        hipLaunchKernelGGL(merge_kernel<kTopLOverlap>, g, t, 0, st, d, lists, pod_stride, nl, list_stride, out, bits,
+                           nwl, blk0, lset_fixed);
+    } else if (L != kTopL) {
+        return hipErrorInvalidValue;
+    } else if ((int64_t)nl_max * kL <= kWave && !bits) {
         hipLaunchKernelGGL(merge_small_kernel, dim3((B + 3) / 4, S), dim3(256), 0, st, d, lists, pod_stride, nl,
                            list_stride, out);
-    else
-        hipLaunchKernelGGL(merge_kernel, dim3(B, S), dim3(nl_max > 1024 ? 1024 : 256), 0, st, d, lists, pod_stride, nl,
-                           list_stride, out, bits, nwl, blk0, lset_fixed);
+    } else {
+        hipLaunchKernelGGL(merge_kernel<kTopL>, g, t, 0, st, d, lists, pod_stride, nl, list_stride, out, bits, nwl, blk0,
+                           lset_fixed);
+    }
     return hipGetLastError();
 }
 

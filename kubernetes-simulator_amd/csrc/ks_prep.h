@@ -258,6 +258,8 @@ __device__ __forceinline__ void prep_body(const EngineArgs& a, int64_t start, in
     if (tid == 0) {
         ws.nb = nb; ws.e_cnt = e_cnt; ws.n_e = n_e; ws.n_es = n_es; ws.nslot = 0; ws.rescan = rescan;
         ws.lset = touch ? 0 : 1;  // pruned lists: the speculative scan's set, or the engine's own scan's
+        if (rescan) a.ctr[kCtrRescan] += 1;  // (diagnostics: ks_debug_counters [5])
+        if (touch && reuse) a.ctr[kCtrReuse] += 1;
         ws.split = touch && reuse ? (int32_t)(sp_start - start) : 0;
         ws.moff = (int32_t)(start - prev_start);
         ws.mpar = slot;

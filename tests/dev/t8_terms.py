@@ -48,8 +48,10 @@ def run(world, flags=0):
     eng.load_nodes(enc["alloc"], enc["taint"], enc["label"])
     eng.submit(enc["pods"])
     eng.step(S)
+    c0 = eng.debug_counters()
     eng.step(S)  # unprofiled: the batch time as the bench runs it (HIP events around the whole step)
     st0 = eng.last_step_stats()
+    c1 = eng.debug_counters()
     eng.set_profiling(True)
     eng.step(S)
     st, k = eng.last_step_stats(), eng.last_step_kernels()
@@ -57,7 +59,9 @@ def run(world, flags=0):
     nb = max(st["launches"], 1)
     us = lambda ms, n: ms / max(n, 1) * 1e3  # noqa: E731
     print(f"world {world} flags {flags}: {st0['step_ms'] / max(st0['launches'], 1) * 1e3:.1f} us per batch "
-          f"({st['step_ms'] / nb * 1e3:.1f} profiled), {st0['pods'] / max(st0['launches'], 1):.1f} pods/batch")
+          f"({st['step_ms'] / nb * 1e3:.1f} profiled), {st0['pods'] / max(st0['launches'], 1):.1f} pods/batch; "
+          f"per step: {st0['launches']} batches, {int(c1[4])} early stops, {int(c1[5] - c0[5])} rescans, "
+          f"{int(c1[6] - c0[6])} list reuses")
     print(f"   prep {us(k['prep_ms'], k['prep_n']):.1f} us x {k['prep_n'] / nb:.2f}, scan {us(k['scan_ms'], k['scan_n']):.1f}, "
           f"merge {us(k['merge_ms'], k['merge_n']):.1f} (part merges {us(k['part_ms'], k['xchg_n']):.1f}, "
           f"host exchange {us(k['xchg_ms'], k['xchg_n']):.1f} x {k['xchg_n'] / nb:.2f}), resolve {us(k['resolve_ms'], k['resolve_n']):.1f} x "
