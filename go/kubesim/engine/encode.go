@@ -33,20 +33,36 @@ func milli(q resource.Quantity) (int64, error) {
 }
 
 // Dicts are the taint and label dictionaries of a cluster: NoSchedule / NoExecute taints
-// (the only effects the taint filter sees) and (key, value) labels, at most 64 / 63 each.
+// (the only effects the taint filter sees) and (key, value) labels, each mapped to a mask bit.
+// Within one 64-bit mask every taint and pair has its own bit; a wider cluster encoded with
+// NodeArraysFor shares bits between interchangeable taints and leaves unreferenced pairs out
+// (include/ks_ingest.h ks_cluster_seal: the same rule as the C++ ingest).
 type Dicts struct {
-	taints []v1.Taint
-	labels map[[2]string]int
+	taints    []v1.Taint
+	taintBit  []int
+	labels    map[[2]string]int
+	nodePairs map[[2]string]bool
 }
 
 // NodeArrays encodes nodes (in config order: node index = tie-break order, kubesim.go:208-215)
-// for Engine.LoadNodes and builds the dictionaries pods are encoded against.
+// for Engine.LoadNodes and builds the dictionaries pods are encoded against; at most 64 distinct
+// NoSchedule/NoExecute taints and 63 label pairs (use NodeArraysFor past that).
 func NodeArrays(nodes []*v1.Node) (alloc []int64, taint, label []uint64, d *Dicts, err error) {
-	d = &Dicts{labels: map[[2]string]int{}}
+	return NodeArraysFor(nodes, nil)
+}
+
+// NodeArraysFor is NodeArrays for a cluster past one 64-bit mask, given every pod it will see
+// (VERDICT r5 item 5): only the label pairs some pod's nodeSelector references get bits (no other
+// label changes a placement: per-node hostname labels need none), and taints that exactly the same
+// pods tolerate share one bit (a node is feasible for a pod iff the pod tolerates each of its
+// taints).  With pods == nil, or a cluster within one mask, it is the plain encoding.
+func NodeArraysFor(nodes []*v1.Node, pods []*v1.Pod) (alloc []int64, taint, label []uint64, d *Dicts, err error) {
+	d = &Dicts{labels: map[[2]string]int{}, nodePairs: map[[2]string]bool{}}
 	seen := map[[3]string]int{}
 	alloc = make([]int64, 4*len(nodes))
 	taint = make([]uint64, len(nodes))
 	label = make([]uint64, len(nodes))
+	nodeTaints := make([][]int, len(nodes))
 	for i, n := range nodes {
 		cap := n.Status.Capacity
 		for k, name := range resourceNames {
@@ -65,26 +81,73 @@ func NodeArrays(nodes []*v1.Node) (alloc []int64, taint, label []uint64, d *Dict
 			key := [3]string{t.Key, t.Value, string(t.Effect)}
 			b, ok := seen[key]
 			if !ok {
-				if len(d.taints) == 64 {
-					return nil, nil, nil, nil, errors.Wrap(ErrOutOfDomain, "more than 64 distinct taints")
-				}
 				b = len(d.taints)
 				seen[key] = b
 				d.taints = append(d.taints, t)
 			}
-			taint[i] |= 1 << uint(b)
+			nodeTaints[i] = append(nodeTaints[i], b)
 		}
 		for k, v := range n.ObjectMeta.Labels {
+			d.nodePairs[[2]string{k, v}] = true
+		}
+	}
+	// taint bits: one per taint, or one per class of equal toleration signatures over the pods
+	d.taintBit = make([]int, len(d.taints))
+	nbits := len(d.taints)
+	if len(d.taints) > 64 && pods != nil {
+		class := map[string]int{}
+		for b := range d.taints {
+			sig := make([]byte, len(pods))
+			for j, pod := range pods {
+				for i := range pod.Spec.Tolerations {
+					if pod.Spec.Tolerations[i].ToleratesTaint(&d.taints[b]) {
+						sig[j] = 1
+						break
+					}
+				}
+			}
+			c, ok := class[string(sig)]
+			if !ok {
+				c = len(class)
+				class[string(sig)] = c
+			}
+			d.taintBit[b] = c
+		}
+		nbits = len(class)
+	} else {
+		for b := range d.taints {
+			d.taintBit[b] = b
+		}
+	}
+	if nbits > 64 {
+		return nil, nil, nil, nil, errors.Wrapf(ErrOutOfDomain, "%d distinct taint classes", nbits)
+	}
+	// label bits: every node pair, or the referenced ones past 63
+	referenced := map[[2]string]bool{}
+	for _, pod := range pods {
+		for k, v := range pod.Spec.NodeSelector {
+			referenced[[2]string{k, v}] = true
+		}
+	}
+	wide := len(d.nodePairs) > 63 && pods != nil
+	for i, n := range nodes {
+		for k, v := range n.ObjectMeta.Labels {
 			key := [2]string{k, v}
+			if wide && !referenced[key] {
+				continue
+			}
 			b, ok := d.labels[key]
 			if !ok {
 				if len(d.labels) == 63 {
-					return nil, nil, nil, nil, errors.Wrap(ErrOutOfDomain, "more than 63 distinct labels")
+					return nil, nil, nil, nil, errors.Wrap(ErrOutOfDomain, "more than 63 distinct (referenced) labels")
 				}
 				b = len(d.labels)
 				d.labels[key] = b
 			}
 			label[i] |= 1 << uint(b)
+		}
+		for _, b := range nodeTaints[i] {
+			taint[i] |= 1 << uint(d.taintBit[b])
 		}
 	}
 	return alloc, taint, label, d, nil
@@ -168,19 +231,30 @@ func EncodePods(pods []*v1.Pod, arrival int64, d *Dicts, kt *KeyTable) (*Pods, e
 				km |= 1 << uint(k)
 			}
 		}
-		var tol uint64
+		var tol, seen uint64
 		for b := range d.taints {
+			hit := false
 			for i := range pod.Spec.Tolerations {
 				if pod.Spec.Tolerations[i].ToleratesTaint(&d.taints[b]) {
-					tol |= 1 << uint(b)
+					hit = true
 					break
 				}
+			}
+			bit := uint64(1) << uint(d.taintBit[b])
+			if seen&bit != 0 && (tol&bit != 0) != hit { // a pod NodeArraysFor did not see splits a class
+				return nil, errors.Wrap(ErrOutOfDomain, "a pod's tolerations split a taint class")
+			}
+			seen |= bit
+			if hit {
+				tol |= bit
 			}
 		}
 		var sel uint64
 		for k, v := range pod.Spec.NodeSelector {
 			if b, ok := d.labels[[2]string{k, v}]; ok {
 				sel |= 1 << uint(b)
+			} else if d.nodePairs[[2]string{k, v}] { // a node pair NodeArraysFor saw unreferenced
+				return nil, errors.Wrap(ErrOutOfDomain, "a nodeSelector pair without a mask bit")
 			} else {
 				sel |= selImpossible
 			}

@@ -18,7 +18,9 @@
  * errInvalidResourceUsageField, an unsupported taint effect, malformed YAML); KS_ERANGE = a valid
  * input outside the engine's exact domain (a quantity that is negative, not a whole number of
  * milli-units or >= 2^63 milli-units; a simSpec resource other than cpu / memory / nvidia.com/gpu;
- * more than 64 NoSchedule/NoExecute taints or 63 label pairs).
+ * more than 64 NoSchedule/NoExecute taints or 63 label pairs — or, sealed with the pods noted,
+ * more than 64 toleration classes or 63 referenced pairs; a pod the seal did not see that splits a
+ * class or names an unreferenced node pair).
  */
 #ifndef KS_INGEST_H
 #define KS_INGEST_H
@@ -46,6 +48,23 @@ ks_status ks_parse_simspec(const char* yaml, int32_t max_phases, int32_t* n_phas
  * masks of each node's NoSchedule/NoExecute taints and of its labels, and "namespace/name". */
 typedef struct ks_cluster ks_cluster;
 ks_status ks_cluster_parse(const char* yaml, ks_cluster** out, char* err, int32_t err_len);
+
+/* The two-phase form for clusters past one 64-bit mask (a unique kubernetes.io/hostname label per
+ * node, hundreds of taints): parse with KS_CLUSTER_DEFER_MASKS, note every pod's tolerations and
+ * nodeSelector (ks_cluster_note_pod, the same strings ks_cluster_tolerations / _selector take),
+ * then ks_cluster_seal.  The seal gives bits only to label pairs some noted selector references and
+ * one bit per class of taints the same noted toleration lists tolerate — exact for every noted pod
+ * (toleration.go:37-56 decides identically on interchangeable taints; an unreferenced label cannot
+ * change a placement).  A cluster that fits one mask seals to the plain one-bit-per-entry encoding
+ * ks_cluster_parse gives.  Until sealed, ks_cluster_arrays / _tolerations / _selector return
+ * KS_EINVAL.  Replaces nothing in the reference (its maps hold any number of entries): it is how
+ * the masks reach the reference's domain. */
+#define KS_CLUSTER_DEFER_MASKS 1
+ks_status ks_cluster_parse_ex(const char* yaml, int32_t flags, ks_cluster** out, char* err, int32_t err_len);
+ks_status ks_cluster_note_pod(ks_cluster* c, int32_t n_tol, const char* const* key, const char* const* op,
+                              const char* const* value, const char* const* effect, int32_t n_sel,
+                              const char* const* sel_key, const char* const* sel_value);
+ks_status ks_cluster_seal(ks_cluster* c, char* err, int32_t err_len);
 void ks_cluster_free(ks_cluster* c);
 int64_t ks_cluster_nodes(const ks_cluster* c);
 int32_t ks_cluster_tick(const ks_cluster* c);          /* `tick`, default 10 (kubesim.go:239) */

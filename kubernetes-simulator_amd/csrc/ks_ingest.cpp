@@ -10,6 +10,7 @@
 // flow collections); yaml.v2 hands map values to a map[string]string as their literal text
 // (vendor/gopkg.in/yaml.v2/decode.go:420-428), which is what a scalar keeps here.
 #include <algorithm>
+#include <array>
 #include <cctype>
 #include <cerrno>
 #include <climits>
@@ -552,14 +553,90 @@ int resource_index(const std::string& name) {
 // Cluster
 // ------------------------------------------------------------------------------------------
 struct ks_cluster {
+    using Taint = std::tuple<std::string, std::string, std::string>;  // key, value, effect
+    using Pair = std::pair<std::string, std::string>;
+    using Tol = std::array<std::string, 4>;                            // key, operator, value, effect
     int32_t tick = 10;
     std::string start_clock;
     std::vector<std::string> names;
     std::vector<int64_t> alloc;  // [n][4]
     std::vector<uint64_t> taint, label;
-    std::vector<std::tuple<std::string, std::string, std::string>> taint_dict;  // key, value, effect
-    std::map<std::pair<std::string, std::string>, int> label_dict;
+    // every NoSchedule/NoExecute taint and label pair the nodes carry (sorted), and each node's
+    std::vector<Taint> all_taints;
+    std::vector<Pair> all_pairs;
+    std::vector<std::vector<int32_t>> node_taints, node_pairs;
+    // the encoding ks_cluster_seal chose: taint -> bit (its toleration class) and label pair -> bit
+    bool sealed = false;
+    std::vector<int32_t> taint_bit;
+    int32_t n_taint_bits = 0;
+    std::map<Pair, int> label_dict;
+    // pods noted before sealing (the two-phase form): distinct toleration lists, referenced pairs
+    std::set<std::vector<Tol>> noted_tols;
+    std::set<Pair> noted_pairs;
 };
+
+namespace {
+
+bool tolerates(const ks_cluster::Tol& t, const ks_cluster::Taint& x) {
+    const auto& [tk, tv, te] = x;
+    bool ok = t[3].empty() || t[3] == te;                                  // toleration.go:38-40
+    ok = ok && (t[0].empty() || t[0] == tk);                               // :42-44
+    return ok && ((t[1].empty() || t[1] == "Equal") ? t[2] == tv : t[1] == "Exists");  // :47-55
+}
+
+/* Choose the masks' bits and build the node masks.  One bit per taint and per label pair while
+ * the cluster fits one 64-bit mask (the cluster alone decides: ks_cluster_parse).  Past that
+ * (VERDICT r5 item 5), with the pods noted: only label pairs some noted nodeSelector references get
+ * bits (no other pair can change a placement — per-node hostname labels need none), and taints
+ * that exactly the same noted toleration lists tolerate share one bit (a node is feasible for a pod
+ * iff the pod tolerates each of its taints, so interchangeable taints decide identically). */
+ks_status seal(ks_cluster* c, bool wide, char* err, int32_t err_len) {
+    const size_t T = c->all_taints.size(), L = c->all_pairs.size();
+    c->taint_bit.assign(T, 0);
+    if (T <= 64 || !wide) {
+        for (size_t t = 0; t < T; t++) c->taint_bit[t] = (int32_t)t;
+        c->n_taint_bits = (int32_t)T;
+    } else {
+        std::map<std::vector<bool>, int32_t> cls;
+        for (size_t t = 0; t < T; t++) {
+            std::vector<bool> sig;
+            sig.reserve(c->noted_tols.size());
+            for (const auto& tl : c->noted_tols) {
+                bool any = false;
+                for (const auto& x : tl) any = any || tolerates(x, c->all_taints[t]);
+                sig.push_back(any);
+            }
+            const auto it = cls.emplace(std::move(sig), (int32_t)cls.size()).first;
+            c->taint_bit[t] = it->second;
+        }
+        c->n_taint_bits = (int32_t)cls.size();
+    }
+    c->label_dict.clear();
+    int li = 0;
+    for (const auto& l : c->all_pairs)
+        if (L <= 63 || !wide || c->noted_pairs.count(l)) c->label_dict[l] = li++;
+    if (c->n_taint_bits > 64 || li > 63) {
+        set_err(err, err_len, "%d taint classes / %d label pairs exceed one 64-bit mask%s", c->n_taint_bits, li,
+                wide ? "" : " (note the pods and seal: ks_cluster_parse_ex)");
+        return KS_ERANGE;
+    }
+    const size_t n = c->names.size();
+    c->taint.assign(n, 0);
+    c->label.assign(n, 0);
+    for (size_t i = 0; i < n; i++) {
+        for (int32_t t : c->node_taints[i]) c->taint[i] |= 1ull << c->taint_bit[t];
+        for (int32_t l : c->node_pairs[i]) {
+            const auto it = c->label_dict.find(c->all_pairs[l]);
+            if (it != c->label_dict.end()) c->label[i] |= 1ull << it->second;
+        }
+    }
+    c->sealed = true;
+    return KS_OK;
+}
+
+std::string cstr(const char* s) { return std::string(s ? s : ""); }
+
+}  // namespace
 
 extern "C" {
 
@@ -632,8 +709,8 @@ ks_status ks_parse_simspec(const char* yaml, int32_t max_phases, int32_t* n_phas
     return KS_OK;
 }
 
-ks_status ks_cluster_parse(const char* yaml, ks_cluster** out, char* err, int32_t err_len) {
-    if (!yaml || !out) return KS_EINVAL;
+ks_status ks_cluster_parse_ex(const char* yaml, int32_t flags, ks_cluster** out, char* err, int32_t err_len) {
+    if (!yaml || !out || (flags & ~KS_CLUSTER_DEFER_MASKS)) return KS_EINVAL;
     *out = nullptr;
     std::unique_ptr<YNode> doc;
     try {
@@ -736,27 +813,51 @@ ks_status ks_cluster_parse(const char* yaml, ks_cluster** out, char* err, int32_
             if (std::get<2>(t) != "PreferNoSchedule") tset.insert(t);  // never filters
         for (const auto& l : x.labels) lset.insert(l);
     }
-    if (tset.size() > 64 || lset.size() > 63) {
-        set_err(err, err_len, "%zu taints / %zu label pairs exceed one 64-bit mask", tset.size(), lset.size());
-        return KS_ERANGE;
-    }
-    c->taint_dict.assign(tset.begin(), tset.end());
-    int li = 0;
-    for (const auto& l : lset) c->label_dict[l] = li++;
+    c->all_taints.assign(tset.begin(), tset.end());
+    c->all_pairs.assign(lset.begin(), lset.end());
     const size_t n = in.size();
     c->alloc.resize(4 * n);
-    c->taint.assign(n, 0);
-    c->label.assign(n, 0);
+    c->node_taints.resize(n);
+    c->node_pairs.resize(n);
     for (size_t i = 0; i < n; i++) {
         for (int k = 0; k < 4; k++) c->alloc[4 * i + k] = in[i].alloc[k];
         for (const auto& t : in[i].taints) {
-            const auto it = std::lower_bound(c->taint_dict.begin(), c->taint_dict.end(), t);
-            if (it != c->taint_dict.end() && *it == t) c->taint[i] |= 1ull << (it - c->taint_dict.begin());
+            const auto it = std::lower_bound(c->all_taints.begin(), c->all_taints.end(), t);
+            if (it != c->all_taints.end() && *it == t) c->node_taints[i].push_back((int32_t)(it - c->all_taints.begin()));
         }
-        for (const auto& l : in[i].labels) c->label[i] |= 1ull << c->label_dict[l];
+        for (const auto& l : in[i].labels)
+            c->node_pairs[i].push_back((int32_t)(std::lower_bound(c->all_pairs.begin(), c->all_pairs.end(), l) -
+                                                 c->all_pairs.begin()));
+    }
+    if (!(flags & KS_CLUSTER_DEFER_MASKS)) {
+        const ks_status r = seal(c.get(), false, err, err_len);
+        if (r != KS_OK) return r;
     }
     *out = c.release();
     return KS_OK;
+}
+
+ks_status ks_cluster_parse(const char* yaml, ks_cluster** out, char* err, int32_t err_len) {
+    return ks_cluster_parse_ex(yaml, 0, out, err, err_len);
+}
+
+ks_status ks_cluster_note_pod(ks_cluster* c, int32_t n_tol, const char* const* key, const char* const* op,
+                              const char* const* value, const char* const* effect, int32_t n_sel,
+                              const char* const* sel_key, const char* const* sel_value) {
+    if (!c || c->sealed || n_tol < 0 || n_sel < 0 || (n_tol > 0 && (!key || !op || !value || !effect)) ||
+        (n_sel > 0 && (!sel_key || !sel_value)))
+        return KS_EINVAL;
+    std::vector<ks_cluster::Tol> tl;
+    for (int32_t i = 0; i < n_tol; i++) tl.push_back({cstr(key[i]), cstr(op[i]), cstr(value[i]), cstr(effect[i])});
+    std::sort(tl.begin(), tl.end());
+    c->noted_tols.insert(std::move(tl));
+    for (int32_t i = 0; i < n_sel; i++) c->noted_pairs.emplace(cstr(sel_key[i]), cstr(sel_value[i]));
+    return KS_OK;
+}
+
+ks_status ks_cluster_seal(ks_cluster* c, char* err, int32_t err_len) {
+    if (!c || c->sealed) return KS_EINVAL;
+    return seal(c, true, err, err_len);
 }
 
 void ks_cluster_free(ks_cluster* c) { delete c; }
@@ -768,7 +869,7 @@ const char* ks_cluster_node_name(const ks_cluster* c, int64_t i) {
 }
 
 ks_status ks_cluster_arrays(const ks_cluster* c, int64_t* alloc, uint64_t* taint, uint64_t* label) {
-    if (!c) return KS_EINVAL;
+    if (!c || !c->sealed) return KS_EINVAL;
     const size_t n = c->names.size();
     if (alloc) std::memcpy(alloc, c->alloc.data(), sizeof(int64_t) * 4 * n);
     if (taint) std::memcpy(taint, c->taint.data(), sizeof(uint64_t) * n);
@@ -778,18 +879,19 @@ ks_status ks_cluster_arrays(const ks_cluster* c, int64_t* alloc, uint64_t* taint
 
 ks_status ks_cluster_tolerations(const ks_cluster* c, int32_t n, const char* const* key, const char* const* op,
                                  const char* const* value, const char* const* effect, uint64_t* tol_out) {
-    if (!c || !tol_out || n < 0 || (n > 0 && (!key || !op || !value || !effect))) return KS_EINVAL;
-    uint64_t m = 0;
-    auto str = [](const char* s) { return std::string(s ? s : ""); };
-    for (int32_t i = 0; i < n; i++) {
-        const std::string k = str(key[i]), o = str(op[i]), v = str(value[i]), e = str(effect[i]);
-        for (size_t t = 0; t < c->taint_dict.size(); t++) {
-            const auto& [tk, tv, te] = c->taint_dict[t];
-            bool ok = e.empty() || e == te;                          // toleration.go:38-40
-            ok = ok && (k.empty() || k == tk);                       // :42-44
-            ok = ok && ((o.empty() || o == "Equal") ? v == tv : o == "Exists");  // :47-55
-            if (ok) m |= 1ull << t;
-        }
+    if (!c || !c->sealed || !tol_out || n < 0 || (n > 0 && (!key || !op || !value || !effect))) return KS_EINVAL;
+    std::vector<ks_cluster::Tol> tl;
+    for (int32_t i = 0; i < n; i++) tl.push_back({cstr(key[i]), cstr(op[i]), cstr(value[i]), cstr(effect[i])});
+    uint64_t m = 0, seen = 0;
+    for (size_t t = 0; t < c->all_taints.size(); t++) {
+        bool any = false;
+        for (const auto& x : tl) any = any || tolerates(x, c->all_taints[t]);
+        const uint64_t b = 1ull << c->taint_bit[t];
+        // a class shares one bit only if this pod tolerates all of it or none of it: a pod the
+        // seal never saw may split a class, and its mask would then be inexact
+        if ((seen & b) && (bool)(m & b) != any) return KS_ERANGE;
+        seen |= b;
+        if (any) m |= b;
     }
     *tol_out = m;
     return KS_OK;
@@ -797,11 +899,18 @@ ks_status ks_cluster_tolerations(const ks_cluster* c, int32_t n, const char* con
 
 ks_status ks_cluster_selector(const ks_cluster* c, int32_t n, const char* const* key, const char* const* value,
                               uint64_t* sel_out) {
-    if (!c || !sel_out || n < 0 || (n > 0 && (!key || !value))) return KS_EINVAL;
+    if (!c || !c->sealed || !sel_out || n < 0 || (n > 0 && (!key || !value))) return KS_EINVAL;
     uint64_t m = 0;
     for (int32_t i = 0; i < n; i++) {
-        const auto it = c->label_dict.find({key[i] ? key[i] : "", value[i] ? value[i] : ""});
-        m |= it == c->label_dict.end() ? (1ull << 63) : (1ull << it->second);
+        const ks_cluster::Pair pr(cstr(key[i]), cstr(value[i]));
+        const auto it = c->label_dict.find(pr);
+        if (it != c->label_dict.end()) {
+            m |= 1ull << it->second;
+        } else if (std::binary_search(c->all_pairs.begin(), c->all_pairs.end(), pr)) {
+            return KS_ERANGE;  // a pair some node carries that the seal did not see referenced
+        } else {
+            m |= 1ull << 63;   // no node carries it: infeasible everywhere
+        }
     }
     *sel_out = m;
     return KS_OK;

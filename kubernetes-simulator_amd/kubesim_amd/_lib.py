@@ -42,7 +42,9 @@ EXPORTED_SYMBOLS = ("ks_create", "ks_destroy", "ks_load_nodes", "ks_submit_pods"
                     # include/ks_ingest.h
                     "ks_parse_quantity", "ks_parse_simspec", "ks_cluster_parse", "ks_cluster_free",
                     "ks_cluster_nodes", "ks_cluster_tick", "ks_cluster_start_clock", "ks_cluster_arrays",
-                    "ks_cluster_node_name", "ks_cluster_tolerations", "ks_cluster_selector")
+                    "ks_cluster_node_name", "ks_cluster_tolerations", "ks_cluster_selector",
+                    "ks_cluster_parse_ex", "ks_cluster_note_pod", "ks_cluster_seal")
+KS_CLUSTER_DEFER_MASKS = 1
 KS_COMM_ID_BYTES = 128
 # include/ks_kubesim.h (libks_kubesim.so)
 RUN_SYMBOLS = ("ks_run", "ks_trace_submit", "ks_local_exchange_create", "ks_local_exchange_destroy",
@@ -256,5 +258,11 @@ def load():
     L.ks_cluster_tolerations.restype = C.c_int
     L.ks_cluster_selector.argtypes = [p, C.c_int32, p, p, C.POINTER(C.c_uint64)]
     L.ks_cluster_selector.restype = C.c_int
+    L.ks_cluster_parse_ex.argtypes = [C.c_char_p, C.c_int32, C.POINTER(C.c_void_p), C.c_char_p, C.c_int32]
+    L.ks_cluster_parse_ex.restype = C.c_int
+    L.ks_cluster_note_pod.argtypes = [p, C.c_int32, p, p, p, p, C.c_int32, p, p]
+    L.ks_cluster_note_pod.restype = C.c_int
+    L.ks_cluster_seal.argtypes = [p, C.c_char_p, C.c_int32]
+    L.ks_cluster_seal.restype = C.c_int
     _lib = L
     return L

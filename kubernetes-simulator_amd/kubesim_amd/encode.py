@@ -67,8 +67,38 @@ def _unique_rows(rows: np.ndarray):
     return uniq, inv.reshape(-1)
 
 
-def encode_nodes(nodes: dict):
-    """Return ``(alloc[n][4] i64, taint[n] u64, label[n] u64, taint_dict, label_dict)``."""
+def _taint_classes(uniq, pods):
+    """Wide taint domains (> 64 distinct NoSchedule/NoExecute taints): taints that exactly the same
+    pods tolerate are interchangeable for the filter — a node is feasible for pod p iff p tolerates
+    every one of its taints — so one bit per class of equal toleration signatures (over every pod of
+    the trace, ``Toleration.ToleratesTaint`` as ``tolerates``) decides exactly as one bit per taint.
+    Returns each taint's class and the classes' representatives (a pod tolerates a class iff it
+    tolerates its representative)."""
+    tol = pods["tol"]
+    sig_class, cls, reps = {}, np.zeros(len(uniq), dtype=np.int64), []
+    for i, (k, v, e) in enumerate(uniq):
+        if len(tol):
+            hit = tolerates(tol[:, 0], tol[:, 1], tol[:, 2], tol[:, 3], int(k), int(v), int(e)).astype(np.uint64)
+            per_pod = _or_reduce_csr(hit, pods["tol_off"]) != 0
+        else:
+            per_pod = np.zeros(pods["m"], dtype=bool)
+        key = np.packbits(per_pod).tobytes()
+        if key not in sig_class:
+            sig_class[key] = len(reps)
+            reps.append(tuple(int(x) for x in (k, v, e)))
+        cls[i] = sig_class[key]
+    return cls, reps
+
+
+def encode_nodes(nodes: dict, pods: dict | None = None):
+    """Return ``(alloc[n][4] i64, taint[n] u64, label[n] u64, taint_dict, label_dict)``.
+
+    With the trace's ``pods`` the domain widens where one 64-bit mask per node
+    would not hold it: more than 63 distinct label pairs encode only the pairs some pod's
+    nodeSelector references (no other label can change a placement — per-node hostname labels
+    need no bits), and more than 64 distinct NoSchedule/NoExecute taints encode one bit per class of
+    taints that the same pods tolerate (``_taint_classes``).  Within one mask the encoding is the
+    plain one-bit-per-entry dictionary."""
     n = nodes["n"]
     alloc = nodes["alloc"].astype(np.int64).copy()
     has = nodes["alloc_has"]
@@ -86,9 +116,12 @@ def encode_nodes(nodes: dict):
         # sorted distinct rows: the order of sorted(set(tuples)).
         uniq, inv = _unique_rows(t[filt])
         taint_dict = [tuple(int(x) for x in r) for r in uniq]
+        bit_of = np.arange(len(taint_dict), dtype=np.int64)
+        if len(taint_dict) > MAX_TAINT_BITS and pods is not None:
+            bit_of, taint_dict = _taint_classes(uniq, pods)
         if len(taint_dict) > MAX_TAINT_BITS:
-            raise EncodeError(f"{len(taint_dict)} distinct NoSchedule/NoExecute taints > {MAX_TAINT_BITS} (W=1)")
-        tbits[filt] = np.left_shift(np.uint64(1), inv.reshape(-1).astype(np.uint64))
+            raise EncodeError(f"{len(taint_dict)} distinct NoSchedule/NoExecute taint classes > {MAX_TAINT_BITS} (W=1)")
+        tbits[filt] = np.left_shift(np.uint64(1), bit_of[inv.reshape(-1)].astype(np.uint64))
     node_taint = _or_reduce_csr(tbits, nodes["taint_off"])
 
     lab = nodes["label"]
@@ -97,9 +130,17 @@ def encode_nodes(nodes: dict):
     if len(lab):
         uniq, inv = _unique_rows(lab)
         pairs = [(int(r[0]), int(r[1])) for r in uniq]
+        keep = np.ones(len(pairs), dtype=bool)
+        if len(pairs) > MAX_LABEL_BITS and pods is not None:  # only the pairs a selector references
+            sel = pods["sel"]
+            ref = set(zip(sel[:, 0].tolist(), sel[:, 1].tolist())) if len(sel) else set()
+            keep = np.array([pr in ref for pr in pairs], dtype=bool)
+            pairs = [pr for pr, k in zip(pairs, keep) if k]
         if len(pairs) > MAX_LABEL_BITS:
-            raise EncodeError(f"{len(pairs)} distinct label pairs > {MAX_LABEL_BITS} (W=1)")
-        lbits = np.left_shift(np.uint64(1), inv.reshape(-1).astype(np.uint64))
+            raise EncodeError(f"{len(pairs)} distinct (referenced) label pairs > {MAX_LABEL_BITS} (W=1)")
+        bit = np.cumsum(keep) - 1
+        lbits = np.where(keep[inv.reshape(-1)], np.left_shift(np.uint64(1), np.maximum(bit[inv.reshape(-1)], 0).astype(np.uint64)),
+                         np.uint64(0)).astype(np.uint64)
     node_label = _or_reduce_csr(lbits, nodes["label_off"])
     assert n == len(alloc)
     return alloc, node_taint, node_label, taint_dict, pairs
@@ -155,6 +196,6 @@ def encode_pods(pods: dict, taint_dict, label_dict):
 
 
 def encode_trace(trace: dict):
-    alloc, taint, label, tdict, ldict = encode_nodes(trace["nodes"])
+    alloc, taint, label, tdict, ldict = encode_nodes(trace["nodes"], trace["pods"])
     pods = encode_pods(trace["pods"], tdict, ldict)
     return dict(alloc=alloc, taint=taint, label=label, taint_dict=tdict, label_dict=ldict, pods=pods)

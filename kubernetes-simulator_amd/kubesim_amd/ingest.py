@@ -53,14 +53,30 @@ class Cluster:
     """A parsed cluster config: node arrays for ``Engine.load_nodes`` plus the taint / label
     dictionaries pod tolerations and selectors are encoded against."""
 
-    def __init__(self, yaml_text: str):
+    def __init__(self, yaml_text: str, pods=None):
+        """``pods``: optional [(tolerations, selector pairs)] of every pod the cluster will see
+        (``tolerations`` / ``selector`` argument forms).  Given, the masks are sealed over them
+        (ks_cluster_parse_ex + ks_cluster_note_pod + ks_cluster_seal), so a cluster past one 64-bit
+        mask — a hostname label per node, hundreds of taints — still encodes exactly."""
         self._L = _lib.load()
         h = C.c_void_p()
         err = C.create_string_buffer(256)
-        rc = self._L.ks_cluster_parse(_cs(yaml_text), C.byref(h), err, 256)
+        if pods is None:
+            rc = self._L.ks_cluster_parse(_cs(yaml_text), C.byref(h), err, 256)
+        else:
+            rc = self._L.ks_cluster_parse_ex(_cs(yaml_text), _lib.KS_CLUSTER_DEFER_MASKS, C.byref(h), err, 256)
         if rc != _lib.KS_OK:
             raise KsError(rc, err.value.decode())
         self.h = h
+        if pods is not None:
+            for tols, pairs in pods:
+                rc = self._L.ks_cluster_note_pod(h, len(tols), *self._tol_arrays(tols), len(pairs),
+                                                 *self._pair_arrays(pairs))
+                if rc != _lib.KS_OK:
+                    raise KsError(rc, "ks_cluster_note_pod")
+            rc = self._L.ks_cluster_seal(h, err, 256)
+            if rc != _lib.KS_OK:
+                raise KsError(rc, err.value.decode())
         self.n = int(self._L.ks_cluster_nodes(h))
         self.tick = int(self._L.ks_cluster_tick(h))
         self.start_clock = self._L.ks_cluster_start_clock(h).decode()
@@ -71,23 +87,26 @@ class Cluster:
         self._L.ks_cluster_arrays(h, p(self.alloc), p(self.taint), p(self.label))
         self.names = [self._L.ks_cluster_node_name(h, i).decode() for i in range(self.n)]
 
+    @staticmethod
+    def _tol_arrays(tols):
+        return [(C.c_char_p * max(len(tols), 1))(*[_cs(t[j] or "") for t in tols]) for j in range(4)]
+
+    @staticmethod
+    def _pair_arrays(pairs):
+        return [(C.c_char_p * max(len(pairs), 1))(*[_cs(x[j]) for x in pairs]) for j in range(2)]
+
     def tolerations(self, tols):
         """tols: [(key, operator, value, effect)] -> tolerated-taint mask."""
-        n = len(tols)
-        arr = [(C.c_char_p * max(n, 1))(*[_cs(t[j] or "") for t in tols]) for j in range(4)]
         out = C.c_uint64(0)
-        rc = self._L.ks_cluster_tolerations(self.h, n, *arr, C.byref(out))
+        rc = self._L.ks_cluster_tolerations(self.h, len(tols), *self._tol_arrays(tols), C.byref(out))
         if rc != _lib.KS_OK:
             raise KsError(rc, "ks_cluster_tolerations")
         return out.value
 
     def selector(self, pairs):
         """pairs: [(key, value)] -> required-label mask (bit 63: a pair no node carries)."""
-        n = len(pairs)
-        ks = (C.c_char_p * max(n, 1))(*[_cs(k) for k, _ in pairs])
-        vs = (C.c_char_p * max(n, 1))(*[_cs(v) for _, v in pairs])
         out = C.c_uint64(0)
-        rc = self._L.ks_cluster_selector(self.h, n, ks, vs, C.byref(out))
+        rc = self._L.ks_cluster_selector(self.h, len(pairs), *self._pair_arrays(pairs), C.byref(out))
         if rc != _lib.KS_OK:
             raise KsError(rc, "ks_cluster_selector")
         return out.value

@@ -323,6 +323,91 @@ def synth_trace(n_nodes: int, n_pods: int, seed: int, *, taints: bool, labels: b
     return dict(config=config, tick_seconds=10, strings=st.strings, nodes=nodes, pods=pods)
 
 
+def wide_trace(n_nodes=50_000, n_pods=20_000, seed=0x5EED0006, n_taint_keys=30, n_taint_vals=4, n_host_sel=24,
+               host_sel_permille=2):
+    """A cluster past one 64-bit mask per node: every node carries a unique
+    ``kubernetes.io/hostname`` label beside the C3 families, and the taint dictionary holds
+    ``n_taint_keys`` x ``n_taint_vals`` NoSchedule / NoExecute taints (120 by default) plus 10
+    PreferNoSchedule.  A quarter of the nodes carry one or two of them.  Pods tolerate with the C3
+    mix of kinds, but their keys come from the first ten taint keys only (clusters carry more taints
+    than any pod tolerates); ``host_sel_permille`` / 1000 of the pods select the hostname of one of ``n_host_sel`` untainted
+    nodes (and nothing else; 100m CPU, 128Mi, no GPU), the rest select C3 families as ``c3_trace`` does."""
+    tr = synth_trace(n_nodes, n_pods, seed, taints=False, labels=True, tolerations=False, selectors=True,
+                     config="wide")
+    st = StringTable()
+    st.strings = list(tr["strings"])
+    st.index = {x: i for i, x in enumerate(st.strings)}
+    N, P = int(n_nodes), int(n_pods)
+    nid = np.arange(N, dtype=np.uint64)
+    pid = np.arange(P, dtype=np.uint64)
+    # taints
+    T = n_taint_keys * n_taint_vals
+    tdict = []
+    for j in range(T):
+        eff = NO_EXECUTE if j % 3 == 2 else NO_SCHEDULE
+        tdict.append((st.intern(f"taint.wide/k{j % n_taint_keys}"), st.intern(f"w{j // n_taint_keys}"), eff))
+    for j in range(10):
+        tdict.append((st.intern(f"taint.wide/pref{j}"), st.intern("x"), PREFER_NO_SCHEDULE))
+    tdict = np.array(tdict, dtype=np.int32)
+    u = uniform_int(seed, 50, nid, 4)
+    ntaint = np.where(u < 3, 0, 1 + uniform_int(seed, 51, nid, 2)).astype(np.int32)
+    t_off = _csr_from_counts(ntaint)
+    first = uniform_int(seed, 52, nid, len(tdict))
+    second = (first + 1 + uniform_int(seed, 53, nid, len(tdict) - 1)) % len(tdict)
+    owner = np.repeat(np.arange(N), ntaint)
+    slot = np.arange(int(t_off[-1])) - t_off[owner]
+    rows = tdict[np.where(slot == 0, first[owner], second[owner])].astype(np.int32)
+    nodes = tr["nodes"]
+    nodes["taint_off"], nodes["taint"] = t_off, rows
+    # a unique hostname label per node (after the four families)
+    host_key = st.intern("kubernetes.io/hostname")
+    lab = nodes["label"].reshape(N, 4, 2)
+    host = np.array([[host_key, st.intern(f"node-{i:07d}")] for i in range(N)], dtype=np.int32)
+    nodes["label"] = np.concatenate([lab, host[:, None, :]], axis=1).reshape(-1, 2)
+    nodes["label_off"] = np.arange(0, 5 * N + 1, 5, dtype=np.int32)
+    # tolerations over the first ten taint keys (the C3 kinds)
+    ntol = uniform_int(seed, 54, pid, 4).astype(np.int32)
+    tl_off = _csr_from_counts(ntol)
+    K = int(tl_off[-1])
+    kid = np.arange(K, dtype=np.uint64)
+    kind = uniform_int(seed, 55, kid, 16)
+    j = uniform_int(seed, 56, kid, 10) + n_taint_keys * uniform_int(seed, 57, kid, n_taint_vals)
+    tk, tv, te = tdict[j, 0], tdict[j, 1], tdict[j, 2]
+    vrand = np.array([st.intern(f"w{x}") for x in range(n_taint_vals + 1)], dtype=np.int32)[
+        uniform_int(seed, 58, kid, n_taint_vals + 1)]
+    rare = uniform_int(seed, 59, kid, 4) != 0
+    kind = np.where((kind == 0) & rare, 2, kind)
+    key = np.where(kind <= 1, 0, tk)
+    op = np.where(kind <= 1, OP_EXISTS, np.where((kind >= 8) & (kind <= 11), OP_EXISTS,
+                                                  np.where(kind == 15, OP_INVALID, OP_EQUAL)))
+    val = np.where(kind <= 1, 0, np.where((kind >= 8) & (kind <= 11), 0,
+                                          np.where((kind >= 12) & (kind <= 14), vrand, tv)))
+    eff = np.where(kind == 0, EFFECT_NONE, np.where(kind == 1, NO_SCHEDULE,
+                   np.where((kind >= 2) & (kind <= 7), te, EFFECT_NONE)))
+    pods = tr["pods"]
+    pods["tol_off"] = tl_off
+    pods["tol"] = np.stack([key, op, val, eff], axis=1).astype(np.int32)
+    # 0.2 % of the pods: a hostname selector alone (one of n_host_sel untainted nodes)
+    untainted = np.nonzero((ntaint == 0) & (nodes["alloc_has"] == 15))[0]
+    hosts = untainted[(np.arange(n_host_sel) * 7919) % len(untainted)]
+    hsel = uniform_int(seed, 60, pid, 1000) < host_sel_permille
+    pick = hosts[uniform_int(seed, 61, pid, n_host_sel)]
+    s_off, sel = pods["sel_off"], pods["sel"]
+    nsel = np.diff(s_off)
+    nsel = np.where(hsel, 1, nsel).astype(np.int32)
+    new_off = _csr_from_counts(nsel)
+    new_sel = np.zeros((int(new_off[-1]), 2), dtype=np.int32)
+    for i in np.nonzero(~hsel & (np.diff(s_off) > 0))[0]:
+        new_sel[new_off[i]:new_off[i + 1]] = sel[s_off[i]:s_off[i + 1]]
+    hi = np.nonzero(hsel)[0]
+    new_sel[new_off[hi], 0] = host_key
+    new_sel[new_off[hi], 1] = host[pick[hi], 1]
+    pods["sel_off"], pods["sel"] = new_off, new_sel
+    pods["req"][hsel] = (100, 128 * 2**20 * MILLI, 0)   # a pinned pod is small: its node must keep room
+    tr["strings"] = st.strings
+    return tr
+
+
 def c2_trace(n_nodes=5000, n_pods=100_000, seed=0x5EED0002, **kw):
     """BASELINE.json configs[1]: 5k nodes / 100k pods, cpu+mem+gpu, multi-phase simSpec."""
     return synth_trace(n_nodes, n_pods, seed, taints=False, labels=False, tolerations=False,

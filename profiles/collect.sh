@@ -17,7 +17,7 @@ export TMPDIR=/tmp
 ( while true; do date +%T >> "$OUT/heartbeat.txt"; sleep 30; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
-B="$ROOT/bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-c5 --no-dropin --no-c3q --no-c4"
+B="$ROOT/bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-c5 --no-dropin --no-c3q --no-c4 --no-c3-literal"
 cd /tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$DB/c3" -o run -- python3 $B > "$ROOT/$OUT/c3_bench.json"
 echo "c3 trace done"

@@ -60,3 +60,38 @@ def test_negative_inputs_rejected():
     tr["pods"]["req"][0, 0] = -1
     with pytest.raises(encode.EncodeError):
         encode.encode_trace(tr)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_wide_domain_masks_match_literal_predicates(seed):
+    """a cluster past one 64-bit mask — a unique hostname label per node (more
+    than 63 label pairs) and 130 distinct taints (120 NoSchedule/NoExecute) — encodes referenced
+    label pairs only and one bit per toleration class of taints, and still decides every (pod, node)
+    exactly as the literal string predicates do."""
+    tr = tracegen.wide_trace(n_nodes=800, n_pods=90, seed=0x77 + seed, host_sel_permille=80)
+    assert len(np.unique(tr["nodes"]["label"], axis=0)) > encode.MAX_LABEL_BITS
+    t = tr["nodes"]["taint"]
+    assert len(np.unique(t[t[:, 2] != tracegen.PREFER_NO_SCHEDULE], axis=0)) > encode.MAX_TAINT_BITS
+    enc = encode.encode_trace(tr)
+    assert len(enc["label_dict"]) <= encode.MAX_LABEL_BITS and len(enc["taint_dict"]) <= encode.MAX_TAINT_BITS
+    ps = PySim(tr)
+    ps.submit(tr)
+    p = enc["pods"]
+    hosts = 0
+    for j in range(tr["pods"]["m"]):
+        pod = ps.pods[j]
+        for n in range(tr["nodes"]["n"]):
+            taint_ok = (int(enc["taint"][n]) & ~int(p["tol"][j]) & 0xFFFFFFFFFFFFFFFF) == 0
+            sel_ok = (int(enc["label"][n]) & int(p["sel"][j])) == int(p["sel"][j])
+            assert taint_ok == ps._taint_ok(n, pod), (j, n)
+            assert sel_ok == ps._selector_ok(n, pod), (j, n)
+            hosts += sel_ok and p["sel"][j] != 0 and bin(int(p["sel"][j])).count("1") == 1
+    assert hosts > 0
+
+
+def test_wide_domain_full_size_encodes():
+    """The 50k-node form of the wide trace (unique hostnames, 130 taints) fits one mask per node."""
+    tr = tracegen.wide_trace()
+    enc = encode.encode_trace(tr)
+    assert tr["nodes"]["n"] == 50_000
+    assert len(enc["taint_dict"]) <= encode.MAX_TAINT_BITS and len(enc["label_dict"]) <= encode.MAX_LABEL_BITS

@@ -220,3 +220,55 @@ def test_tolerations_match_python_encoder():
         a, b = p["tol_off"][q], p["tol_off"][q + 1]
         tols = [(st[k], ops[int(o)], st[v], effn[int(e)]) for k, o, v, e in p["tol"][a:b]]
         assert c.tolerations(tols) == int(enc["pods"]["tol"][q]), (q, tols)
+
+
+def test_wide_cluster_two_phase_seal_matches_literal_predicates():
+    """VERDICT r5 item 5 through the C++ ingest: a cluster past one 64-bit mask (a unique hostname
+    label per node, > 64 NoSchedule/NoExecute taints) is refused by ks_cluster_parse and, with its
+    pods noted (ks_cluster_parse_ex + ks_cluster_note_pod + ks_cluster_seal), decides every
+    (pod, node) exactly as the literal string predicates (tests/pysim.py)."""
+    from harness import cluster_yaml, pod_strings
+    from pysim import PySim
+    tr = tracegen.wide_trace(n_nodes=800, n_pods=90, seed=0x91, host_sel_permille=80)
+    text = cluster_yaml(tr)
+    with pytest.raises(KsError) as e:
+        Cluster(text)
+    assert e.value.code == _lib.KS_ERANGE
+    ps = pod_strings(tr)
+    c = Cluster(text, pods=ps)
+    assert c.n == 800
+    ref = PySim(tr)
+    ref.submit(tr)
+    for j, (tols, pairs) in enumerate(ps):
+        tol, sel = c.tolerations(tols), c.selector(pairs)
+        for n in range(c.n):
+            assert ((int(c.taint[n]) & ~tol) == 0) == ref._taint_ok(n, ref.pods[j]), (j, n)
+            assert ((int(c.label[n]) & sel) == sel) == ref._selector_ok(n, ref.pods[j]), (j, n)
+
+
+def test_two_phase_seal_refuses_unseen_pods():
+    """A sealed wide cluster refuses (KS_ERANGE) a pod it did not see when that pod would make the
+    compact masks inexact: tolerations splitting a taint class, or a selector on a node label pair
+    no noted pod referenced.  Pairs no node carries still encode as infeasible (bit 63)."""
+    from harness import cluster_yaml, pod_strings
+    tr = tracegen.wide_trace(n_nodes=800, n_pods=40, seed=0x92, host_sel_permille=0)
+    c = Cluster(cluster_yaml(tr), pods=pod_strings(tr))
+    with pytest.raises(KsError) as e:
+        c.selector([("kubernetes.io/hostname", "node-0000007")])
+    assert e.value.code == _lib.KS_ERANGE
+    assert c.selector([("kubernetes.io/hostname", "no-such-node")]) == 1 << 63
+    with pytest.raises(KsError) as e:   # taint.wide/k20 is tolerated by no noted pod's key
+        c.tolerations([("taint.wide/k20", "Equal", "w0", "")])
+    assert e.value.code == _lib.KS_ERANGE
+    assert c.tolerations([("", "Exists", "", "")]) != 0
+
+
+def test_two_phase_seal_of_a_narrow_cluster_is_the_plain_encoding():
+    """A cluster within one mask seals to exactly what ks_cluster_parse gives, pods noted or not."""
+    from harness import cluster_yaml, pod_strings
+    tr = tracegen.c3_trace(n_nodes=300, n_pods=200)
+    text = cluster_yaml(tr)
+    a, b = Cluster(text), Cluster(text, pods=pod_strings(tr))
+    np.testing.assert_array_equal(a.taint, b.taint)
+    np.testing.assert_array_equal(a.label, b.label)
+    np.testing.assert_array_equal(a.alloc, b.alloc)
